@@ -1,0 +1,97 @@
+"""ctypes binding of libcyclonus_hip.so (include/cyclonus_hip.h).
+
+The product path is the HIP library; there is no CPU fallback.  If the shared library is
+missing or fails to load, every entry point raises instead of silently computing on the host.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(_PKG, "libcyclonus_hip.so")
+
+# cyc_status
+OK, ERR_ARG, ERR_JSON, ERR_INVALID_POLICY, ERR_PANIC_IP, ERR_PANIC_CIDR, ERR_PANIC_SELECTOR = 0, 1, 2, 3, 4, 5, 6
+ERR_DUPLICATE_KEY, ERR_HIP, ERR_OOM, ERR_RCCL = 7, 8, 9, 10
+PANIC_CODES = (ERR_INVALID_POLICY, ERR_PANIC_IP, ERR_PANIC_CIDR, ERR_PANIC_SELECTOR)
+
+# cyc_job_status
+JOB_NONE, JOB_VALID, JOB_BAD_NAMED_PORT, JOB_BAD_PORT_PROTOCOL = 0, 1, 2, 3
+
+EXPORTS = [
+    "cyc_ctx_create",
+    "cyc_ctx_destroy",
+    "cyc_last_error",
+    "cyc_version",
+    "cyc_policy_build_json",
+    "cyc_policy_load_ir_json",
+    "cyc_policy_ir_json",
+    "cyc_resources_load_json",
+    "cyc_probe_prepare",
+    "cyc_probe_run",
+    "cyc_probe_run_host",
+    "cyc_last_timings",
+    "cyc_query_traffic",
+]
+
+
+class CyclonusError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[cyc_status {code}] {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class CyclonusPanic(CyclonusError):
+    """The Go reference would panic (or log.Fatalf) on this input; msg is the panic text."""
+
+
+class ProbeShape(ctypes.Structure):
+    _fields_ = [
+        (n, ctypes.c_int64)
+        for n in ("pods", "slots", "words", "configs", "targets_in", "targets_eg", "peers", "classes_in", "classes_eg", "may_panic")
+    ]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """Load libcyclonus_hip.so (raises if it is missing: no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO_PATH):
+            raise ImportError(f"{SO_PATH} is missing: run `python -m cyclonus_amd.build` (hipcc, gfx950)")
+        L = ctypes.CDLL(SO_PATH)
+        vp, cp, sz, i, i64 = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int64
+        L.cyc_ctx_create.argtypes = [i, ctypes.POINTER(vp)]
+        L.cyc_ctx_destroy.argtypes = [vp]
+        L.cyc_ctx_destroy.restype = None
+        L.cyc_last_error.argtypes = [vp]
+        L.cyc_last_error.restype = cp
+        L.cyc_version.restype = cp
+        L.cyc_policy_build_json.argtypes = [vp, i, cp, sz]
+        L.cyc_policy_load_ir_json.argtypes = [vp, cp, sz]
+        L.cyc_policy_ir_json.argtypes = [vp, cp, sz]
+        L.cyc_policy_ir_json.restype = i64
+        L.cyc_resources_load_json.argtypes = [vp, cp, sz]
+        L.cyc_probe_prepare.argtypes = [vp, cp, sz, ctypes.POINTER(ProbeShape)]
+        L.cyc_probe_run.argtypes = [vp, vp, vp, vp, vp, i64, i64]
+        L.cyc_probe_run_host.argtypes = [vp, vp, vp, vp, i64, i64]
+        L.cyc_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i]
+        L.cyc_query_traffic.argtypes = [vp, cp, sz, vp, i64]
+        _lib = L
+    return _lib
+
+
+def check(ctx, rc: int):
+    if rc == OK:
+        return
+    msg = lib().cyc_last_error(ctx).decode(errors="replace")
+    if rc in PANIC_CODES or rc == ERR_DUPLICATE_KEY:
+        raise CyclonusPanic(rc, msg)
+    raise CyclonusError(rc, msg)

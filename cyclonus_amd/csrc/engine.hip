@@ -1,0 +1,1114 @@
+// engine.hip — CDNA4 (gfx950) verdict engine for cyclonus's simulated-connectivity path.
+//
+// What the reference does per cell (pkg/connectivity/probe/jobrunner.go:68-94 ->
+// pkg/matcher/policy.go:131-174): for the ingress direction, walk EVERY ingress target, keep the
+// ones whose namespace equals the destination's and whose pod selector matches its labels
+// (TargetsApplyingToPod :68-82); the cell is allowed iff no target matched, or some matched
+// target's ordered peer list (target.go:29-36) allows the source on the job's port; same for
+// egress with source and destination swapped.
+//
+// What this engine does instead (exact rewriting, no per-cell walk):
+//   k_selectors     every (selector, label set) pair once            -> SELRES u8 [S][L]
+//   k_peer_rows     every pod/IP peer over all pods as packed bits    -> PM / ER [R][W] u64
+//                   (ER = the peer would panic for that pod: bad CIDR/IP/operator)
+//   k_portok        every (port matcher, job descriptor)              -> PORTOK u8 [M][D]
+//   k_slot_words    per (slot, 64-pod word): valid bits, desc masks   -> VALID, DESCW, DM
+//   k_member        per pod IDENTITY (ns, labels[, job descriptors]): matching targets,
+//                   a 64-bit hash, and a device hash table that elects one representative
+//                   identity per distinct target set                  -> classes
+//   k_class_rows    per class representative, slot, word: OR over its targets of the ordered
+//                   peer walk done 64 pods at a time with bit ops     -> A_in / A_eg rows
+//   k_emit          per target pod: copy its class rows into the output planes (HBM-bound;
+//                   the roofline kernel)
+//   k_first_error / k_error_detail   only when the inputs can panic: first panicking job in
+//                   the reference's job order and the panic message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "cyclonus_hip.h"
+#include "host.hpp"
+
+namespace cyc {
+
+// ----------------------------------------------------------------------------- device helpers
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Evaluate selector `sel` on label set `ls`: 0 no match, 1 match, 2 panic (invalid operator).
+// labelselector.go:66-86: matchLabels first (all must hold), then expressions in order.
+__device__ uint8_t eval_selector(const uint32_t* __restrict__ sel_off, const DReq* __restrict__ reqs,
+                                 const uint32_t* __restrict__ req_vals, const uint32_t* __restrict__ ls_off,
+                                 const uint32_t* __restrict__ ls_key, const uint32_t* __restrict__ ls_val,
+                                 uint32_t sel, uint32_t ls) {
+  uint32_t r0 = sel_off[sel], r1 = sel_off[sel + 1];
+  uint32_t l0 = ls_off[ls], l1 = ls_off[ls + 1];
+  for (uint32_t r = r0; r < r1; r++) {
+    DReq q = reqs[r];
+    if (q.op == REQ_INVALID) return 2;
+    // binary search the key in the (sorted) label set
+    uint32_t lo = l0, hi = l1;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (ls_key[mid] < q.key) lo = mid + 1;
+      else hi = mid;
+    }
+    bool present = lo < l1 && ls_key[lo] == q.key;
+    uint32_t v = present ? ls_val[lo] : 0xFFFFFFFFu;
+    bool ok;
+    switch (q.op) {
+      case REQ_EQ: ok = present && v == req_vals[q.voff]; break;
+      case REQ_EQ_EMPTY: ok = !present || v == req_vals[q.voff]; break;
+      case REQ_IN:
+      case REQ_NOTIN: {
+        bool in = false;
+        for (uint32_t i = 0; i < q.vcnt; i++) in |= (req_vals[q.voff + i] == v);
+        ok = present && (q.op == REQ_IN ? in : !in);
+        break;
+      }
+      case REQ_EXISTS: ok = present; break;
+      default: ok = !present; break;  // REQ_DNE
+    }
+    if (!ok) return 0;
+  }
+  return 1;
+}
+
+__global__ void k_selectors(uint32_t S, uint32_t L, const uint32_t* sel_off, const DReq* reqs, const uint32_t* req_vals,
+                            const uint32_t* ls_off, const uint32_t* ls_key, const uint32_t* ls_val,
+                            uint8_t* __restrict__ selres) {
+  uint64_t n = uint64_t(S) * L;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    uint32_t s = uint32_t(i / L), l = uint32_t(i % L);
+    selres[i] = eval_selector(sel_off, reqs, req_vals, ls_off, ls_key, ls_val, s, l);
+  }
+}
+
+// IPNet.Contains after To4 collapse (ipaddress.go:10-20): families must agree.
+__device__ __forceinline__ bool cidr_contains(const DCidr& c, const DIP& ip) {
+  if (c.fam != ip.fam) return false;
+  if (c.fam == 4) return ((c.net[3] ^ ip.w[3]) & c.mask[3]) == 0;
+  return (((c.net[0] ^ ip.w[0]) & c.mask[0]) | ((c.net[1] ^ ip.w[1]) & c.mask[1]) |
+          ((c.net[2] ^ ip.w[2]) & c.mask[2]) | ((c.net[3] ^ ip.w[3]) & c.mask[3])) == 0;
+}
+
+// Outcome of one pod/IP peer for peer pod q: 0 no, 1 match (before the port check), 2 panic.
+// podpeermatcher.go:21-28 (ns matcher, then pod matcher); ippeermatcher.go:43-50 ->
+// ipaddress.go:22-40 (CIDR parse, IP parse, contains, each except in order).
+struct PeerCtx {
+  const DPeer* peers;
+  const uint8_t* selres;
+  uint32_t L;
+  const uint32_t *pod_ns, *pod_ls, *pod_nsls;
+  const DIP* pod_ip;
+  const DCidr* cidrs;
+  const DIPBlock* ipbs;
+  const uint32_t* ipb_ex;
+};
+
+__device__ __forceinline__ uint32_t peer_outcome(const PeerCtx& c, const DPeer& pr, uint32_t q) {
+  if (pr.kind == 2) {
+    uint32_t ns = c.pod_ns[q];
+    if (pr.nskind == 0) {
+      if (ns != pr.nsval) return 0;
+    } else if (pr.nskind == 2) {
+      uint8_t r = c.selres[uint64_t(pr.nsval) * c.L + c.pod_nsls[q]];
+      if (r != 1) return r == 2 ? 2u : 0u;
+    }
+    if (pr.podsel == CYC_ALL) return 1;
+    uint8_t r = c.selres[uint64_t(pr.podsel) * c.L + c.pod_ls[q]];
+    return r;
+  }
+  // IP peer
+  DIPBlock b = c.ipbs[pr.ipb];
+  DCidr cd = c.cidrs[b.cidr];
+  if (!cd.valid) return 2;
+  DIP ip = c.pod_ip[q];
+  if (!ip.valid) return 2;
+  if (!cidr_contains(cd, ip)) return 0;
+  for (uint32_t e = 0; e < b.excnt; e++) {
+    DCidr x = c.cidrs[c.ipb_ex[b.exoff + e]];
+    if (!x.valid) return 2;
+    if (cidr_contains(x, ip)) return 0;
+  }
+  return 1;
+}
+
+// One block per (peer, chunk of 64 words); one wave per word, one lane per pod, ballot -> word.
+constexpr int ROWS_WORDS_PER_BLOCK = 64;
+__global__ __launch_bounds__(256) void k_peer_rows(PeerCtx c, uint32_t P, uint32_t W, uint64_t* __restrict__ PM,
+                                                   uint64_t* __restrict__ ER) {
+  uint32_t chunks = (W + ROWS_WORDS_PER_BLOCK - 1) / ROWS_WORDS_PER_BLOCK;
+  uint32_t r = blockIdx.x / chunks;
+  DPeer pr = c.peers[r];
+  if (pr.kind < 2) return;
+  uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t w0 = (blockIdx.x % chunks) * ROWS_WORDS_PER_BLOCK;
+  for (uint32_t w = w0 + wave; w < min(W, w0 + ROWS_WORDS_PER_BLOCK); w += 4) {
+    uint32_t q = w * 64 + lane;
+    uint32_t o = q < P ? peer_outcome(c, pr, q) : 0u;
+    uint64_t m = __ballot(o == 1);
+    uint64_t e = __ballot(o == 2);
+    if (lane == 0) {
+      PM[uint64_t(r) * W + w] = m;
+      ER[uint64_t(r) * W + w] = e;
+    }
+  }
+}
+
+// PortMatcher.Allows(ResolvedPort, ResolvedPortName, Protocol) — portmatcher.go:10-92, 190-199.
+__global__ void k_portok(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents, const DDesc* descs,
+                         uint8_t* __restrict__ portok) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * D) return;
+  uint32_t m = i / D, e = i % D;
+  DPortM pm = pms[m];
+  DDesc d = descs[e];
+  uint8_t ok = pm.all ? 1 : 0;
+  for (uint32_t j = 0; j < pm.ecnt && !ok; j++) {
+    DPortEntry pe = pents[pm.eoff + j];
+    if (pe.proto != d.proto) continue;  // raw protocol string compare ("tcp" != "TCP")
+    switch (pe.kind) {
+      case PE_PROTO: ok = 1; break;
+      case PE_INT: ok = pe.a == d.port; break;
+      case PE_NAME: ok = uint32_t(pe.a) == d.name; break;
+      default: ok = pe.a <= d.port && d.port <= pe.b; break;
+    }
+  }
+  portok[i] = ok;
+}
+
+// Per (slot k, word w over pods-as-destinations): VALID bits, the word's common descriptor
+// (DESCW >= 0), none valid (-2) or mixed (-1), and per-descriptor masks DM for mixed words.
+__global__ __launch_bounds__(256) void k_slot_words(uint32_t P, uint32_t K, uint32_t W, uint32_t D,
+                                                    const int32_t* __restrict__ slot_desc,
+                                                    const uint8_t* __restrict__ slot_status, uint64_t* __restrict__ VALID,
+                                                    int32_t* __restrict__ DESCW, uint64_t* __restrict__ DM) {
+  uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t idx = blockIdx.x * 4 + wave;  // (k, w)
+  if (idx >= K * W) return;
+  uint32_t k = idx / W, w = idx % W;
+  uint32_t q = w * 64 + lane;
+  int32_t e = -1;
+  bool valid = false;
+  if (q < P) {
+    valid = slot_status[uint64_t(q) * K + k] == CYC_JOB_VALID;
+    e = valid ? slot_desc[uint64_t(q) * K + k] : -1;
+  }
+  uint64_t vm = __ballot(valid);
+  // first valid lane's descriptor, broadcast
+  int32_t first = -2;
+  if (vm) first = __shfl(e, __ffsll((unsigned long long)vm) - 1);
+  bool same = !valid || e == first;
+  uint64_t sm = __ballot(same);
+  int32_t dw = vm == 0 ? -2 : (sm == ~0ull ? first : -1);
+  if (lane == 0) {
+    VALID[uint64_t(k) * W + w] = vm;
+    DESCW[uint64_t(k) * W + w] = dw;
+  }
+  if (dw == -1) {
+    for (uint32_t d = 0; d < D; d++) {
+      uint64_t m = __ballot(valid && e == int32_t(d));
+      if (lane == 0) DM[(uint64_t(k) * D + d) * W + w] = m;
+    }
+  }
+}
+
+// Target membership per pod identity (TargetsApplyingToPod policy.go:68-82 over the identity's
+// namespace's targets), class hash, and election of a representative per distinct class.
+struct MemberArgs {
+  uint32_t n_ident, L, K;
+  const uint32_t *id_ns, *id_ls;
+  const int32_t* id_desc;     // ingress: [n_ident][K] descriptor (-1 invalid); egress: null
+  const uint8_t* id_status;   // ingress: [n_ident][K]
+  const uint32_t *tns_lo, *tns_hi;
+  const DTarget* tgt;
+  const uint8_t* selres;
+  const uint32_t* list_off;   // host-computed upper-bound offsets
+  uint32_t* list;             // matching target ids (ascending = primary-key order)
+  uint32_t* cnt;
+  uint64_t* hash;
+  uint8_t* err;               // a target selector panics on this identity
+  unsigned long long* ht_key; // hash table (capacity ht_cap, power of two), 0 = empty
+  uint32_t* ht_rep;           // min identity per key
+  uint32_t ht_cap;
+};
+
+__device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* keys, uint32_t cap, uint64_t h) {
+  uint32_t s = uint32_t(h) & (cap - 1);
+  for (uint32_t probe = 0; probe < cap; probe++) {
+    unsigned long long old = atomicCAS(&keys[s], 0ull, (unsigned long long)h);
+    if (old == 0ull || old == h) return s;
+    s = (s + 1) & (cap - 1);
+  }
+  return 0xFFFFFFFFu;  // unreachable: cap >= 2 * n_ident
+}
+
+__device__ __forceinline__ uint32_t ht_find(const unsigned long long* keys, uint32_t cap, uint64_t h) {
+  uint32_t s = uint32_t(h) & (cap - 1);
+  for (uint32_t probe = 0; probe < cap; probe++) {
+    unsigned long long k = keys[s];
+    if (k == h) return s;
+    if (k == 0ull) return 0xFFFFFFFFu;
+    s = (s + 1) & (cap - 1);
+  }
+  return 0xFFFFFFFFu;
+}
+
+__global__ void k_member(MemberArgs a) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_ident) return;
+  uint32_t ns = a.id_ns[i], ls = a.id_ls[i];
+  uint32_t lo = a.tns_lo[ns], hi = a.tns_hi[ns];
+  uint32_t n = 0, off = a.list_off[i];
+  uint8_t e = 0;
+  uint64_t h = 0x5bd1e9955bd1e995ull;
+  for (uint32_t t = lo; t < hi; t++) {
+    uint8_t r = a.selres[uint64_t(a.tgt[t].sel) * a.L + ls];
+    if (r == 2) e = 1;
+    if (r == 1) {
+      a.list[off + n++] = t;
+      h = mix64(h ^ (uint64_t(t) + 1));
+    }
+  }
+  if (a.id_desc) {
+    for (uint32_t k = 0; k < a.K; k++) {
+      uint64_t st = a.id_status[uint64_t(i) * a.K + k];
+      int32_t d = st == CYC_JOB_VALID ? a.id_desc[uint64_t(i) * a.K + k] : -1;
+      h = mix64(h ^ ((st << 40) | uint32_t(d + 1)) ^ (uint64_t(k) << 48));
+    }
+  }
+  h |= 1ull;  // never the empty key
+  a.cnt[i] = n;
+  a.hash[i] = h;
+  a.err[i] = e;
+  if (!e) {
+    uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
+    atomicMin(&a.ht_rep[s], i);
+  }
+}
+
+__global__ void k_classify(MemberArgs a, uint32_t* __restrict__ class_of) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_ident) return;
+  uint32_t c = i;
+  if (!a.err[i]) {
+    uint32_t s = ht_find(a.ht_key, a.ht_cap, a.hash[i]);
+    uint32_t r = s == 0xFFFFFFFFu ? i : a.ht_rep[s];
+    if (r != i) {  // verify (a 64-bit hash collision must never merge distinct classes)
+      bool eq = a.cnt[r] == a.cnt[i];
+      for (uint32_t j = 0; eq && j < a.cnt[i]; j++) eq = a.list[a.list_off[r] + j] == a.list[a.list_off[i] + j];
+      if (eq && a.id_desc) {
+        for (uint32_t k = 0; eq && k < a.K; k++) {
+          uint8_t si = a.id_status[uint64_t(i) * a.K + k], sr = a.id_status[uint64_t(r) * a.K + k];
+          eq = si == sr && (si != CYC_JOB_VALID || a.id_desc[uint64_t(i) * a.K + k] == a.id_desc[uint64_t(r) * a.K + k]);
+        }
+      }
+      c = eq ? r : i;
+    }
+  }
+  class_of[i] = c;
+}
+
+// Ordered peer walk of one target over 64 peer pods at once (target.go:29-36 short-circuit;
+// a panicking peer stops the walk with a panic, ippeermatcher.go:46-48).
+struct WalkCtx {
+  const DTarget* tgt;
+  const DPeer* peers;
+  const uint64_t *PM, *ER;
+  const uint8_t* portok;
+  uint32_t W, D;
+};
+
+template <bool EGRESS>
+__device__ __forceinline__ void walk_target(const WalkCtx& c, uint32_t t, uint32_t w, int32_t desc_uniform,
+                                            const uint64_t* __restrict__ dm_kw /* DM + k*D*W + w */, uint64_t& allow,
+                                            uint64_t& err) {
+  DTarget tg = c.tgt[t];
+  uint64_t decided = 0;
+  for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
+    DPeer pr = c.peers[j];
+    if (pr.kind == 0) {  // AllPeersMatcher
+      allow |= ~decided;
+      return;
+    }
+    uint64_t okm;
+    if (!EGRESS || desc_uniform >= 0) {
+      okm = c.portok[uint64_t(pr.port) * c.D + uint32_t(desc_uniform)] ? ~0ull : 0ull;
+    } else if (desc_uniform == -2) {
+      okm = 0;
+    } else {  // mixed descriptors in this destination word
+      okm = 0;
+      for (uint32_t d = 0; d < c.D; d++)
+        if (c.portok[uint64_t(pr.port) * c.D + d]) okm |= dm_kw[uint64_t(d) * c.W];
+    }
+    if (pr.kind == 1) {  // PortsForAllPeersMatcher
+      uint64_t a = okm & ~decided;
+      allow |= a;
+      decided |= a;
+    } else {
+      uint64_t pm = c.PM[uint64_t(j) * c.W + w], er = c.ER[uint64_t(j) * c.W + w];
+      uint64_t ne = er & ~decided;
+      uint64_t na = pm & okm & ~decided;
+      err |= ne;
+      allow |= na;
+      decided |= ne | na;
+    }
+    if (decided == ~0ull) return;
+  }
+}
+
+struct RowArgs {
+  WalkCtx wc;
+  uint32_t n_ident, K, W, P;
+  const uint32_t* class_of;
+  const uint32_t *cnt, *list_off, *list;
+  const uint8_t* id_err;
+  const int32_t* id_desc;    // ingress only
+  const uint8_t* id_status;  // ingress only
+  const uint64_t* VALID;     // egress only [K][W]
+  const int32_t* DESCW;      // egress only
+  const uint64_t* DM;        // egress only [K][D][W]
+  uint64_t* A;               // [n_ident][K][W]
+  uint64_t* AE;              // [n_ident][K][W] or null
+};
+
+// One block = (identity, slot) x 256 words.  Only class representatives do work.
+template <bool EGRESS>
+__global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
+  uint32_t chunks = (a.W + 255) / 256;
+  uint32_t i = blockIdx.x / (chunks * a.K);
+  uint32_t k = (blockIdx.x / chunks) % a.K;
+  if (a.class_of[i] != i || a.id_err[i]) return;
+  uint32_t w = (blockIdx.x % chunks) * blockDim.x + threadIdx.x;
+  if (w >= a.W) return;
+  uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
+  uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
+  uint64_t allow = 0, err = 0;
+  uint64_t valid;
+  int32_t du;
+  const uint64_t* dm_kw = nullptr;
+  if (EGRESS) {
+    valid = a.VALID[uint64_t(k) * a.W + w];
+    du = a.DESCW[uint64_t(k) * a.W + w];
+    dm_kw = a.DM + uint64_t(k) * a.wc.D * a.W + w;
+  } else {
+    uint8_t st = a.id_status[uint64_t(i) * a.K + k];
+    valid = st == CYC_JOB_VALID ? wmask : 0ull;
+    du = a.id_desc[uint64_t(i) * a.K + k];
+  }
+  if (valid) {
+    uint32_t n = a.cnt[i];
+    if (n == 0) {
+      allow = ~0ull;  // no target applies: allowed (policy.go:158-160)
+    } else {
+      const uint32_t* lst = a.list + a.list_off[i];
+      for (uint32_t j = 0; j < n; j++) walk_target<EGRESS>(a.wc, lst[j], w, du, dm_kw, allow, err);
+    }
+  }
+  uint64_t idx = (uint64_t(i) * a.K + k) * a.W + w;
+  a.A[idx] = allow & valid;
+  if (a.AE) a.AE[idx] = err & valid;
+}
+
+// The HBM-bound kernel: every target pod's plane rows are a copy of its class rows.
+// One block per pod (class-clustered order), 16-byte stores when the row pitch allows.
+struct EmitArgs {
+  uint32_t n_rows;            // pods in [row_lo, row_hi)
+  uint32_t row_lo;
+  const uint32_t* order;      // pods in [row_lo,row_hi) clustered by class, or null
+  const uint32_t *pod_iid, *pod_eid, *class_in, *class_eg;
+  const uint64_t *A_in, *A_eg;
+  uint64_t *out_in, *out_eg;
+  uint64_t row_words;         // K * W
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
+  uint32_t b = blockIdx.x;
+  if (b >= a.n_rows) return;
+  uint32_t p = a.order ? a.order[b] : a.row_lo + b;
+  uint64_t orow = uint64_t(p - a.row_lo) * a.row_words;
+  const uint64_t* src_in = a.A_in + uint64_t(a.class_in[a.pod_iid[p]]) * a.row_words;
+  const uint64_t* src_eg = a.A_eg + uint64_t(a.class_eg[a.pod_eid[p]]) * a.row_words;
+  uint64_t* dst_in = a.out_in + orow;
+  uint64_t* dst_eg = a.out_eg + orow;
+  if (VEC) {
+    uint64_t n2 = a.row_words / 2;
+    const ulonglong2* si = reinterpret_cast<const ulonglong2*>(src_in);
+    const ulonglong2* se = reinterpret_cast<const ulonglong2*>(src_eg);
+    ulonglong2* di = reinterpret_cast<ulonglong2*>(dst_in);
+    ulonglong2* de = reinterpret_cast<ulonglong2*>(dst_eg);
+    for (uint64_t x = threadIdx.x; x < n2; x += blockDim.x) {
+      ulonglong2 v0 = si[x];
+      ulonglong2 v1 = se[x];
+      __builtin_nontemporal_store(v0.x, &di[x].x);
+      __builtin_nontemporal_store(v0.y, &di[x].y);
+      __builtin_nontemporal_store(v1.x, &de[x].x);
+      __builtin_nontemporal_store(v1.y, &de[x].y);
+    }
+  } else {
+    for (uint64_t x = threadIdx.x; x < a.row_words; x += blockDim.x) {
+      dst_in[x] = src_in[x];
+      dst_eg[x] = src_eg[x];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- panic path (rare)
+struct ErrArgs {
+  uint32_t P, K, W, n_cfg;
+  uint32_t row_lo, row_hi;
+  const uint8_t* slot_status;  // [P][K]
+  const uint32_t *slot_cfg, *slot_idx;
+  const uint32_t *pod_iid, *pod_eid, *class_in, *class_eg;
+  const uint8_t *err_in, *err_eg;  // per identity: a target selector panics
+  const uint64_t *AE_in, *AE_eg;
+  unsigned long long* first;       // min job-order key
+};
+
+// key = ((cfg*P + s)*P + d)*65536 + idx_in_cfg : the reference's job order (resources.go:286-333)
+__global__ __launch_bounds__(256) void k_first_error(ErrArgs a) {
+  uint32_t chunks = (a.P + 255) / 256;
+  uint32_t s = blockIdx.x / chunks;
+  uint32_t d = (blockIdx.x % chunks) * blockDim.x + threadIdx.x;
+  if (d >= a.P) return;
+  bool s_err = a.err_eg[a.pod_eid[s]];
+  bool d_err = a.err_in[a.pod_iid[d]];
+  uint32_t ci = a.class_in[a.pod_iid[d]], ce = a.class_eg[a.pod_eid[s]];
+  unsigned long long best = ~0ull;
+  for (uint32_t k = 0; k < a.K; k++) {
+    if (a.slot_status[uint64_t(d) * a.K + k] != CYC_JOB_VALID) continue;
+    bool e = d_err || s_err;
+    if (!e && a.AE_in) e = (a.AE_in[(uint64_t(ci) * a.K + k) * a.W + s / 64] >> (s % 64)) & 1;
+    if (!e && a.AE_eg) e = (a.AE_eg[(uint64_t(ce) * a.K + k) * a.W + d / 64] >> (d % 64)) & 1;
+    if (e) {
+      unsigned long long key = ((uint64_t(a.slot_cfg[k]) * a.P + s) * a.P + d) * 65536ull + a.slot_idx[k];
+      best = key < best ? key : best;
+    }
+  }
+  if (best != ~0ull) atomicMin(a.first, best);
+}
+
+}  // namespace cyc
+
+// ============================================================================ context + C ABI
+using namespace cyc;
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) throw HipErr{std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+namespace {
+struct HipErr {
+  std::string msg;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  void alloc(size_t n) {
+    if (p) {
+      (void)hipFree(p);
+      p = nullptr;
+    }
+    bytes = n;
+    if (n) HIPCHK(hipMalloc(&p, n));
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+template <class T>
+void upload(DevBuf& b, const std::vector<T>& v) {
+  b.alloc(std::max<size_t>(v.size() * sizeof(T), 16));
+  if (!v.empty()) HIPCHK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+
+struct Identities {  // pod identities for one direction
+  std::vector<uint32_t> ns, ls, list_off;
+  std::vector<int32_t> desc;     // ingress: [n][K]
+  std::vector<uint8_t> status;   // ingress: [n][K]
+  std::vector<uint32_t> of_pod;  // [P]
+  uint64_t list_total = 0;
+  uint32_t ht_cap = 0;
+};
+
+struct DirDev {
+  DevBuf id_ns, id_ls, id_desc, id_status, list_off, list, cnt, hash, err, ht_key, ht_rep, class_of, A, AE, tns_lo,
+      tns_hi, tgt, pod_id;
+  uint32_t n = 0, ht_cap = 0;
+};
+}  // namespace
+
+struct cyc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool have_policy = false, have_res = false, prepared = false;
+  PolicyIR policy;
+  Resources res;
+  Problem pb;
+  Identities ids[2];
+  // device tables
+  DevBuf ls_off, ls_key, ls_val, sel_off, reqs, req_vals, pod_ns, pod_ls, pod_nsls, pod_ip, cidrs, ipbs, ipb_ex, pms,
+      pents, peers, descs, slot_desc, slot_status, slot_cfg, slot_idx;
+  DevBuf selres, PM, ER, portok, VALID, DESCW, DM, first_err, order;
+  DirDev dir[2];
+  int64_t order_lo = -1, order_hi = -1;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double last_ms[3] = {0, 0, 0};
+  bool timed = false;
+};
+
+int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t idx);
+
+static int fail(cyc_ctx* c, int code, const std::string& m) {
+  if (c) c->err = m;
+  return code;
+}
+
+template <class F>
+static int guarded(cyc_ctx* c, F&& f) {
+  try {
+    return f();
+  } catch (Panic& p) {
+    return fail(c, p.code, p.msg);
+  } catch (HipErr& h) {
+    return fail(c, CYC_ERR_HIP, h.msg);
+  } catch (std::bad_alloc&) {
+    return fail(c, CYC_ERR_OOM, "host allocation failed");
+  } catch (std::exception& e) {
+    return fail(c, CYC_ERR_JSON, e.what());
+  }
+}
+
+static void build_identities(cyc_ctx* c) {
+  Problem& pb = c->pb;
+  for (int d = 0; d < 2; d++) {
+    Identities& I = c->ids[d];
+    I = Identities{};
+    std::unordered_map<std::string, uint32_t> map;
+    I.of_pod.resize(pb.P);
+    std::string key;
+    for (uint32_t p = 0; p < pb.P; p++) {
+      key.assign(reinterpret_cast<const char*>(&pb.pod_ns[p]), 4);
+      key.append(reinterpret_cast<const char*>(&pb.pod_ls[p]), 4);
+      if (d == 0 && pb.K) {  // ingress identity includes the pod's job descriptors
+        key.append(reinterpret_cast<const char*>(&pb.slot_desc[size_t(p) * pb.K]), 4 * pb.K);
+        key.append(reinterpret_cast<const char*>(&pb.slot_status[size_t(p) * pb.K]), pb.K);
+      }
+      auto it = map.find(key);
+      if (it == map.end()) {
+        uint32_t id = uint32_t(I.ns.size());
+        I.ns.push_back(pb.pod_ns[p]);
+        I.ls.push_back(pb.pod_ls[p]);
+        if (d == 0)
+          for (uint32_t k = 0; k < pb.K; k++) {
+            I.desc.push_back(pb.slot_desc[size_t(p) * pb.K + k]);
+            I.status.push_back(pb.slot_status[size_t(p) * pb.K + k]);
+          }
+        it = map.emplace(key, id).first;
+      }
+      I.of_pod[p] = it->second;
+    }
+    I.list_off.resize(I.ns.size());
+    uint64_t tot = 0;
+    for (size_t i = 0; i < I.ns.size(); i++) {
+      I.list_off[i] = uint32_t(tot);
+      tot += pb.tns_hi[d][I.ns[i]] - pb.tns_lo[d][I.ns[i]];
+      if (tot > 0xFFFFFFFFull) throw Panic{CYC_ERR_OOM, "membership lists exceed 2^32 entries"};
+    }
+    I.list_total = tot;
+    uint32_t cap = 2;
+    while (cap < 2 * I.ns.size()) cap <<= 1;
+    I.ht_cap = cap;
+  }
+}
+
+static void prepare_device(cyc_ctx* c) {
+  Problem& pb = c->pb;
+  upload(c->ls_off, pb.ls_off);
+  upload(c->ls_key, pb.ls_key);
+  upload(c->ls_val, pb.ls_val);
+  upload(c->sel_off, pb.sel_off);
+  upload(c->reqs, pb.reqs);
+  upload(c->req_vals, pb.req_vals);
+  upload(c->pod_ns, pb.pod_ns);
+  upload(c->pod_ls, pb.pod_ls);
+  upload(c->pod_nsls, pb.pod_nsls);
+  upload(c->pod_ip, pb.pod_ip);
+  upload(c->cidrs, pb.cidrs);
+  upload(c->ipbs, pb.ipbs);
+  upload(c->ipb_ex, pb.ipb_ex);
+  upload(c->pms, pb.pms);
+  upload(c->pents, pb.pents);
+  upload(c->peers, pb.peers);
+  upload(c->descs, pb.descs);
+  upload(c->slot_desc, pb.slot_desc);
+  upload(c->slot_status, pb.slot_status);
+  upload(c->slot_cfg, pb.slot_cfg);
+  upload(c->slot_idx, pb.slot_idx);
+  uint64_t R = pb.peers.size(), W = pb.W, D = std::max<size_t>(pb.descs.size(), 1), K = pb.K;
+  c->selres.alloc(std::max<uint64_t>(uint64_t(pb.S) * pb.L, 16));
+  c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
+  c->ER.alloc(std::max<uint64_t>(R * W * 8, 16));
+  c->portok.alloc(std::max<uint64_t>(pb.pms.size() * D, 16));
+  c->VALID.alloc(std::max<uint64_t>(K * W * 8, 16));
+  c->DESCW.alloc(std::max<uint64_t>(K * W * 4, 16));
+  c->DM.alloc(std::max<uint64_t>(K * D * W * 8, 16));
+  c->first_err.alloc(16);
+  for (int d = 0; d < 2; d++) {
+    Identities& I = c->ids[d];
+    DirDev& dd = c->dir[d];
+    dd.n = uint32_t(I.ns.size());
+    dd.ht_cap = I.ht_cap;
+    upload(dd.id_ns, I.ns);
+    upload(dd.id_ls, I.ls);
+    upload(dd.id_desc, I.desc);
+    upload(dd.id_status, I.status);
+    upload(dd.list_off, I.list_off);
+    upload(dd.tns_lo, pb.tns_lo[d]);
+    upload(dd.tns_hi, pb.tns_hi[d]);
+    upload(dd.tgt, pb.tgt[d]);
+    upload(dd.pod_id, I.of_pod);
+    dd.list.alloc(std::max<uint64_t>(I.list_total * 4, 16));
+    dd.cnt.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
+    dd.hash.alloc(std::max<uint64_t>(dd.n * 8ull, 16));
+    dd.err.alloc(std::max<uint64_t>(dd.n, 16));
+    dd.ht_key.alloc(uint64_t(dd.ht_cap) * 8);
+    dd.ht_rep.alloc(uint64_t(dd.ht_cap) * 4);
+    dd.class_of.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
+    dd.A.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
+    if (pb.may_err) dd.AE.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
+    else dd.AE.alloc(0);
+  }
+  c->order_lo = c->order_hi = -1;
+}
+
+static unsigned grid1(uint64_t n, unsigned block) { return unsigned(std::min<uint64_t>((n + block - 1) / block, 1u << 20)); }
+
+static MemberArgs member_args(cyc_ctx* c, int d) {
+  Problem& pb = c->pb;
+  DirDev& dd = c->dir[d];
+  MemberArgs a{};
+  a.n_ident = dd.n;
+  a.L = pb.L;
+  a.K = pb.K;
+  a.id_ns = dd.id_ns.as<uint32_t>();
+  a.id_ls = dd.id_ls.as<uint32_t>();
+  a.id_desc = d == 0 ? dd.id_desc.as<int32_t>() : nullptr;
+  a.id_status = d == 0 ? dd.id_status.as<uint8_t>() : nullptr;
+  a.tns_lo = dd.tns_lo.as<uint32_t>();
+  a.tns_hi = dd.tns_hi.as<uint32_t>();
+  a.tgt = dd.tgt.as<DTarget>();
+  a.selres = c->selres.as<uint8_t>();
+  a.list_off = dd.list_off.as<uint32_t>();
+  a.list = dd.list.as<uint32_t>();
+  a.cnt = dd.cnt.as<uint32_t>();
+  a.hash = dd.hash.as<uint64_t>();
+  a.err = dd.err.as<uint8_t>();
+  a.ht_key = dd.ht_key.as<unsigned long long>();
+  a.ht_rep = dd.ht_rep.as<uint32_t>();
+  a.ht_cap = dd.ht_cap;
+  return a;
+}
+
+// Rows [lo,hi) ordered so pods sharing class rows are adjacent (L2 / Infinity-Cache reuse).
+static void ensure_order(cyc_ctx* c, int64_t lo, int64_t hi) {
+  if (c->order_lo == lo && c->order_hi == hi) return;
+  std::vector<uint32_t> ord(size_t(hi - lo));
+  std::iota(ord.begin(), ord.end(), uint32_t(lo));
+  const auto& iin = c->ids[0].of_pod;
+  const auto& ieg = c->ids[1].of_pod;
+  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+    return iin[x] != iin[y] ? iin[x] < iin[y] : ieg[x] < ieg[y];
+  });
+  upload(c->order, ord);
+  c->order_lo = lo;
+  c->order_hi = hi;
+}
+
+static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
+                        int64_t hi) {
+  Problem& pb = c->pb;
+  const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
+  const uint32_t R = uint32_t(pb.peers.size()), M = uint32_t(pb.pms.size());
+  if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
+  ensure_order(c, lo, hi);
+  HIPCHK(hipEventRecord(c->ev[0], st));
+
+  // 1. selectors x label sets
+  if (uint64_t(pb.S) * pb.L)
+    k_selectors<<<grid1(uint64_t(pb.S) * pb.L, 256), 256, 0, st>>>(
+        pb.S, pb.L, c->sel_off.as<uint32_t>(), c->reqs.as<DReq>(), c->req_vals.as<uint32_t>(), c->ls_off.as<uint32_t>(),
+        c->ls_key.as<uint32_t>(), c->ls_val.as<uint32_t>(), c->selres.as<uint8_t>());
+  // 2. peer rows
+  PeerCtx pc{c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, c->pod_ns.as<uint32_t>(), c->pod_ls.as<uint32_t>(),
+             c->pod_nsls.as<uint32_t>(), c->pod_ip.as<DIP>(), c->cidrs.as<DCidr>(), c->ipbs.as<DIPBlock>(),
+             c->ipb_ex.as<uint32_t>()};
+  if (R && W) {
+    uint64_t g = uint64_t((W + ROWS_WORDS_PER_BLOCK - 1) / ROWS_WORDS_PER_BLOCK) * R;
+    k_peer_rows<<<unsigned(g), 256, 0, st>>>(pc, P, W, c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
+  }
+  // 3. port matchers x job descriptors
+  if (M && pb.descs.size())
+    k_portok<<<grid1(uint64_t(M) * D, 256), 256, 0, st>>>(M, D, c->pms.as<DPortM>(), c->pents.as<DPortEntry>(),
+                                                          c->descs.as<DDesc>(), c->portok.as<uint8_t>());
+  // 4. per-slot destination words
+  if (uint64_t(K) * W)
+    k_slot_words<<<unsigned((uint64_t(K) * W + 3) / 4), 256, 0, st>>>(
+        P, K, W, D, c->slot_desc.as<int32_t>(), c->slot_status.as<uint8_t>(), c->VALID.as<uint64_t>(),
+        c->DESCW.as<int32_t>(), c->DM.as<uint64_t>());
+  // 5. membership + classes per direction
+  for (int d = 0; d < 2; d++) {
+    DirDev& dd = c->dir[d];
+    if (!dd.n) continue;
+    HIPCHK(hipMemsetAsync(dd.ht_key.p, 0, dd.ht_key.bytes, st));
+    HIPCHK(hipMemsetAsync(dd.ht_rep.p, 0xFF, dd.ht_rep.bytes, st));
+    MemberArgs ma = member_args(c, d);
+    k_member<<<grid1(dd.n, 128), 128, 0, st>>>(ma);
+    k_classify<<<grid1(dd.n, 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
+  }
+  HIPCHK(hipEventRecord(c->ev[1], st));
+  // 6. class rows
+  WalkCtx wc{nullptr, c->peers.as<DPeer>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), c->portok.as<uint8_t>(), W, D};
+  for (int d = 0; d < 2; d++) {
+    DirDev& dd = c->dir[d];
+    if (!dd.n || !K || !W) continue;
+    RowArgs ra{};
+    ra.wc = wc;
+    ra.wc.tgt = dd.tgt.as<DTarget>();
+    ra.n_ident = dd.n;
+    ra.K = K;
+    ra.W = W;
+    ra.P = P;
+    ra.class_of = dd.class_of.as<uint32_t>();
+    ra.cnt = dd.cnt.as<uint32_t>();
+    ra.list_off = dd.list_off.as<uint32_t>();
+    ra.list = dd.list.as<uint32_t>();
+    ra.id_err = dd.err.as<uint8_t>();
+    ra.id_desc = dd.id_desc.as<int32_t>();
+    ra.id_status = dd.id_status.as<uint8_t>();
+    ra.VALID = c->VALID.as<uint64_t>();
+    ra.DESCW = c->DESCW.as<int32_t>();
+    ra.DM = c->DM.as<uint64_t>();
+    ra.A = dd.A.as<uint64_t>();
+    ra.AE = pb.may_err ? dd.AE.as<uint64_t>() : nullptr;
+    unsigned g = unsigned(uint64_t((W + 255) / 256) * dd.n * K);
+    if (d == 0) k_class_rows<false><<<g, 256, 0, st>>>(ra);
+    else k_class_rows<true><<<g, 256, 0, st>>>(ra);
+  }
+  HIPCHK(hipEventRecord(c->ev[2], st));
+  // 7. emit
+  if (hi > lo && K && W) {
+    EmitArgs ea{};
+    ea.n_rows = uint32_t(hi - lo);
+    ea.row_lo = uint32_t(lo);
+    ea.order = c->order.as<uint32_t>();
+    ea.pod_iid = c->dir[0].pod_id.as<uint32_t>();
+    ea.pod_eid = c->dir[1].pod_id.as<uint32_t>();
+    ea.class_in = c->dir[0].class_of.as<uint32_t>();
+    ea.class_eg = c->dir[1].class_of.as<uint32_t>();
+    ea.A_in = c->dir[0].A.as<uint64_t>();
+    ea.A_eg = c->dir[1].A.as<uint64_t>();
+    ea.out_in = d_in;
+    ea.out_eg = d_eg;
+    ea.row_words = uint64_t(K) * W;
+    bool vec = (ea.row_words % 2 == 0) && (reinterpret_cast<uintptr_t>(d_in) % 16 == 0) &&
+               (reinterpret_cast<uintptr_t>(d_eg) % 16 == 0);
+    if (vec) k_emit<true><<<ea.n_rows, 256, 0, st>>>(ea);
+    else k_emit<false><<<ea.n_rows, 256, 0, st>>>(ea);
+  }
+  HIPCHK(hipEventRecord(c->ev[3], st));
+  if (d_status && uint64_t(P) * K)
+    HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(P) * K, hipMemcpyDeviceToDevice, st));
+  c->timed = true;
+
+  // 8. panic path: the first panicking job in job order, as the reference would hit it
+  if (pb.may_err) {
+    HIPCHK(hipMemsetAsync(c->first_err.p, 0xFF, 8, st));
+    ErrArgs e{};
+    e.P = P;
+    e.K = K;
+    e.W = W;
+    e.n_cfg = pb.n_cfg;
+    e.slot_status = c->slot_status.as<uint8_t>();
+    e.slot_cfg = c->slot_cfg.as<uint32_t>();
+    e.slot_idx = c->slot_idx.as<uint32_t>();
+    e.pod_iid = c->dir[0].pod_id.as<uint32_t>();
+    e.pod_eid = c->dir[1].pod_id.as<uint32_t>();
+    e.class_in = c->dir[0].class_of.as<uint32_t>();
+    e.class_eg = c->dir[1].class_of.as<uint32_t>();
+    e.err_in = c->dir[0].err.as<uint8_t>();
+    e.err_eg = c->dir[1].err.as<uint8_t>();
+    e.AE_in = c->dir[0].n ? c->dir[0].AE.as<uint64_t>() : nullptr;
+    e.AE_eg = c->dir[1].n ? c->dir[1].AE.as<uint64_t>() : nullptr;
+    e.first = c->first_err.as<unsigned long long>();
+    if (P && K) k_first_error<<<unsigned(uint64_t((P + 255) / 256) * P), 256, 0, st>>>(e);
+    unsigned long long first = ~0ull;
+    HIPCHK(hipMemcpyAsync(&first, c->first_err.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (first != ~0ull) {
+      uint32_t idx = uint32_t(first % 65536);
+      uint64_t rest = first / 65536;
+      uint32_t d = uint32_t(rest % P), s = uint32_t((rest / P) % P), cfg = uint32_t(rest / P / P);
+      // duplicate-key fatal of an EARLIER config's table wins (tables are built per config)
+      for (uint32_t cc = 0; cc < cfg; cc++)
+        if (!pb.dup_key_msg[cc].empty()) return fail(c, CYC_ERR_DUPLICATE_KEY, pb.dup_key_msg[cc]);
+      return describe_panic(c, s, d, cfg, idx);
+    }
+  }
+  for (uint32_t cc = 0; cc < pb.n_cfg; cc++)
+    if (!pb.dup_key_msg[cc].empty()) return fail(c, CYC_ERR_DUPLICATE_KEY, pb.dup_key_msg[cc]);
+  return (int)CYC_OK;
+}
+
+// Host-side formatting of the panic message for the identified first panicking job.  The
+// device found WHICH job panics; this re-derives the reference's message text for it by
+// replaying that single job's evaluation order over the compiled tables (error path only).
+int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t idx) {
+  Problem& pb = c->pb;
+  uint32_t k = 0;
+  for (uint32_t kk = 0; kk < pb.K; kk++)
+    if (pb.slot_cfg[kk] == cfg && pb.slot_idx[kk] == idx) k = kk;
+  std::vector<uint8_t> selres(size_t(pb.S) * pb.L);
+  HIPCHK(hipMemcpy(selres.data(), c->selres.p, selres.size(), hipMemcpyDeviceToHost));
+  auto sel = [&](uint32_t sid, uint32_t ls) { return selres[size_t(sid) * pb.L + ls]; };
+  auto ip_err = [&](const DPeer& pr, uint32_t q, std::string& msg) -> int {
+    const DIPBlock& b = pb.ipbs[pr.ipb];
+    auto cidr_msg = [&](uint32_t id) {
+      return "unable to parse CIDR '" + pb.cidr_str[id] + "': invalid CIDR address: " + pb.cidr_str[id];
+    };
+    if (!pb.cidrs[b.cidr].valid) {
+      msg = cidr_msg(b.cidr);
+      return CYC_ERR_PANIC_CIDR;
+    }
+    if (!pb.pod_ip[q].valid) {
+      msg = "unable to parse IP '" + pb.pod_ip_str[q] + "'";
+      return CYC_ERR_PANIC_IP;
+    }
+    for (uint32_t e = 0; e < b.excnt; e++) {
+      uint32_t x = pb.ipb_ex[b.exoff + e];
+      if (!pb.cidrs[x].valid) {
+        msg = cidr_msg(x);
+        return CYC_ERR_PANIC_CIDR;
+      }
+    }
+    return 0;
+  };
+  // direction 0 (ingress): target d, peer s; direction 1 (egress): target s, peer d
+  for (int dir = 0; dir < 2; dir++) {
+    uint32_t tp = dir == 0 ? d : s, peer = dir == 0 ? s : d;
+    uint32_t ns = pb.pod_ns[tp], ls = pb.pod_ls[tp];
+    uint32_t lo = pb.tns_lo[dir][ns], hi = pb.tns_hi[dir][ns];
+    for (uint32_t t = lo; t < hi; t++)
+      if (sel(pb.tgt[dir][t].sel, ls) == 2) return fail(c, CYC_ERR_PANIC_SELECTOR, "invalid operator");
+    // copy of the device outcome rows for the peer pod's word
+    for (uint32_t t = lo; t < hi; t++) {
+      if (sel(pb.tgt[dir][t].sel, ls) != 1) continue;
+      const DTarget& tg = pb.tgt[dir][t];
+      for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
+        const DPeer& pr = pb.peers[j];
+        if (pr.kind == 0) break;
+        int32_t de = pb.slot_desc[size_t(d) * pb.K + k];
+        std::vector<uint8_t> ok(1);
+        HIPCHK(hipMemcpy(ok.data(), c->portok.as<uint8_t>() + size_t(pr.port) * std::max<size_t>(pb.descs.size(), 1) + de, 1,
+                         hipMemcpyDeviceToHost));
+        if (pr.kind == 1) {
+          if (ok[0]) break;
+          continue;
+        }
+        uint64_t pm, er;
+        HIPCHK(hipMemcpy(&pm, c->PM.as<uint64_t>() + size_t(j) * pb.W + peer / 64, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&er, c->ER.as<uint64_t>() + size_t(j) * pb.W + peer / 64, 8, hipMemcpyDeviceToHost));
+        if ((er >> (peer % 64)) & 1) {
+          if (pr.kind == 2) return fail(c, CYC_ERR_PANIC_SELECTOR, "invalid operator");
+          std::string msg;
+          int code = ip_err(pr, peer, msg);
+          return fail(c, code ? code : CYC_ERR_PANIC_CIDR, msg);
+        }
+        if (((pm >> (peer % 64)) & 1) && ok[0]) break;
+      }
+    }
+  }
+  return fail(c, CYC_ERR_PANIC_CIDR, "panic (unresolved message)");
+}
+
+static void destroy_events(cyc_ctx* c) {
+  for (auto& e : c->ev)
+    if (e) {
+      (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+}
+
+extern "C" {
+
+const char* cyc_version(void) { return "cyclonus_hip 0.1 (gfx950)"; }
+
+int cyc_ctx_create(int device_id, cyc_ctx** out) {
+  if (!out) return CYC_ERR_ARG;
+  // No HIP call here: policy compilation / IR export work on a host without a GPU; the device
+  // is initialised by the first call that needs it (cyc_probe_prepare).
+  auto* c = new cyc_ctx();
+  c->device = device_id;
+  *out = c;
+  return (int)CYC_OK;
+}
+
+void cyc_ctx_destroy(cyc_ctx* c) {
+  if (!c) return;
+  if (c->stream) {
+    (void)hipSetDevice(c->device);
+    destroy_events(c);
+    (void)hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+const char* cyc_last_error(const cyc_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int cyc_policy_build_json(cyc_ctx* c, int simplify, const char* js, size_t len) {
+  if (!c || !js) return CYC_ERR_ARG;
+  return guarded(c, [&] {
+    json::Node n = json::parse(js, len);
+    c->policy = build_network_policies(n, simplify != 0);
+    c->have_policy = true;
+    c->prepared = false;
+    return (int)CYC_OK;
+  });
+}
+
+int cyc_policy_load_ir_json(cyc_ctx* c, const char* js, size_t len) {
+  if (!c || !js) return CYC_ERR_ARG;
+  return guarded(c, [&] {
+    c->policy = load_policy_ir(json::parse(js, len));
+    c->have_policy = true;
+    c->prepared = false;
+    return (int)CYC_OK;
+  });
+}
+
+int64_t cyc_policy_ir_json(cyc_ctx* c, char* buf, size_t cap) {
+  if (!c || !c->have_policy) return -1;
+  std::string s = dump_policy_ir(c->policy);
+  if (buf && cap > s.size()) {
+    memcpy(buf, s.data(), s.size());
+    buf[s.size()] = 0;
+  }
+  return int64_t(s.size()) + 1;
+}
+
+int cyc_resources_load_json(cyc_ctx* c, const char* js, size_t len) {
+  if (!c || !js) return CYC_ERR_ARG;
+  return guarded(c, [&] {
+    c->res = load_resources(json::parse(js, len));
+    c->have_res = true;
+    c->prepared = false;
+    return (int)CYC_OK;
+  });
+}
+
+int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* shape) {
+  if (!c || !js) return CYC_ERR_ARG;
+  if (!c->have_policy || !c->have_res) return fail(c, CYC_ERR_ARG, "load a policy and resources first");
+  return guarded(c, [&] {
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->stream) {
+      HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+    }
+    auto probes = load_probes(json::parse(js, len));
+    c->pb = build_problem(c->policy, c->res, probes);
+    build_identities(c);
+    prepare_device(c);
+    c->prepared = true;
+    if (shape) {
+      shape->pods = c->pb.P;
+      shape->slots = c->pb.K;
+      shape->words = c->pb.W;
+      shape->configs = c->pb.n_cfg;
+      shape->targets_in = int64_t(c->pb.tgt[0].size());
+      shape->targets_eg = int64_t(c->pb.tgt[1].size());
+      shape->peers = int64_t(c->pb.peers.size());
+      shape->classes_in = c->dir[0].n;
+      shape->classes_eg = c->dir[1].n;
+      shape->may_panic = c->pb.may_err ? 1 : 0;
+    }
+    return (int)CYC_OK;
+  });
+}
+
+int cyc_probe_run(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo, int64_t hi) {
+  if (!c) return CYC_ERR_ARG;
+  if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
+  if ((!d_in || !d_eg) && hi > lo) return fail(c, CYC_ERR_ARG, "null output plane");
+  return guarded(c, [&] {
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    return run_pipeline(c, st, d_in, d_eg, d_status, lo, hi);
+  });
+}
+
+int cyc_probe_run_host(cyc_ctx* c, uint64_t* h_in, uint64_t* h_eg, uint8_t* h_status, int64_t lo, int64_t hi) {
+  if (!c) return CYC_ERR_ARG;
+  if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
+  return guarded(c, [&] {
+    HIPCHK(hipSetDevice(c->device));
+    uint64_t rows = uint64_t(std::max<int64_t>(hi - lo, 0));
+    uint64_t words = rows * c->pb.K * c->pb.W;
+    DevBuf din, deg, dst;
+    din.alloc(std::max<uint64_t>(words * 8, 16));
+    deg.alloc(std::max<uint64_t>(words * 8, 16));
+    dst.alloc(std::max<uint64_t>(uint64_t(c->pb.P) * c->pb.K, 16));
+    int rc = run_pipeline(c, c->stream, din.as<uint64_t>(), deg.as<uint64_t>(), dst.as<uint8_t>(), lo, hi);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (rc != CYC_OK) return rc;
+    if (h_in && words) HIPCHK(hipMemcpy(h_in, din.p, words * 8, hipMemcpyDeviceToHost));
+    if (h_eg && words) HIPCHK(hipMemcpy(h_eg, deg.p, words * 8, hipMemcpyDeviceToHost));
+    if (h_status && uint64_t(c->pb.P) * c->pb.K)
+      HIPCHK(hipMemcpy(h_status, dst.p, uint64_t(c->pb.P) * c->pb.K, hipMemcpyDeviceToHost));
+    return (int)CYC_OK;
+  });
+}
+
+int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
+  if (!c || !ms) return CYC_ERR_ARG;
+  if (!c->timed) return fail(c, CYC_ERR_ARG, "no run yet");
+  return guarded(c, [&] {
+    HIPCHK(hipEventSynchronize(c->ev[3]));
+    float a = 0, b = 0, r = 0;
+    HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[3]));
+    HIPCHK(hipEventElapsedTime(&b, c->ev[2], c->ev[3]));
+    HIPCHK(hipEventElapsedTime(&r, c->ev[1], c->ev[2]));
+    double v[3] = {a, b, r};
+    for (int i = 0; i < n && i < 3; i++) ms[i] = v[i];
+    return (int)CYC_OK;
+  });
+}
+
+int cyc_query_traffic(cyc_ctx* c, const char*, size_t, uint8_t*, int64_t) {
+  return fail(c, CYC_ERR_ARG, "cyc_query_traffic: not implemented yet");
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+"""Engine: one libcyclonus_hip context on one GPU (thin wrapper over include/cyclonus_hip.h)."""
+from __future__ import annotations
+
+import ctypes
+import json
+from typing import Any, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _bytes(doc: Any) -> bytes:
+    if isinstance(doc, bytes):
+        return doc
+    if isinstance(doc, str):
+        return doc.encode()
+    return json.dumps(doc, separators=(",", ":")).encode()
+
+
+class Engine:
+    """A verdict-engine context bound to `device` (HIP device ordinal)."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = ctypes.c_void_p()
+        rc = lib().cyc_ctx_create(int(device), ctypes.byref(self._ctx))
+        if rc != _lib.OK:
+            raise _lib.CyclonusError(rc, f"cyc_ctx_create(device={device}) failed")
+        self.device = device
+        self.shape: Optional[dict] = None
+
+    def close(self):
+        if self._ctx:
+            lib().cyc_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- inputs
+    def build_policies(self, netpols, simplify: bool = True) -> "Engine":
+        b = _bytes(netpols)
+        check(self._ctx, lib().cyc_policy_build_json(self._ctx, int(bool(simplify)), b, len(b)))
+        return self
+
+    def load_policy_ir(self, policy_ir) -> "Engine":
+        b = _bytes(policy_ir)
+        check(self._ctx, lib().cyc_policy_load_ir_json(self._ctx, b, len(b)))
+        return self
+
+    def policy_ir(self) -> dict:
+        n = lib().cyc_policy_ir_json(self._ctx, None, 0)
+        if n < 0:
+            raise _lib.CyclonusError(_lib.ERR_ARG, "no policy loaded")
+        buf = ctypes.create_string_buffer(int(n))
+        lib().cyc_policy_ir_json(self._ctx, buf, int(n))
+        return json.loads(buf.value.decode())
+
+    def load_resources(self, resources) -> "Engine":
+        b = _bytes(resources)
+        check(self._ctx, lib().cyc_resources_load_json(self._ctx, b, len(b)))
+        return self
+
+    def prepare(self, probes) -> dict:
+        b = _bytes(probes)
+        sh = _lib.ProbeShape()
+        check(self._ctx, lib().cyc_probe_prepare(self._ctx, b, len(b), ctypes.byref(sh)))
+        self.shape = sh.as_dict()
+        return self.shape
+
+    # ---------------------------------------------------------------- runs
+    def run_host(self, row_lo: int = 0, row_hi: Optional[int] = None):
+        """Run on the GPU and copy back: (status[P,K] u8, ingress[R,K,W] u64, egress[R,K,W] u64)."""
+        P, K, W = self.shape["pods"], self.shape["slots"], self.shape["words"]
+        hi = P if row_hi is None else row_hi
+        rows = max(hi - row_lo, 0)
+        ing = np.zeros((rows, K, W), np.uint64)
+        eg = np.zeros((rows, K, W), np.uint64)
+        st = np.zeros((P, K), np.uint8)
+        check(
+            self._ctx,
+            lib().cyc_probe_run_host(self._ctx, ing.ctypes.data, eg.ctypes.data, st.ctypes.data, int(row_lo), int(hi)),
+        )
+        return st, ing, eg
+
+    def run_device(self, d_ingress: int, d_egress: int, d_status: int, stream: int = 0, row_lo: int = 0, row_hi=None):
+        """Enqueue the pipeline on `stream` writing device pointers (e.g. torch .data_ptr())."""
+        P = self.shape["pods"]
+        hi = P if row_hi is None else row_hi
+        check(
+            self._ctx,
+            lib().cyc_probe_run(
+                self._ctx, ctypes.c_void_p(stream or None), ctypes.c_void_p(d_ingress), ctypes.c_void_p(d_egress),
+                ctypes.c_void_p(d_status or None), int(row_lo), int(hi),
+            ),
+        )
+
+    def timings(self):
+        """(pipeline_ms, emit_ms, class_rows_ms) of the last run, from HIP events on its stream."""
+        ms = (ctypes.c_double * 3)()
+        check(self._ctx, lib().cyc_last_timings(self._ctx, ms, 3))
+        return tuple(ms)

@@ -1,0 +1,118 @@
+/* cyclonus_hip.h — C ABI of libcyclonus_hip.so, the MI355X (gfx950) NetworkPolicy verdict engine.
+ *
+ * Drop-in boundary for the simulated-connectivity path of cyclonus (reference paths are
+ * relative to the reference repository, github.com/mattfenwick/cyclonus @ johnSchnake fork):
+ *
+ *   cyc_policy_build_json   replaces matcher.BuildNetworkPolicies(simplify, netpols)
+ *                           pkg/matcher/builder.go:11-26 (+ Policy.Simplify policy.go:176-183)
+ *   cyc_policy_load_ir_json accepts json.Marshal(*matcher.Policy) — the already-built Go policy
+ *                           a cgo binding holds in SimulatedJobRunner.Policies (jobrunner.go:64-66)
+ *   cyc_resources_load_json probe.Resources (pkg/connectivity/probe/resources.go:15-19) as JSON
+ *   cyc_probe_prepare       Resources.GetJobsForProbeConfig (resources.go:274-364) for a batch of
+ *                           generator.ProbeConfig values (PortProtocol | AllAvailable)
+ *   cyc_probe_run           Runner.RunProbeForConfig (jobrunner.go:29-58) -> SimulatedJobRunner.RunJobs
+ *                           (jobrunner.go:68-94) -> Policy.IsTrafficAllowed (policy.go:131-174) for
+ *                           every (src pod, dst pod, job) cell, as packed bit-planes
+ *   cyc_query_traffic       Policy.IsTrafficAllowed for arbitrary matcher.Traffic values, including
+ *                           external peers (analyze.go:209-225 query-traffic)
+ *
+ * Conventions: every function returns a cyc_status; on failure cyc_last_error(ctx) holds the
+ * message (for CYC_ERR_PANIC_* it is the text of the Go panic the reference would raise).
+ * Inputs are copied during the call (no caller pointer is retained, cgo-safe).  A context is
+ * not internally locked: use one per thread.  Plane layout (W = ceil(P/64) 64-bit words):
+ *   status[d*K + k]                      cyc_job_status of destination pod d, job slot k
+ *   ingress[((d-row_lo)*K + k)*W + s/64]  bit s%64: ingress verdict of s -> d, slot k
+ *   egress [((s-row_lo)*K + k)*W + d/64]  bit d%64: egress verdict of s -> d, slot k
+ * i.e. each plane is keyed by the pod the direction's policies TARGET (ingress: destination,
+ * egress: source; policy.go:143-149).  Combined = ingress AND egress (policy.go:123-125).
+ * Bits of non-VALID slots are 0; their Ingress/Egress/Combined follow jobrunner.go:36-55.
+ */
+#ifndef CYCLONUS_HIP_H
+#define CYCLONUS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  CYC_OK = 0,
+  CYC_ERR_ARG = 1,             /* bad argument / call order */
+  CYC_ERR_JSON = 2,            /* malformed input document */
+  CYC_ERR_INVALID_POLICY = 3,  /* builder.go:39,174-181 panics */
+  CYC_ERR_PANIC_IP = 4,        /* ippeermatcher.go:46-48 panic: unparsable pod IP */
+  CYC_ERR_PANIC_CIDR = 5,      /* ippeermatcher.go:46-48 panic: unparsable CIDR / except */
+  CYC_ERR_PANIC_SELECTOR = 6,  /* labelselector.go:57 panic("invalid operator") */
+  CYC_ERR_DUPLICATE_KEY = 7,   /* table.go:45 via utils.DoOrDie (log.Fatalf) */
+  CYC_ERR_HIP = 8,
+  CYC_ERR_OOM = 9,
+  CYC_ERR_RCCL = 10
+} cyc_status;
+
+typedef enum {
+  CYC_JOB_NONE = 0,               /* no job in this slot (AllAvailable, fewer containers) */
+  CYC_JOB_VALID = 1,              /* Ingress/Egress from the planes */
+  CYC_JOB_BAD_NAMED_PORT = 2,     /* Ingress=invalidnamedport, Egress=unknown (jobrunner.go:47-55) */
+  CYC_JOB_BAD_PORT_PROTOCOL = 3   /* Ingress=invalidportprotocol, Egress=unknown (:36-45) */
+} cyc_job_status;
+
+typedef struct cyc_ctx cyc_ctx;
+
+typedef struct {
+  int64_t pods;        /* P */
+  int64_t slots;       /* K: job slots per destination pod over all probe configs */
+  int64_t words;       /* W = ceil(P/64) */
+  int64_t configs;     /* number of probe configs */
+  int64_t targets_in;  /* ingress targets after merge/simplify */
+  int64_t targets_eg;
+  int64_t peers;
+  int64_t classes_in;  /* filled after cyc_probe_run */
+  int64_t classes_eg;
+  int64_t may_panic;   /* 1 if evaluation can reach a Go panic (invalid CIDR/IP/operator) */
+} cyc_probe_shape;
+
+/* context / errors */
+int cyc_ctx_create(int device_id, cyc_ctx** out);
+void cyc_ctx_destroy(cyc_ctx* ctx);
+const char* cyc_last_error(const cyc_ctx* ctx);
+const char* cyc_version(void);
+
+/* policy compile: JSON array (or List / single object) of networking.k8s.io/v1 NetworkPolicy */
+int cyc_policy_build_json(cyc_ctx* ctx, int simplify, const char* netpols_json, size_t len);
+/* policy load: json.Marshal(*matcher.Policy) produced by the Go reference */
+int cyc_policy_load_ir_json(cyc_ctx* ctx, const char* policy_json, size_t len);
+/* export the compiled policy as json.Marshal(*matcher.Policy) would; returns bytes needed (+1) */
+int64_t cyc_policy_ir_json(cyc_ctx* ctx, char* buf, size_t cap);
+
+/* probe model: probe.Resources JSON ({"Namespaces": {...}, "Pods": [...]}) */
+int cyc_resources_load_json(cyc_ctx* ctx, const char* resources_json, size_t len);
+
+/* probe configs: JSON array of {"Port": <int|string>, "Protocol": "TCP"} or {"AllAvailable": true};
+ * flattens + uploads all tables and allocates device scratch.  Fills *shape. */
+int cyc_probe_prepare(cyc_ctx* ctx, const char* probes_json, size_t len, cyc_probe_shape* shape);
+
+/* Compute the verdict planes on the GPU for target-pod rows [row_lo, row_hi) (rows are pods in
+ * Resources.Pods order; pass 0, P for the whole table).  Device pointers; stream may be NULL
+ * (the context's stream).  Asynchronous unless the inputs can panic (then it synchronises to
+ * report the first panicking job in job order, as the reference would). */
+int cyc_probe_run(cyc_ctx* ctx, void* hip_stream, uint64_t* d_ingress, uint64_t* d_egress, uint8_t* d_status,
+                  int64_t row_lo, int64_t row_hi);
+
+/* Same, into host buffers (allocates + copies; synchronous). */
+int cyc_probe_run_host(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_t* status, int64_t row_lo,
+                       int64_t row_hi);
+
+/* Average device time (ms) of the last run's kernels, measured with HIP events on the launch
+ * stream: [0] whole pipeline, [1] emit kernel (the HBM-roofline kernel), [2] class rows. */
+int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
+
+/* Single-cell API (policy.go:131-174): traffic_json is a JSON array of matcher.Traffic objects;
+ * out[i] = ingress | egress << 1 (allowed bits).  Needs only a loaded policy. */
+int cyc_query_traffic(cyc_ctx* ctx, const char* traffic_json, size_t len, uint8_t* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CYCLONUS_HIP_H */

@@ -1,0 +1,122 @@
+"""GPU parity: libcyclonus_hip (through the C ABI) vs the per-cell CPU oracle, bit-exact.
+
+Every comparison is on the full truth table: status[d,k], ingress plane[d,k,s] and egress
+plane[s,k,d]; Go panics must be reported with the reference's message for the first
+panicking job in the reference's job order.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from cyclonus_amd._lib import CyclonusPanic
+from cyclonus_amd.engine import Engine
+from oracle.oracle import Oracle, OraclePanic, combined_table
+from randgen import random_problem
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+pytestmark = pytest.mark.gpu
+
+
+def run_both(pols, res, probes, simplify=True, engine=None):
+    try:
+        o = Oracle(pols, res, simplify).probe(probes)
+    except OraclePanic as e:
+        o = ("panic", str(e))
+    eng = engine or Engine(0)
+    try:
+        eng.build_policies(pols, simplify).load_resources(res)
+        eng.prepare(probes)
+        g = eng.run_host()
+    except CyclonusPanic as e:
+        g = ("panic", e.msg)
+    return o, g
+
+
+def assert_same(o, g, ctx=""):
+    if isinstance(o, tuple) or isinstance(g, tuple) and g[0] == "panic":
+        assert isinstance(o, tuple) and isinstance(g, tuple) and g[0] == "panic", f"{ctx}: oracle={o!r:.200} gpu={g!r:.200}"
+        assert o[1] == g[1], f"{ctx}: panic message differs: oracle={o[1]!r} gpu={g[1]!r}"
+        return
+    for name, a, b in zip(("status", "ingress", "egress"), o, g):
+        assert a.shape == b.shape, f"{ctx}: {name} shape {a.shape} vs {b.shape}"
+        if not np.array_equal(a, b):
+            idx = np.argwhere(a != b)[:5]
+            pytest.fail(f"{ctx}: {name} differs at {idx.tolist()} ({int((a != b).sum())} words)")
+
+
+def test_config1_readme(gpu):
+    c = json.load(open(os.path.join(GOLD, "config1.json")))
+    o, g = run_both(c["policies"], c["resources"], c["probes"])
+    assert_same(o, g, "config1")
+    status, inp, egp = g
+    ing, eg = combined_table(status, inp, egp)
+    names = [p["Namespace"] + "/" + p["Name"] for p in c["resources"]["Pods"]]
+    exp = c["readme_combined_tcp80"]["rows"]
+    for s, fr in enumerate(names):
+        for d, to in enumerate(names):
+            got = "." if (ing[s, d, 0] and eg[s, d, 0]) else "X"
+            assert got == exp[fr][to.upper()], (fr, to)
+
+
+@pytest.mark.parametrize("block", range(8))
+def test_random_parity(gpu, block):
+    eng = Engine(0)
+    for seed in range(block * 50, block * 50 + 50):
+        pols, res, probes = random_problem(seed)
+        o, g = run_both(pols, res, probes, simplify=(seed % 5 != 0), engine=eng)
+        assert_same(o, g, f"seed {seed}")
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_random_panics(gpu, block):
+    eng = Engine(0)
+    n_panics = 0
+    for seed in range(10_000 + block * 60, 10_000 + block * 60 + 60):
+        pols, res, probes = random_problem(seed, bad=True)
+        o, g = run_both(pols, res, probes, engine=eng)
+        n_panics += isinstance(o, tuple)
+        assert_same(o, g, f"bad seed {seed}")
+    assert n_panics > 0
+
+
+def test_larger_random(gpu):
+    eng = Engine(0)
+    for seed in range(5):
+        pols, res, probes = random_problem(50_000 + seed, n_pods=300, n_pols=60)
+        o, g = run_both(pols, res, probes, engine=eng)
+        assert_same(o, g, f"large seed {seed}")
+
+
+def test_row_ranges_and_device_path(gpu):
+    import torch
+
+    pols, res, probes = random_problem(777, n_pods=200, n_pols=30)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    sh = eng.prepare(probes)
+    st, ing, eg = eng.run_host()
+    P, K, W = sh["pods"], sh["slots"], sh["words"]
+    for lo, hi in [(0, 1), (3, 77), (100, 200), (199, 200), (50, 50)]:
+        st2, ing2, eg2 = eng.run_host(lo, hi)
+        assert np.array_equal(st, st2)
+        assert np.array_equal(ing[lo:hi], ing2) and np.array_equal(eg[lo:hi], eg2)
+    d_in = torch.zeros((P, K, W), dtype=torch.int64, device="cuda")
+    d_eg = torch.zeros((P, K, W), dtype=torch.int64, device="cuda")
+    d_st = torch.zeros((P, K), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_in.cpu().numpy().view(np.uint64), ing)
+    assert np.array_equal(d_eg.cpu().numpy().view(np.uint64), eg)
+    assert np.array_equal(d_st.cpu().numpy(), st)
+
+
+def test_reference_policy_fixtures(gpu):
+    c = json.load(open(os.path.join(GOLD, "config1.json")))
+    fx = json.load(open(os.path.join(GOLD, "policy_fixtures.json")))
+    probes = [{"AllAvailable": True}, {"Port": 80, "Protocol": "TCP"}, {"Port": 53, "Protocol": "UDP"},
+              {"Port": "serve-81-tcp", "Protocol": "TCP"}]
+    for name, pols in fx.items():
+        o, g = run_both(pols, c["resources"], probes)
+        assert_same(o, g, name)
