@@ -391,9 +391,15 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
   uint32_t chunks = (a.W + 255) / 256;
   uint32_t i = blockIdx.x / (chunks * a.K);
   uint32_t k = (blockIdx.x / chunks) % a.K;
-  if (a.class_of[i] != i || a.id_err[i]) return;
+  if (a.class_of[i] != i) return;
   uint32_t w = (blockIdx.x % chunks) * blockDim.x + threadIdx.x;
   if (w >= a.W) return;
+  if (a.id_err[i]) {  // membership panics: every VALID cell of this row panics (error path);
+    uint64_t idx = (uint64_t(i) * a.K + k) * a.W + w;  // the rest of the row is non-VALID => 0
+    a.A[idx] = 0;
+    if (a.AE) a.AE[idx] = 0;
+    return;
+  }
   uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
   uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
   uint64_t allow = 0, err = 0;

@@ -19,25 +19,33 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 pytestmark = pytest.mark.gpu
 
 
+class Panicked:
+    def __init__(self, msg):
+        self.msg = msg
+
+    def __repr__(self):
+        return f"Panicked({self.msg!r})"
+
+
 def run_both(pols, res, probes, simplify=True, engine=None):
     try:
         o = Oracle(pols, res, simplify).probe(probes)
     except OraclePanic as e:
-        o = ("panic", str(e))
+        o = Panicked(str(e))
     eng = engine or Engine(0)
     try:
         eng.build_policies(pols, simplify).load_resources(res)
         eng.prepare(probes)
         g = eng.run_host()
     except CyclonusPanic as e:
-        g = ("panic", e.msg)
+        g = Panicked(e.msg)
     return o, g
 
 
 def assert_same(o, g, ctx=""):
-    if isinstance(o, tuple) or isinstance(g, tuple) and g[0] == "panic":
-        assert isinstance(o, tuple) and isinstance(g, tuple) and g[0] == "panic", f"{ctx}: oracle={o!r:.200} gpu={g!r:.200}"
-        assert o[1] == g[1], f"{ctx}: panic message differs: oracle={o[1]!r} gpu={g[1]!r}"
+    if isinstance(o, Panicked) or isinstance(g, Panicked):
+        assert isinstance(o, Panicked) and isinstance(g, Panicked), f"{ctx}: oracle={o!r:.300} gpu={g!r:.300}"
+        assert o.msg == g.msg, f"{ctx}: panic message differs: oracle={o.msg!r} gpu={g.msg!r}"
         return
     for name, a, b in zip(("status", "ingress", "egress"), o, g):
         assert a.shape == b.shape, f"{ctx}: {name} shape {a.shape} vs {b.shape}"
@@ -76,7 +84,7 @@ def test_random_panics(gpu, block):
     for seed in range(10_000 + block * 60, 10_000 + block * 60 + 60):
         pols, res, probes = random_problem(seed, bad=True)
         o, g = run_both(pols, res, probes, engine=eng)
-        n_panics += isinstance(o, tuple)
+        n_panics += isinstance(o, Panicked)
         assert_same(o, g, f"bad seed {seed}")
     assert n_panics > 0
 
