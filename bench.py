@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Benchmark: simulated-connectivity verdict grid on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config config3]
+
+A step is one full pass of the hot path over the synthetic workload with every input table
+already resident in HBM: selector evaluation, peer rows, port tables, target membership and
+class election, class rows, and the emit of both packed verdict planes (ingress keyed by
+destination, egress keyed by source) for this rank's rows.  N > 1 shards target-pod rows across
+ranks (one process per GPU, torch.distributed over RCCL for the barrier / max-time reduce only;
+there is no collective on the data path).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "pod-pair×port verdicts/sec (node) at 100k pods×10k policies; HBM GB/s"
+
+
+def cpu_baseline(data, seconds: float, seed: int = 1):
+    """Time the per-cell CPU oracle (restated reference walk, 1 thread) on random cells."""
+    import numpy as np
+
+    from oracle.oracle import Oracle
+
+    t0 = time.perf_counter()
+    orc = Oracle(data["policies"], data["resources"], True)
+    build_s = time.perf_counter() - t0
+    P, K = orc.shape(data["probes"])
+    rng = np.random.default_rng(seed)
+    cells, elapsed, chunk = 0, 0.0, 64
+    while elapsed < seconds:
+        s = rng.integers(0, P, chunk)
+        d = rng.integers(0, P, chunk)
+        k = rng.integers(0, K, chunk)
+        t = time.perf_counter()
+        orc.cells(data["probes"], s, d, k)
+        elapsed += time.perf_counter() - t
+        cells += chunk
+        chunk = min(chunk * 2, 4096)
+    return {
+        "value": cells / elapsed,
+        "unit": "verdicts/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{cells} uniformly random (src, dst, slot) cells of {data['name']} through the oracle's per-cell "
+        f"IsTrafficAllowed walk (oracle/oracle.cpp), {elapsed:.1f} s of CPU time, 1 thread; policy build {build_s:.1f} s excluded",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from cyclonus_amd import synth
+    from cyclonus_amd.engine import Engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    data = synth.CONFIGS[args.config]()
+    eng = Engine(local)
+    eng.build_policies(json.dumps(data["policies"]))
+    eng.load_resources(json.dumps(data["resources"]))
+    shape = eng.prepare(data["probes"])
+    P, K, W = shape["pods"], shape["slots"], shape["words"]
+    lo, hi = rank * P // world, (rank + 1) * P // world
+    rows = hi - lo
+
+    d_in = torch.empty((max(rows, 1), K, W), dtype=torch.int64, device="cuda")
+    d_eg = torch.empty((max(rows, 1), K, W), dtype=torch.int64, device="cuda")
+    d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), stream, lo, hi)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # per-kernel device times from HIP events on the launch stream (separate, synchronised runs)
+    tm = []
+    for _ in range(5):
+        step()
+        tm.append(eng.timings())
+    tm = np.array(tm)
+    pipe_ms, emit_ms, rows_ms = (float(x) for x in tm.mean(axis=0))
+
+    status = d_st.cpu().numpy()
+    valid_slots = int((status == 1).sum())  # (dst, slot) pairs with a VALID job
+    cells = P * valid_slots  # every source pod x every valid (dst, slot) job
+    ms_per_step = dt / args.steps * 1e3
+    value = cells / (dt / args.steps)
+
+    emit_bytes = 2 * rows * K * W * 8  # both planes of this rank's rows, written once
+    achieved = emit_bytes / (emit_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "verdicts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (cyclonus_amd/synth.py, xoshiro256** seed 20250217)",
+            "config": {
+                "workload": f"{data['name']}: {data['description']} (AllAvailable probe)",
+                "pods": P,
+                "policies": len(data["policies"]),
+                "slots": K,
+                "cells": cells,
+                "targets_in": shape["targets_in"],
+                "targets_eg": shape["targets_eg"],
+                "peers": shape["peers"],
+                "identities_in": shape["classes_in"],
+                "identities_eg": shape["classes_eg"],
+                "parallelism": f"target-row shards x{world}",
+                "rows_per_rank": rows,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_emit",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "algorithmic_bytes_per_launch": emit_bytes,
+                "emit_ms": emit_ms,
+            },
+            "pipeline_ms": {"total": pipe_ms, "emit": emit_ms, "class_rows": rows_ms, "front": pipe_ms - emit_ms - rows_ms},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(data, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
