@@ -99,6 +99,9 @@ class Engine:
             ),
         )
 
+    def set_option(self, name: str, value: int):
+        check(self._ctx, lib().cyc_set_option(self._ctx, name.encode(), int(value)))
+
     def timings(self):
         """(pipeline_ms, emit_ms, class_rows_ms) of the last run, from HIP events on its stream."""
         ms = (ctypes.c_double * 3)()

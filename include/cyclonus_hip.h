@@ -108,6 +108,9 @@ int cyc_probe_run_host(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_
  * stream: [0] whole pipeline, [1] emit kernel (the HBM-roofline kernel), [2] class rows. */
 int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 
+/* Tuning knobs (no effect on results): "emit_variant" 0..3 selects the emit store pattern. */
+int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
+
 /* Single-cell API (policy.go:131-174): traffic_json is a JSON array of matcher.Traffic objects;
  * out[i] = ingress | egress << 1 (allowed bits).  Needs only a loaded policy. */
 int cyc_query_traffic(cyc_ctx* ctx, const char* traffic_json, size_t len, uint8_t* out, int64_t n);
