@@ -1278,7 +1278,7 @@ int cyc_probe_run(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg, uint
   if ((!d_in || !d_eg) && hi > lo) return fail(c, CYC_ERR_ARG, "null output plane");
   return guarded(c, [&] {
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the HIP default (null) stream
     return run_pipeline(c, st, d_in, d_eg, d_status, lo, hi);
   });
 }

@@ -578,6 +578,12 @@ PolicyIR load_policy_ir(const Node& root) {
       if (auto ns = tn.val("Namespace")) t.ns = ns->str();
       if (auto ps = tn.val("PodSelector")) t.sel = decode_selector(*ps);
       t.pk = target_pk(t.ns, t.sel);
+      if (auto sr = tn.val("SourceRules"); sr && sr->is_arr())
+        for (auto& r : sr->a) {
+          const Node* md = r.val("metadata");
+          const Node* nm = md ? md->val("name") : nullptr;
+          t.rules.push_back(nm ? nm->str() : std::string());
+        }
       if (auto peers = tn.val("Peers"); peers && peers->is_arr()) {
         t.peers_nil = false;
         for (auto& pn : peers->a) {

@@ -94,9 +94,10 @@ int cyc_resources_load_json(cyc_ctx* ctx, const char* resources_json, size_t len
 int cyc_probe_prepare(cyc_ctx* ctx, const char* probes_json, size_t len, cyc_probe_shape* shape);
 
 /* Compute the verdict planes on the GPU for target-pod rows [row_lo, row_hi) (rows are pods in
- * Resources.Pods order; pass 0, P for the whole table).  Device pointers; stream may be NULL
- * (the context's stream).  Asynchronous unless the inputs can panic (then it synchronises to
- * report the first panicking job in job order, as the reference would). */
+ * Resources.Pods order; pass 0, P for the whole table).  Device pointers; `hip_stream` is the
+ * hipStream_t to enqueue on (NULL = the HIP default stream, as with every HIP API).  Asynchronous
+ * unless the inputs can panic (then it synchronises to report the first panicking job in job
+ * order, as the reference would). */
 int cyc_probe_run(cyc_ctx* ctx, void* hip_stream, uint64_t* d_ingress, uint64_t* d_egress, uint8_t* d_status,
                   int64_t row_lo, int64_t row_hi);
 
