@@ -149,6 +149,14 @@ def main():
     emit_bytes = 2 * rows * K * W * 8  # both planes of this rank's rows, written once
     achieved = emit_bytes / (emit_ms * 1e-3) / 1e9
 
+    # HBM traffic of k_emit from the committed PMC passes for this same workload (rocprofv3
+    # --pmc FETCH_SIZE / WRITE_SIZE, corrected per MI355X_MICROARCH.md; scripts/pmc_summary.py)
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(ROOT, "profiles", f"r01_pmc_{args.config}.json")
+    if os.path.exists(pmc_path) and world == 1:
+        pmc = json.load(open(pmc_path))
+        traffic, traffic_src = pmc.get("emit_hbm_bytes_per_launch"), os.path.relpath(pmc_path, ROOT)
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -184,7 +192,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": emit_bytes,
                 "emit_ms": emit_ms,
                 "fill_ceiling_GBs": fill_gbs,
