@@ -613,6 +613,117 @@ __global__ __launch_bounds__(256) void k_first_error(ErrArgs a) {
   if (best != ~0ull) atomicMin(a.first, best);
 }
 
+// ---------------------------------------------------------------- single-cell queries
+// Policy.IsTrafficAllowed (policy.go:131-174) for arbitrary matcher.Traffic values, one thread per
+// traffic.  Endpoint 2i is the source, 2i+1 the destination; ext[e] = Internal == nil.
+// res[i] = ingress | egress << 1; pan[i] = panic code | (string kind << 8), pid[i] = string id.
+struct QueryArgs {
+  uint32_t n, L, D;
+  const uint32_t *pod_ns, *pod_ls, *pod_nsls, *ext, *tdesc;
+  const DIP* pod_ip;
+  const uint8_t* selres;
+  const uint8_t* portok;
+  const DTarget* tgt[2];
+  const uint32_t *tns_lo[2], *tns_hi[2];
+  const DPeer* peers;
+  const DIPBlock* ipbs;
+  const DCidr* cidrs;
+  const uint32_t* ipb_ex;
+  uint8_t* res;
+  uint32_t *pan, *pid;
+};
+
+enum { QP_NONE = 0, QP_SELECTOR = 1, QP_IP = 2, QP_CIDR = 3 };
+
+// returns 1 allowed / 0 denied, or sets *code and returns 2 (panic)
+__device__ uint32_t query_direction(const QueryArgs& a, int dir, uint32_t T, uint32_t Q, uint32_t desc, uint32_t* code,
+                                    uint32_t* sid) {
+  if (a.ext[T]) return 1;  // policy.go:151-153
+  const uint32_t ns = a.pod_ns[T], ls = a.pod_ls[T];
+  const uint32_t lo = a.tns_lo[dir][ns], hi = a.tns_hi[dir][ns];
+  uint32_t nmatch = 0;
+  for (uint32_t t = lo; t < hi; t++) {  // TargetsApplyingToPod evaluates every target first
+    uint8_t r = a.selres[uint64_t(a.tgt[dir][t].sel) * a.L + ls];
+    if (r == 2) {
+      *code = QP_SELECTOR;
+      return 2;
+    }
+    nmatch += r;
+  }
+  if (nmatch == 0) return 1;  // :158-160
+  uint32_t allowed = 0;
+  for (uint32_t t = lo; t < hi; t++) {
+    if (a.selres[uint64_t(a.tgt[dir][t].sel) * a.L + ls] != 1) continue;
+    DTarget tg = a.tgt[dir][t];
+    for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {  // Target.Allows: every matching target runs
+      DPeer pr = a.peers[j];
+      if (pr.kind == 0) {
+        allowed = 1;
+        break;
+      }
+      bool pok = a.portok[uint64_t(pr.port) * a.D + desc] != 0;
+      if (pr.kind == 1) {
+        if (pok) {
+          allowed = 1;
+          break;
+        }
+        continue;
+      }
+      uint32_t o;
+      if (pr.kind == 2) {
+        if (a.ext[Q]) continue;  // podpeermatcher.go:22-24
+        o = pod_peer_outcome(pr, a.selres, a.L, a.pod_ns[Q], a.pod_nsls[Q], a.pod_ls[Q]);
+        if (o == 2) {
+          *code = QP_SELECTOR;
+          return 2;
+        }
+      } else {
+        DIPBlock b = a.ipbs[pr.ipb];
+        if (!a.cidrs[b.cidr].valid) {
+          *code = QP_CIDR;
+          *sid = b.cidr;
+          return 2;
+        }
+        DIP ip = a.pod_ip[Q];
+        if (!ip.valid) {
+          *code = QP_IP;
+          *sid = Q;
+          return 2;
+        }
+        o = ip_peer_outcome(b, a.cidrs, a.ipb_ex, ip);
+        if (o == 2) {  // an except failed to parse: find which (evaluation order)
+          for (uint32_t e = 0; e < b.excnt; e++) {
+            uint32_t x = a.ipb_ex[b.exoff + e];
+            if (!a.cidrs[x].valid) {
+              *code = QP_CIDR;
+              *sid = x;
+              return 2;
+            }
+            if (cidr_contains(a.cidrs[x], ip)) break;
+          }
+        }
+      }
+      if (o == 1 && pok) {
+        allowed = 1;
+        break;
+      }
+    }
+  }
+  return allowed;
+}
+
+__global__ void k_query(QueryArgs a) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  uint32_t code = 0, sid = 0;
+  uint32_t in = query_direction(a, 0, 2 * i + 1, 2 * i, a.tdesc[i], &code, &sid);
+  uint32_t eg = 0;
+  if (in != 2) eg = query_direction(a, 1, 2 * i, 2 * i + 1, a.tdesc[i], &code, &sid);
+  a.res[i] = uint8_t((in == 1 ? 1 : 0) | (eg == 1 ? 2 : 0));
+  a.pan[i] = code;
+  a.pid[i] = sid;
+}
+
 }  // namespace cyc
 
 // ============================================================================ context + C ABI
@@ -1329,8 +1440,99 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   return fail(c, CYC_ERR_ARG, std::string("unknown option ") + name);
 }
 
-int cyc_query_traffic(cyc_ctx* c, const char*, size_t, uint8_t*, int64_t) {
-  return fail(c, CYC_ERR_ARG, "cyc_query_traffic: not implemented yet");
+int cyc_query_traffic(cyc_ctx* c, const char* js, size_t len, uint8_t* out, int64_t n) {
+  if (!c || !js) return CYC_ERR_ARG;
+  if (!c->have_policy) return fail(c, CYC_ERR_ARG, "load a policy first");
+  return guarded(c, [&]() -> int {
+    auto ts = load_traffics(json::parse(js, len));
+    if (int64_t(ts.size()) > n) return fail(c, CYC_ERR_ARG, "output buffer smaller than the traffic list");
+    if (ts.empty()) return (int)CYC_OK;
+    HIPCHK(hipSetDevice(c->device));
+    std::vector<uint32_t> ext, tdesc;
+    Problem q = build_query_problem(c->policy, ts, ext, tdesc);
+    DevBuf ls_off, ls_key, ls_val, sel_off, reqs, req_vals, pod_ns, pod_ls, pod_nsls, pod_ip, cidrs, ipbs, ipb_ex, pms, pents,
+        peers, descs, dext, dtdesc, tgt0, tgt1, lo0, lo1, hi0, hi1, selres, portok, res, pan, pid;
+    upload(ls_off, q.ls_off);
+    upload(ls_key, q.ls_key);
+    upload(ls_val, q.ls_val);
+    upload(sel_off, q.sel_off);
+    upload(reqs, q.reqs);
+    upload(req_vals, q.req_vals);
+    upload(pod_ns, q.pod_ns);
+    upload(pod_ls, q.pod_ls);
+    upload(pod_nsls, q.pod_nsls);
+    upload(pod_ip, q.pod_ip);
+    upload(cidrs, q.cidrs);
+    upload(ipbs, q.ipbs);
+    upload(ipb_ex, q.ipb_ex);
+    upload(pms, q.pms);
+    upload(pents, q.pents);
+    upload(peers, q.peers);
+    upload(descs, q.descs);
+    upload(dext, ext);
+    upload(dtdesc, tdesc);
+    upload(tgt0, q.tgt[0]);
+    upload(tgt1, q.tgt[1]);
+    upload(lo0, q.tns_lo[0]);
+    upload(lo1, q.tns_lo[1]);
+    upload(hi0, q.tns_hi[0]);
+    upload(hi1, q.tns_hi[1]);
+    const uint32_t D = uint32_t(std::max<size_t>(q.descs.size(), 1)), M = uint32_t(q.pms.size());
+    selres.alloc(std::max<uint64_t>(uint64_t(q.S) * q.L, 16));
+    portok.alloc(std::max<uint64_t>(uint64_t(M) * D, 16));
+    res.alloc(std::max<size_t>(ts.size(), 16));
+    pan.alloc(std::max<size_t>(ts.size() * 4, 16));
+    pid.alloc(std::max<size_t>(ts.size() * 4, 16));
+    hipStream_t st = nullptr;
+    if (uint64_t(q.S) * q.L)
+      k_selectors<<<grid1(uint64_t(q.S) * q.L, 256), 256, 0, st>>>(q.S, q.L, sel_off.as<uint32_t>(), reqs.as<DReq>(),
+                                                                    req_vals.as<uint32_t>(), ls_off.as<uint32_t>(),
+                                                                    ls_key.as<uint32_t>(), ls_val.as<uint32_t>(),
+                                                                    selres.as<uint8_t>());
+    if (M) k_portok<<<grid1(uint64_t(M) * D, 256), 256, 0, st>>>(M, D, pms.as<DPortM>(), pents.as<DPortEntry>(), descs.as<DDesc>(),
+                                                                portok.as<uint8_t>());
+    QueryArgs qa{};
+    qa.n = uint32_t(ts.size());
+    qa.L = q.L;
+    qa.D = D;
+    qa.pod_ns = pod_ns.as<uint32_t>();
+    qa.pod_ls = pod_ls.as<uint32_t>();
+    qa.pod_nsls = pod_nsls.as<uint32_t>();
+    qa.ext = dext.as<uint32_t>();
+    qa.tdesc = dtdesc.as<uint32_t>();
+    qa.pod_ip = pod_ip.as<DIP>();
+    qa.selres = selres.as<uint8_t>();
+    qa.portok = portok.as<uint8_t>();
+    qa.tgt[0] = tgt0.as<DTarget>();
+    qa.tgt[1] = tgt1.as<DTarget>();
+    qa.tns_lo[0] = lo0.as<uint32_t>();
+    qa.tns_lo[1] = lo1.as<uint32_t>();
+    qa.tns_hi[0] = hi0.as<uint32_t>();
+    qa.tns_hi[1] = hi1.as<uint32_t>();
+    qa.peers = peers.as<DPeer>();
+    qa.ipbs = ipbs.as<DIPBlock>();
+    qa.cidrs = cidrs.as<DCidr>();
+    qa.ipb_ex = ipb_ex.as<uint32_t>();
+    qa.res = res.as<uint8_t>();
+    qa.pan = pan.as<uint32_t>();
+    qa.pid = pid.as<uint32_t>();
+    k_query<<<grid1(ts.size(), 128), 128, 0, st>>>(qa);
+    std::vector<uint8_t> hres(ts.size());
+    std::vector<uint32_t> hpan(ts.size()), hpid(ts.size());
+    HIPCHK(hipMemcpy(hres.data(), res.p, ts.size(), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hpan.data(), pan.p, ts.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hpid.data(), pid.p, ts.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < ts.size(); i++) {
+      if (hpan[i]) {  // analyze.go:209-225 prints the earlier traffics, then the reference panics
+        if (hpan[i] == QP_SELECTOR) return fail(c, CYC_ERR_PANIC_SELECTOR, "invalid operator");
+        if (hpan[i] == QP_IP) return fail(c, CYC_ERR_PANIC_IP, "unable to parse IP '" + q.pod_ip_str[hpid[i]] + "'");
+        const std::string& cs = q.cidr_str[hpid[i]];
+        return fail(c, CYC_ERR_PANIC_CIDR, "unable to parse CIDR '" + cs + "': invalid CIDR address: " + cs);
+      }
+      out[i] = hres[i];
+    }
+    return (int)CYC_OK;
+  });
 }
 
 }  // extern "C"

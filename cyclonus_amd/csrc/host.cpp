@@ -998,35 +998,8 @@ struct Flattener {
 };
 }  // namespace
 
-Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vector<ProbeConfig>& probes) {
-  Problem pb;
-  Flattener F(pb, ir);
-  pb.P = uint32_t(res.pods.size());
-  pb.W = (pb.P + 63) / 64;
-
-  // ---- pods
-  bool any_bad_ip = false;
-  std::vector<uint32_t> ns_ls_cache;
-  std::unordered_map<std::string, uint32_t> nsls;
-  for (auto& p : res.pods) {
-    pb.pod_ns.push_back(pb.intern(p.ns));
-    pb.pod_ls.push_back(F.label_set(p.labels));
-    auto it = nsls.find(p.ns);
-    if (it == nsls.end()) {
-      uint32_t id = 0;
-      auto nit = res.namespaces.find(p.ns);  // r.Namespaces[ns]: nil when absent
-      if (nit != res.namespaces.end() && nit->second) id = F.label_set(*nit->second);
-      it = nsls.emplace(p.ns, id).first;
-    }
-    pb.pod_nsls.push_back(it->second);
-    DIP ip = parse_ip(p.ip);
-    if (!ip.valid) any_bad_ip = true;
-    pb.pod_ip.push_back(ip);
-    pb.pod_ip_str.push_back(p.ip);
-    pb.pod_key.push_back(p.ns + "/" + p.name);
-  }
-
-  // ---- targets and peers
+// Targets and their ordered peers (both directions) -> DTarget / DPeer / port / CIDR tables.
+static bool flatten_targets(Problem& pb, Flattener& F, const PolicyIR& ir) {
   bool any_ip_peer = false;
   for (int d = 0; d < 2; d++) {
     for (auto& t : ir.dir[d]) {
@@ -1060,6 +1033,55 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
       pb.tgt[d].push_back(dt);
     }
   }
+  return any_ip_peer;
+}
+
+static void finish_tables(Problem& pb) {
+  // ---- per-namespace target ranges (targets are sorted by primary key, which starts with the
+  //      namespace, so each namespace's targets are contiguous)
+  pb.L = uint32_t(pb.ls_off.size() - 1);
+  pb.S = uint32_t(pb.sel_off.size() - 1);
+  for (int d = 0; d < 2; d++) {
+    pb.tns_lo[d].assign(pb.strings.size(), 0);
+    pb.tns_hi[d].assign(pb.strings.size(), 0);
+    for (uint32_t t = 0; t < pb.tgt[d].size(); t++) {
+      uint32_t ns = pb.tgt[d][t].ns;
+      if (pb.tns_hi[d][ns] == 0) pb.tns_lo[d][ns] = t;
+      else if (pb.tns_hi[d][ns] != t) throw std::runtime_error("internal: namespace targets not contiguous");
+      pb.tns_hi[d][ns] = t + 1;
+    }
+  }
+}
+
+Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vector<ProbeConfig>& probes) {
+  Problem pb;
+  Flattener F(pb, ir);
+  pb.P = uint32_t(res.pods.size());
+  pb.W = (pb.P + 63) / 64;
+
+  // ---- pods
+  bool any_bad_ip = false;
+  std::vector<uint32_t> ns_ls_cache;
+  std::unordered_map<std::string, uint32_t> nsls;
+  for (auto& p : res.pods) {
+    pb.pod_ns.push_back(pb.intern(p.ns));
+    pb.pod_ls.push_back(F.label_set(p.labels));
+    auto it = nsls.find(p.ns);
+    if (it == nsls.end()) {
+      uint32_t id = 0;
+      auto nit = res.namespaces.find(p.ns);  // r.Namespaces[ns]: nil when absent
+      if (nit != res.namespaces.end() && nit->second) id = F.label_set(*nit->second);
+      it = nsls.emplace(p.ns, id).first;
+    }
+    pb.pod_nsls.push_back(it->second);
+    DIP ip = parse_ip(p.ip);
+    if (!ip.valid) any_bad_ip = true;
+    pb.pod_ip.push_back(ip);
+    pb.pod_ip_str.push_back(p.ip);
+    pb.pod_key.push_back(p.ns + "/" + p.name);
+  }
+
+  bool any_ip_peer = flatten_targets(pb, F, ir);
   if (any_ip_peer && any_bad_ip) pb.may_err = true;
 
   // ---- probe job slots (resources.go:274-364, resolved per destination pod)
@@ -1139,20 +1161,64 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
       pb.dup_key_msg[c] = "unable to add job result: duplicate key (pod " + dup_pod_key + " appears twice)";
   }
 
-  // ---- per-namespace target ranges (targets are sorted by primary key, which starts with the
-  //      namespace, so each namespace's targets are contiguous)
-  pb.L = uint32_t(pb.ls_off.size() - 1);
-  pb.S = uint32_t(pb.sel_off.size() - 1);
-  for (int d = 0; d < 2; d++) {
-    pb.tns_lo[d].assign(pb.strings.size(), 0);
-    pb.tns_hi[d].assign(pb.strings.size(), 0);
-    for (uint32_t t = 0; t < pb.tgt[d].size(); t++) {
-      uint32_t ns = pb.tgt[d][t].ns;
-      if (pb.tns_hi[d][ns] == 0) pb.tns_lo[d][ns] = t;
-      else if (pb.tns_hi[d][ns] != t) throw std::runtime_error("internal: namespace targets not contiguous");
-      pb.tns_hi[d][ns] = t + 1;
+  finish_tables(pb);
+  return pb;
+}
+
+std::vector<QueryTraffic> load_traffics(const Node& n) {
+  std::vector<QueryTraffic> out;
+  if (!n.is_arr()) return out;
+  auto end = [](const Node* p) {
+    QueryEnd e;
+    if (!p) return e;
+    if (auto ip = p->val("IP")) e.ip = ip->str();
+    if (auto in = p->val("Internal")) {
+      e.external = false;
+      if (auto ns = in->val("Namespace")) e.ns = ns->str();
+      bool nil;
+      decode_labels(in->val("PodLabels"), nil, e.labels);
+      decode_labels(in->val("NamespaceLabels"), nil, e.ns_labels);
     }
+    return e;
+  };
+  for (auto& t : n.a) {
+    QueryTraffic q;
+    q.src = end(t.val("Source"));
+    q.dst = end(t.val("Destination"));
+    if (auto x = t.val("ResolvedPort")) q.port = int32_t(x->i64());
+    if (auto x = t.val("ResolvedPortName")) q.port_name = x->str();
+    if (auto x = t.val("Protocol")) q.proto = x->str();
+    out.push_back(std::move(q));
   }
+  return out;
+}
+
+// Query mode (analyze --mode query-traffic, analyze.go:209-225): endpoint 2i is traffic i's
+// source, 2i+1 its destination; namespace labels come from the Traffic itself.
+Problem build_query_problem(const PolicyIR& ir, const std::vector<QueryTraffic>& ts, std::vector<uint32_t>& ext,
+                            std::vector<uint32_t>& tdesc) {
+  Problem pb;
+  Flattener F(pb, ir);
+  pb.P = uint32_t(ts.size() * 2);
+  pb.W = (pb.P + 63) / 64;
+  bool any_bad_ip = false;
+  ext.clear();
+  tdesc.clear();
+  for (auto& t : ts)
+    for (const QueryEnd* e : {&t.src, &t.dst}) {
+      pb.pod_ns.push_back(pb.intern(e->ns));
+      pb.pod_ls.push_back(F.label_set(e->labels));
+      pb.pod_nsls.push_back(F.label_set(e->ns_labels));
+      DIP ip = parse_ip(e->ip);
+      any_bad_ip |= !ip.valid;
+      pb.pod_ip.push_back(ip);
+      pb.pod_ip_str.push_back(e->ip);
+      ext.push_back(e->external ? 1u : 0u);
+    }
+  for (auto& t : ts) tdesc.push_back(F.desc(t.port, t.port_name, t.proto));
+  bool any_ip_peer = flatten_targets(pb, F, ir);
+  if (any_ip_peer && any_bad_ip) pb.may_err = true;
+  finish_tables(pb);
   return pb;
 }
 

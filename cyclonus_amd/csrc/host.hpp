@@ -185,4 +185,19 @@ struct Problem {
 
 Problem build_problem(const PolicyIR& pol, const Resources& res, const std::vector<ProbeConfig>& probes);
 
+// matcher.Traffic (traffic.go:11-18) for the single-cell query API.
+struct QueryEnd {
+  bool external = true;  // Internal == nil
+  std::string ns, ip;
+  std::map<std::string, std::string> labels, ns_labels;
+};
+struct QueryTraffic {
+  QueryEnd src, dst;
+  int32_t port = 0;
+  std::string port_name, proto;
+};
+std::vector<QueryTraffic> load_traffics(const json::Node& n);
+Problem build_query_problem(const PolicyIR& pol, const std::vector<QueryTraffic>& ts, std::vector<uint32_t>& ext,
+                            std::vector<uint32_t>& tdesc);
+
 }  // namespace cyc

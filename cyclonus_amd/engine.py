@@ -99,6 +99,14 @@ class Engine:
             ),
         )
 
+    def query_traffic(self, traffics):
+        """Policy.IsTrafficAllowed on the GPU for a list of matcher.Traffic dicts -> [(ingress, egress)]."""
+        b = _bytes(list(traffics))
+        n = len(traffics)
+        out = np.zeros(max(n, 1), np.uint8)
+        check(self._ctx, lib().cyc_query_traffic(self._ctx, b, len(b), out.ctypes.data, n))
+        return [(bool(o & 1), bool(o & 2)) for o in out[:n]]
+
     def set_option(self, name: str, value: int):
         check(self._ctx, lib().cyc_set_option(self._ctx, name.encode(), int(value)))
 

@@ -40,7 +40,8 @@ def readme_combined_table():
     for r in rows[1:]:
         cells = [c.strip() for c in r.strip("|").split("|")]
         table[cells[0]] = dict(zip(header[1:], cells[1:]))
-    return {"header": header[1:], "rows": table}
+    raw = [l for l in lines[start + 1 : start + 20] if l.startswith("+") or l.startswith("|")]
+    return {"header": header[1:], "rows": table, "text": "\n".join(raw) + "\n"}
 
 
 def config1():
