@@ -71,29 +71,35 @@ def main():
 
     from cyclonus_amd import synth
     from cyclonus_amd.engine import Engine
+    from cyclonus_amd.shard import row_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    device = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs only in a rehearsal
+    torch.cuda.set_device(device)
+    backend = os.environ.get("CYC_BENCH_BACKEND", "nccl")  # "gloo" = CPU rehearsal of the N>1 flow
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     data = synth.CONFIGS[args.config]()
-    eng = Engine(local)
+    eng = Engine(device)
     eng.build_policies(json.dumps(data["policies"]))
     eng.load_resources(json.dumps(data["resources"]))
     shape = eng.prepare(data["probes"])
     P, K, W = shape["pods"], shape["slots"], shape["words"]
-    lo, hi = rank * P // world, (rank + 1) * P // world
+    lo, hi = row_range(P, world, rank)
     rows = hi - lo
 
     d_in = torch.empty((max(rows, 1), K, W), dtype=torch.int64, device="cuda")
@@ -116,7 +122,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 

@@ -86,13 +86,15 @@ __device__ uint8_t eval_selector(const uint32_t* __restrict__ sel_off, const DRe
   return 1;
 }
 
+// sel_list (optional): only these selectors' rows are evaluated (range plan); S = its length.
 __global__ void k_selectors(uint32_t S, uint32_t L, const uint32_t* sel_off, const DReq* reqs, const uint32_t* req_vals,
                             const uint32_t* ls_off, const uint32_t* ls_key, const uint32_t* ls_val,
-                            uint8_t* __restrict__ selres) {
+                            uint8_t* __restrict__ selres, const uint32_t* __restrict__ sel_list = nullptr) {
   uint64_t n = uint64_t(S) * L;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
     uint32_t s = uint32_t(i / L), l = uint32_t(i % L);
-    selres[i] = eval_selector(sel_off, reqs, req_vals, ls_off, ls_key, ls_val, s, l);
+    if (sel_list) s = sel_list[s];
+    selres[uint64_t(s) * L + l] = eval_selector(sel_off, reqs, req_vals, ls_off, ls_key, ls_val, s, l);
   }
 }
 
@@ -312,6 +314,8 @@ struct MemberArgs {
   unsigned long long* ht_key; // hash table (capacity ht_cap, power of two), 0 = empty
   uint32_t* ht_rep;           // min identity per key
   uint32_t ht_cap;
+  const uint32_t* act;        // identities used by the rows of this run (range plan)
+  uint32_t n_act;
 };
 
 __device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* keys, uint32_t cap, uint64_t h) {
@@ -336,8 +340,9 @@ __device__ __forceinline__ uint32_t ht_find(const unsigned long long* keys, uint
 }
 
 __global__ void k_member(MemberArgs a) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n_ident) return;
+  uint32_t ii = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ii >= a.n_act) return;
+  const uint32_t i = a.act[ii];
   uint32_t ns = a.id_ns[i], ls = a.id_ls[i];
   uint32_t lo = a.tns_lo[ns], hi = a.tns_hi[ns];
   uint32_t n = 0, off = a.list_off[i];
@@ -369,8 +374,9 @@ __global__ void k_member(MemberArgs a) {
 }
 
 __global__ void k_classify(MemberArgs a, uint32_t* __restrict__ class_of) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n_ident) return;
+  uint32_t ii = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ii >= a.n_act) return;
+  const uint32_t i = a.act[ii];
   uint32_t c = i;
   if (!a.err[i]) {
     uint32_t s = ht_find(a.ht_key, a.ht_cap, a.hash[i]);
@@ -404,6 +410,8 @@ struct RowArgs {
   const uint8_t* portok;
   uint32_t D;
   uint32_t n_ident, K, W, P;
+  const uint32_t* act;  // active identities (range plan)
+  uint32_t n_act;
   const uint32_t* class_of;
   const uint32_t *cnt, *list_off, *list;
   const uint8_t* id_err;
@@ -419,10 +427,12 @@ struct RowArgs {
 template <bool EGRESS, bool ERR>
 __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
   const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
-  const uint32_t i = blockIdx.x / (chunks * nkc);
+  const uint32_t ii = blockIdx.x / (chunks * nkc);
   const uint32_t kc = (blockIdx.x / chunks) % nkc;
   const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
-  if (i >= a.n_ident || a.class_of[i] != i || w >= a.W) return;
+  if (ii >= a.n_act) return;
+  const uint32_t i = a.act[ii];
+  if (a.class_of[i] != i || w >= a.W) return;
   const uint32_t k0 = kc * KC;
   const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
   const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
@@ -596,15 +606,18 @@ __global__ __launch_bounds__(256) void k_first_error(ErrArgs a) {
   uint32_t s = blockIdx.x / chunks;
   uint32_t d = (blockIdx.x % chunks) * blockDim.x + threadIdx.x;
   if (d >= a.P) return;
-  bool s_err = a.err_eg[a.pod_eid[s]];
-  bool d_err = a.err_in[a.pod_iid[d]];
-  uint32_t ci = a.class_in[a.pod_iid[d]], ce = a.class_eg[a.pod_eid[s]];
+  // only the directions whose rows this run computes (the whole table when [lo,hi) = [0,P))
+  const bool din = d >= a.row_lo && d < a.row_hi, sin = s >= a.row_lo && s < a.row_hi;
+  if (!din && !sin) return;
+  bool s_err = sin && a.err_eg[a.pod_eid[s]];
+  bool d_err = din && a.err_in[a.pod_iid[d]];
+  uint32_t ci = din ? a.class_in[a.pod_iid[d]] : 0, ce = sin ? a.class_eg[a.pod_eid[s]] : 0;
   unsigned long long best = ~0ull;
   for (uint32_t k = 0; k < a.K; k++) {
     if (a.slot_status[uint64_t(d) * a.K + k] != CYC_JOB_VALID) continue;
     bool e = d_err || s_err;
-    if (!e && a.AE_in) e = (a.AE_in[(uint64_t(ci) * a.K + k) * a.W + s / 64] >> (s % 64)) & 1;
-    if (!e && a.AE_eg) e = (a.AE_eg[(uint64_t(ce) * a.K + k) * a.W + d / 64] >> (d % 64)) & 1;
+    if (!e && din && a.AE_in) e = (a.AE_in[(uint64_t(ci) * a.K + k) * a.W + s / 64] >> (s % 64)) & 1;
+    if (!e && sin && a.AE_eg) e = (a.AE_eg[(uint64_t(ce) * a.K + k) * a.W + d / 64] >> (d % 64)) & 1;
     if (e) {
       unsigned long long key = ((uint64_t(a.slot_cfg[k]) * a.P + s) * a.P + d) * 65536ull + a.slot_idx[k];
       best = key < best ? key : best;
@@ -782,6 +795,12 @@ struct DirDev {
 };
 }  // namespace
 
+struct PeerPlan {
+  std::vector<uint32_t> pod_peers, ip_peers, word_off, run_e;
+  std::vector<uint64_t> run_mask;
+  std::vector<DIPTest> ip_tests;
+  std::vector<DCidr> ip_ex;
+};
 struct cyc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -798,6 +817,9 @@ struct cyc_ctx {
   // peer-row stage: pod peers in identity space + per-word identity runs; IP peers per pod
   DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido;
   uint32_t Rp = 0, Ri = 0;
+  PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
+  DevBuf act[2], sel_list;
+  uint32_t n_act[2] = {0, 0}, n_sel = 0;
   int emit_variant = 0;  // tuning knob (cyc_set_option "emit_variant")
   DirDev dir[2];
   int64_t order_lo = -1, order_hi = -1;
@@ -874,12 +896,6 @@ static void build_identities(cyc_ctx* c) {
 
 // Host side of the peer-row stage: which peers are pod peers / IP peers, and for every 64-pod
 // word the runs of equal egress identity (a pod peer's outcome is a function of that identity).
-struct PeerPlan {
-  std::vector<uint32_t> pod_peers, ip_peers, word_off, run_e;
-  std::vector<uint64_t> run_mask;
-  std::vector<DIPTest> ip_tests;
-  std::vector<DCidr> ip_ex;
-};
 static PeerPlan plan_peers(const Problem& pb, const Identities& eg) {
   PeerPlan pl;
   for (uint32_t j = 0; j < pb.peers.size(); j++) {
@@ -949,18 +965,13 @@ static void prepare_device(cyc_ctx* c) {
   c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
   c->ER.alloc(pb.may_err ? std::max<uint64_t>(R * W * 8, 16) : 16);
   {
-    PeerPlan pl = plan_peers(pb, c->ids[1]);
-    c->Rp = uint32_t(pl.pod_peers.size());
-    c->Ri = uint32_t(pl.ip_peers.size());
-    upload(c->pod_peers, pl.pod_peers);
-    upload(c->ip_peers, pl.ip_peers);
-    upload(c->ip_tests, pl.ip_tests);
-    upload(c->ip_ex, pl.ip_ex);
+    c->plan = plan_peers(pb, c->ids[1]);
+    PeerPlan& pl = c->plan;
     upload(c->word_off, pl.word_off);
     upload(c->run_e, pl.run_e);
     upload(c->run_mask, pl.run_mask);
     upload(c->id_nsls, c->ids[1].nsls);
-    c->ido.alloc(std::max<uint64_t>(uint64_t(c->Rp) * c->ids[1].ns.size(), 16));
+    c->ido.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * c->ids[1].ns.size(), 16));
   }
   c->portok.alloc(std::max<uint64_t>(pb.pms.size() * D, 16));
   c->VALID.alloc(std::max<uint64_t>(K * W * 8, 16));
@@ -1020,12 +1031,19 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   a.ht_key = dd.ht_key.as<unsigned long long>();
   a.ht_rep = dd.ht_rep.as<uint32_t>();
   a.ht_cap = dd.ht_cap;
+  a.act = c->act[d].as<uint32_t>();
+  a.n_act = c->n_act[d];
   return a;
 }
 
-// Rows [lo,hi) ordered so pods sharing class rows are adjacent (L2 / Infinity-Cache reuse).
-static void ensure_order(cyc_ctx* c, int64_t lo, int64_t hi) {
+// Range plan for rows [lo,hi): (1) the rows ordered so pods sharing class rows are adjacent
+// (L2 / Infinity-Cache reuse in k_emit); (2) the identities those rows use, per direction —
+// only their classes are elected and their class rows computed; (3) the peers of the targets
+// in those identities' namespaces — only their PM rows are built.  A rank of an N-GPU run thus
+// does ~1/N of the front work too, not just 1/N of the emit.
+static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   if (c->order_lo == lo && c->order_hi == hi) return;
+  Problem& pb = c->pb;
   std::vector<uint32_t> ord(size_t(hi - lo));
   std::iota(ord.begin(), ord.end(), uint32_t(lo));
   const auto& iin = c->ids[0].of_pod;
@@ -1034,6 +1052,67 @@ static void ensure_order(cyc_ctx* c, int64_t lo, int64_t hi) {
     return iin[x] != iin[y] ? iin[x] < iin[y] : ieg[x] < ieg[y];
   });
   upload(c->order, ord);
+  std::vector<uint8_t> peer_needed(pb.peers.size(), 0);
+  for (int d = 0; d < 2; d++) {
+    const Identities& I = c->ids[d];
+    std::vector<uint8_t> used(I.ns.size(), 0);
+    std::vector<uint32_t> act;
+    for (int64_t p = lo; p < hi; p++) {
+      uint32_t i = I.of_pod[size_t(p)];
+      if (!used[i]) {
+        used[i] = 1;
+        act.push_back(i);
+      }
+    }
+    std::sort(act.begin(), act.end());
+    std::vector<uint8_t> ns_needed(pb.strings.size(), 0);
+    for (uint32_t i : act) ns_needed[I.ns[i]] = 1;
+    for (const DTarget& t : pb.tgt[d])
+      if (ns_needed[t.ns])
+        for (uint32_t j = t.poff; j < t.poff + t.pcnt; j++) peer_needed[j] = 1;
+    c->n_act[d] = uint32_t(act.size());
+    upload(c->act[d], act);
+  }
+  // selectors the range can reach: its targets' pod selectors and their peers' selectors
+  std::vector<uint8_t> sel_needed(pb.S, 0);
+  for (int d = 0; d < 2; d++)
+    for (const DTarget& t : pb.tgt[d]) {
+      bool needed = false;
+      for (uint32_t j = t.poff; j < t.poff + t.pcnt && !needed; j++) needed = peer_needed[j];
+      if (needed || t.pcnt == 0) sel_needed[t.sel] = 1;
+    }
+  for (int d = 0; d < 2; d++) {  // targets of active namespaces (also those without peers)
+    const Identities& I = c->ids[d];
+    std::vector<uint8_t> ns_needed(pb.strings.size(), 0);
+    for (int64_t p = lo; p < hi; p++) ns_needed[I.ns[I.of_pod[size_t(p)]]] = 1;
+    for (const DTarget& t : pb.tgt[d])
+      if (ns_needed[t.ns]) sel_needed[t.sel] = 1;
+  }
+  for (uint32_t j = 0; j < pb.peers.size(); j++)
+    if (peer_needed[j] && pb.peers[j].kind == PK_POD) {
+      if (pb.peers[j].nskind == NS_LABEL) sel_needed[pb.peers[j].nsval] = 1;
+      if (pb.peers[j].podsel != CYC_ALL) sel_needed[pb.peers[j].podsel] = 1;
+    }
+  std::vector<uint32_t> sl;
+  for (uint32_t i = 0; i < pb.S; i++)
+    if (sel_needed[i]) sl.push_back(i);
+  c->n_sel = uint32_t(sl.size());
+  upload(c->sel_list, sl);
+  std::vector<uint32_t> pp, ip;
+  std::vector<DIPTest> tests;
+  for (uint32_t j : c->plan.pod_peers)
+    if (peer_needed[j]) pp.push_back(j);
+  for (size_t r = 0; r < c->plan.ip_peers.size(); r++)
+    if (peer_needed[c->plan.ip_peers[r]]) {
+      ip.push_back(c->plan.ip_peers[r]);
+      tests.push_back(c->plan.ip_tests[r]);
+    }
+  c->Rp = uint32_t(pp.size());
+  c->Ri = uint32_t(ip.size());
+  upload(c->pod_peers, pp);
+  upload(c->ip_peers, ip);
+  upload(c->ip_tests, tests);
+  upload(c->ip_ex, c->plan.ip_ex);
   c->order_lo = lo;
   c->order_hi = hi;
 }
@@ -1044,14 +1123,14 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size());
   if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
-  ensure_order(c, lo, hi);
+  ensure_range(c, lo, hi);
   HIPCHK(hipEventRecord(c->ev[0], st));
 
   // 1. selectors x label sets
-  if (uint64_t(pb.S) * pb.L)
-    k_selectors<<<grid1(uint64_t(pb.S) * pb.L, 256), 256, 0, st>>>(
-        pb.S, pb.L, c->sel_off.as<uint32_t>(), c->reqs.as<DReq>(), c->req_vals.as<uint32_t>(), c->ls_off.as<uint32_t>(),
-        c->ls_key.as<uint32_t>(), c->ls_val.as<uint32_t>(), c->selres.as<uint8_t>());
+  if (uint64_t(c->n_sel) * pb.L)
+    k_selectors<<<grid1(uint64_t(c->n_sel) * pb.L, 256), 256, 0, st>>>(
+        c->n_sel, pb.L, c->sel_off.as<uint32_t>(), c->reqs.as<DReq>(), c->req_vals.as<uint32_t>(), c->ls_off.as<uint32_t>(),
+        c->ls_key.as<uint32_t>(), c->ls_val.as<uint32_t>(), c->selres.as<uint8_t>(), c->sel_list.as<uint32_t>());
   // 2. peer rows: pod peers in identity space, expanded over word runs; IP peers per pod
   const uint32_t E = c->dir[1].n;
   if (c->Rp && E && W) {
@@ -1093,8 +1172,9 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     HIPCHK(hipMemsetAsync(dd.ht_key.p, 0, dd.ht_key.bytes, st));
     HIPCHK(hipMemsetAsync(dd.ht_rep.p, 0xFF, dd.ht_rep.bytes, st));
     MemberArgs ma = member_args(c, d);
-    k_member<<<grid1(dd.n, 128), 128, 0, st>>>(ma);
-    k_classify<<<grid1(dd.n, 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
+    if (!c->n_act[d]) continue;
+    k_member<<<grid1(c->n_act[d], 128), 128, 0, st>>>(ma);
+    k_classify<<<grid1(c->n_act[d], 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
   }
   HIPCHK(hipEventRecord(c->ev[1], st));
   // 6. class rows
@@ -1109,6 +1189,8 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     ra.portok = c->portok.as<uint8_t>();
     ra.D = D;
     ra.n_ident = dd.n;
+    ra.act = c->act[d].as<uint32_t>();
+    ra.n_act = c->n_act[d];
     ra.K = K;
     ra.W = W;
     ra.P = P;
@@ -1124,7 +1206,8 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     ra.DM = c->DM.as<uint64_t>();
     ra.A = dd.A.as<uint64_t>();
     ra.AE = pb.may_err ? dd.AE.as<uint64_t>() : nullptr;
-    unsigned g = unsigned(uint64_t((W + 255) / 256) * dd.n * ((K + KC - 1) / KC));
+    if (!c->n_act[d]) continue;
+    unsigned g = unsigned(uint64_t((W + 255) / 256) * c->n_act[d] * ((K + KC - 1) / KC));
     if (d == 0) {
       if (pb.may_err) k_class_rows<false, true><<<g, 256, 0, st>>>(ra);
       else k_class_rows<false, false><<<g, 256, 0, st>>>(ra);
@@ -1176,6 +1259,8 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     e.K = K;
     e.W = W;
     e.n_cfg = pb.n_cfg;
+    e.row_lo = uint32_t(lo);
+    e.row_hi = uint32_t(hi);
     e.slot_status = c->slot_status.as<uint8_t>();
     e.slot_cfg = c->slot_cfg.as<uint32_t>();
     e.slot_idx = c->slot_idx.as<uint32_t>();

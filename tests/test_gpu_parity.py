@@ -174,3 +174,20 @@ def test_synthetic_sampled_parity(gpu, name, kw, n):
     want = Oracle(data["policies"], data["resources"]).cells(data["probes"], s, d, k)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, f"{bad.size} cells differ, first {[(int(s[i]), int(d[i]), int(k[i]), int(got[i]), int(want[i])) for i in bad[:5]]}"
+
+
+def test_partial_ranges_match_full_on_synthetic(gpu):
+    """Range plans (active identities / peers per row shard) give the same rows as the full run."""
+    from cyclonus_amd import synth
+    from cyclonus_amd.shard import row_range
+
+    data = synth.config3(n_ns=40)
+    eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
+    eng.prepare(data["probes"])
+    st, ing, eg = eng.run_host()
+    P = st.shape[0]
+    for world in (2, 3, 8):
+        for rank in range(world):
+            lo, hi = row_range(P, world, rank)
+            st2, ing2, eg2 = eng.run_host(lo, hi)
+            assert np.array_equal(ing[lo:hi], ing2) and np.array_equal(eg[lo:hi], eg2), (world, rank)
