@@ -17,7 +17,7 @@ def test_loads_simple_example_in_walk_order(tmp_path):
         (tmp_path / f"{p['metadata']['name']}.yaml").write_text(json.dumps(p))
         names.append(p["metadata"]["name"])
     got = read_policies_from_path(str(tmp_path))
-    assert [p["metadata"]["name"] for p in got] == sorted(names)
+    assert [p["metadata"]["name"] for p in got] == [n[:-5] for n in sorted(n + ".yaml" for n in names)]
     assert sorted(json.dumps(p, sort_keys=True) for p in got) == sorted(json.dumps(p, sort_keys=True) for p in c["policies"])
 
 
