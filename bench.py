@@ -25,11 +25,36 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 METRIC = "pod-pair×port verdicts/sec (node) at 100k pods×10k policies; HBM GB/s"
 
 
+def load_workload(name: str):
+    from cyclonus_amd import synth
+
+    if name != "config5":
+        return synth.CONFIGS[name]()
+    from cyclonus_amd.batch import Batch
+    from cyclonus_amd.generator import sweep
+
+    steps = sweep()
+    bt = Batch(steps)
+    return {"name": "config5", "policies": bt.policies, "resources": bt.resources, "probes": bt.probes, "batch": bt,
+            "steps": steps, "description": f"cyclonus generate sweep: {len(steps)} probe steps batched in one pass"}
+
+
 def cpu_baseline(data, seconds: float, seed: int = 1):
     """Time the per-cell CPU oracle (restated reference walk, 1 thread) on random cells."""
     import numpy as np
 
     from oracle.oracle import Oracle
+
+    if "steps" in data:  # config #5: every cell of every step (small problems)
+        t0 = time.perf_counter()
+        cells = 0
+        for st in data["steps"]:
+            status, _, _ = Oracle(st["policies"], st["resources"]).probe([st["probe"]])
+            cells += status.shape[0] * int((status == 1).sum())
+        el = time.perf_counter() - t0
+        return {"value": cells / el, "unit": "verdicts/s", "cores": 1, "kind": "port",
+                "sample": f"all {cells} cells of the {len(data['steps'])} generate steps through the oracle "
+                f"(policy build per step included), {el:.2f} s, 1 thread"}
 
     t0 = time.perf_counter()
     orc = Oracle(data["policies"], data["resources"], True)
@@ -61,7 +86,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4"])
+    ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4", "config5"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -69,7 +94,6 @@ def main():
     import numpy as np
     import torch
 
-    from cyclonus_amd import synth
     from cyclonus_amd.engine import Engine
     from cyclonus_amd.shard import row_range
 
@@ -93,7 +117,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    data = synth.CONFIGS[args.config]()
+    data = load_workload(args.config)
     eng = Engine(device)
     eng.build_policies(json.dumps(data["policies"]))
     eng.load_resources(json.dumps(data["resources"]))
@@ -147,8 +171,11 @@ def main():
     fill_gbs = (d_in.numel() + d_eg.numel()) * 8 / (min(fills) * 1e-3) / 1e9
 
     status = d_st.cpu().numpy()
-    valid_slots = int((status == 1).sum())  # (dst, slot) pairs with a VALID job
-    cells = P * valid_slots  # every source pod x every valid (dst, slot) job
+    if "batch" in data:  # only the cells inside each batched problem are answers
+        cells = data["batch"].cells(status)
+    else:
+        valid_slots = int((status == 1).sum())  # (dst, slot) pairs with a VALID job
+        cells = P * valid_slots  # every source pod x every valid (dst, slot) job
     ms_per_step = dt / args.steps * 1e3
     value = cells / (dt / args.steps)
 
@@ -178,7 +205,7 @@ def main():
             "dtype": "u64",
             "data": "synthetic (cyclonus_amd/synth.py, xoshiro256** seed 20250217)",
             "config": {
-                "workload": f"{data['name']}: {data['description']} (AllAvailable probe)",
+                "workload": f"{data['name']}: {data['description']}",
                 "pods": P,
                 "policies": len(data["policies"]),
                 "slots": K,

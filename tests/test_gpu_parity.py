@@ -191,3 +191,25 @@ def test_partial_ranges_match_full_on_synthetic(gpu):
             lo, hi = row_range(P, world, rank)
             st2, ing2, eg2 = eng.run_host(lo, hi)
             assert np.array_equal(ing[lo:hi], ing2) and np.array_equal(eg[lo:hi], eg2), (world, rank)
+
+
+def test_config5_generate_sweep_batched(gpu):
+    """All 242 probe steps of `cyclonus generate --mock --exclude ''` in one batched GPU pass,
+    each block bit-exact vs the oracle run on that step alone."""
+    from cyclonus_amd.batch import Batch
+    from cyclonus_amd.generator import sweep
+
+    steps = sweep()
+    assert len(steps) == 242
+    bt = Batch(steps)
+    eng = Engine(0).build_policies(json.dumps(bt.policies)).load_resources(json.dumps(bt.resources))
+    eng.prepare(bt.probes)
+    st, ing, eg = eng.run_host()
+    assert bt.cells(st) > 100_000
+    for b, step in enumerate(steps):
+        want = Oracle(step["policies"], step["resources"]).probe([step["probe"]])
+        got = bt.extract(b, st, ing, eg)
+        if step["probe"].get("AllAvailable"):
+            k = want[0].shape[1]
+            got = (got[0][:, :k], got[1][:, :k], got[2][:, :k])
+        assert_same(want, got, f"step {b} ({step['description']})")
