@@ -203,7 +203,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (cyclonus_amd/synth.py, xoshiro256** seed 20250217)",
+            "data": "synthetic (cyclonus_amd/generator.py restated generate sweep)" if args.config == "config5" else "synthetic (cyclonus_amd/synth.py, xoshiro256** seed 20250217)",
             "config": {
                 "workload": f"{data['name']}: {data['description']}",
                 "pods": P,
