@@ -189,14 +189,14 @@ struct DIPTest {
 template <bool ERR>
 __global__ __launch_bounds__(256) void k_ip_rows(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                  const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
-                                                 uint64_t* __restrict__ PM, uint64_t* __restrict__ ER) {
+                                                 uint64_t* __restrict__ PM, uint64_t* __restrict__ ER, uint32_t batch) {
   __shared__ DIPTest s_t[IPB_BATCH];
   __shared__ DCidr s_ex[IPB_EX_LDS];
   const uint32_t wchunks = (W + 3) / 4;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t w = (blockIdx.x % wchunks) * 4 + wave;
-  const uint32_t r0 = (blockIdx.x / wchunks) * IPB_BATCH;
-  const uint32_t nr = min(Ri - r0, IPB_BATCH);
+  const uint32_t r0 = (blockIdx.x / wchunks) * batch;
+  const uint32_t nr = min(Ri - r0, batch);
   const uint32_t ex0 = tests[r0].exoff;
   const uint32_t nex = tests[r0 + nr - 1].exoff + tests[r0 + nr - 1].excnt - ex0;
   for (uint32_t t = threadIdx.x; t < nr; t += blockDim.x) s_t[t] = tests[r0 + t];
@@ -321,8 +321,12 @@ struct MemberArgs {
 __device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* keys, uint32_t cap, uint64_t h) {
   uint32_t s = uint32_t(h) & (cap - 1);
   for (uint32_t probe = 0; probe < cap; probe++) {
-    unsigned long long old = atomicCAS(&keys[s], 0ull, (unsigned long long)h);
-    if (old == 0ull || old == h) return s;
+    unsigned long long cur = keys[s];
+    if (cur == h) return s;
+    if (cur == ~0ull) {
+      unsigned long long old = atomicCAS(&keys[s], ~0ull, (unsigned long long)h);
+      if (old == ~0ull || old == h) return s;
+    }
     s = (s + 1) & (cap - 1);
   }
   return 0xFFFFFFFFu;  // unreachable: cap >= 2 * n_ident
@@ -333,7 +337,7 @@ __device__ __forceinline__ uint32_t ht_find(const unsigned long long* keys, uint
   for (uint32_t probe = 0; probe < cap; probe++) {
     unsigned long long k = keys[s];
     if (k == h) return s;
-    if (k == 0ull) return 0xFFFFFFFFu;
+    if (k == ~0ull) return 0xFFFFFFFFu;
     s = (s + 1) & (cap - 1);
   }
   return 0xFFFFFFFFu;
@@ -363,13 +367,26 @@ __global__ void k_member(MemberArgs a) {
       h = mix64(h ^ ((st << 40) | uint32_t(d + 1)) ^ (uint64_t(k) << 48));
     }
   }
-  h |= 1ull;  // never the empty key
+  h &= 0x7FFFFFFFFFFFFFFFull;  // never the empty key (~0)
   a.cnt[i] = n;
   a.hash[i] = h;
   a.err[i] = e;
-  if (!e) {
-    uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
-    atomicMin(&a.ht_rep[s], i);
+  // Many identities share a class (e.g. every pod no policy selects): lanes of a wave with the
+  // same key elect their lowest lane (= lowest identity, act[] is sorted) to do the atomics, so
+  // a popular key costs one CAS + one atomicMin per wave instead of one per identity.
+  bool want = !e;
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t pending = __ballot(want);
+  while (pending) {
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const uint64_t hk = __shfl(h, leader);
+    const uint64_t same = __ballot(want && h == hk);
+    if (int(lane) == leader) {
+      uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
+      atomicMin(&a.ht_rep[s], i);
+    }
+    pending &= ~same;
+    if (h == hk) want = false;
   }
 }
 
@@ -821,6 +838,11 @@ struct cyc_ctx {
   DevBuf act[2], sel_list;
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
   int emit_variant = 0;  // tuning knob (cyc_set_option "emit_variant")
+  bool use_graphs = true;  // cyc_set_option "graphs"
+  hipStream_t cap_stream = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  const void* graph_key[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  bool timed_graph = false;
   DirDev dir[2];
   int64_t order_lo = -1, order_hi = -1;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -996,8 +1018,7 @@ static void prepare_device(cyc_ctx* c) {
     dd.cnt.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.hash.alloc(std::max<uint64_t>(dd.n * 8ull, 16));
     dd.err.alloc(std::max<uint64_t>(dd.n, 16));
-    dd.ht_key.alloc(uint64_t(dd.ht_cap) * 8);
-    dd.ht_rep.alloc(uint64_t(dd.ht_cap) * 4);
+    dd.ht_key.alloc(uint64_t(dd.ht_cap) * 12);  // [cap] u64 keys (empty = ~0) then [cap] u32 reps
     dd.class_of.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.A.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
     if (pb.may_err) dd.AE.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
@@ -1029,7 +1050,7 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   a.hash = dd.hash.as<uint64_t>();
   a.err = dd.err.as<uint8_t>();
   a.ht_key = dd.ht_key.as<unsigned long long>();
-  a.ht_rep = dd.ht_rep.as<uint32_t>();
+  a.ht_rep = reinterpret_cast<uint32_t*>(dd.ht_key.as<uint64_t>() + dd.ht_cap);
   a.ht_cap = dd.ht_cap;
   a.act = c->act[d].as<uint32_t>();
   a.n_act = c->n_act[d];
@@ -1117,14 +1138,14 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   c->order_hi = hi;
 }
 
-static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
-                        int64_t hi) {
+// Enqueue steps 1-7 (+ the status copy) on `st`.  `ev` = record the timing events (not when
+// the stream is being captured into a graph).
+static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
+                             int64_t hi, bool ev) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size());
-  if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
-  ensure_range(c, lo, hi);
-  HIPCHK(hipEventRecord(c->ev[0], st));
+  if (ev) HIPCHK(hipEventRecord(c->ev[0], st));
 
   // 1. selectors x label sets
   if (uint64_t(c->n_sel) * pb.L)
@@ -1148,13 +1169,17 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
                                            c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
   }
   if (c->Ri && W) {
-    unsigned g = unsigned(uint64_t((W + 3) / 4) * ((c->Ri + IPB_BATCH - 1) / IPB_BATCH));
+    // batch size: as many peers per block as keep >= ~2048 blocks in flight, at most IPB_BATCH
+    const uint64_t wch = (W + 3) / 4;
+    const uint64_t nb_want = (2048 + wch - 1) / wch;
+    const uint32_t bat = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(IPB_BATCH, (c->Ri + nb_want - 1) / nb_want)));
+    unsigned g = unsigned(wch * ((c->Ri + bat - 1) / bat));
     if (pb.may_err)
       k_ip_rows<true><<<g, 256, 0, st>>>(c->Ri, P, W, c->ip_tests.as<DIPTest>(), c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(),
-                                         c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
+                                         c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), bat);
     else
       k_ip_rows<false><<<g, 256, 0, st>>>(c->Ri, P, W, c->ip_tests.as<DIPTest>(), c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(),
-                                          c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
+                                          c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), bat);
   }
   // 3. port matchers x job descriptors
   if (M && pb.descs.size())
@@ -1169,14 +1194,13 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
   for (int d = 0; d < 2; d++) {
     DirDev& dd = c->dir[d];
     if (!dd.n) continue;
-    HIPCHK(hipMemsetAsync(dd.ht_key.p, 0, dd.ht_key.bytes, st));
-    HIPCHK(hipMemsetAsync(dd.ht_rep.p, 0xFF, dd.ht_rep.bytes, st));
+    HIPCHK(hipMemsetAsync(dd.ht_key.p, 0xFF, dd.ht_key.bytes, st));  // keys and reps: one buffer
     MemberArgs ma = member_args(c, d);
     if (!c->n_act[d]) continue;
     k_member<<<grid1(c->n_act[d], 128), 128, 0, st>>>(ma);
     k_classify<<<grid1(c->n_act[d], 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
   }
-  HIPCHK(hipEventRecord(c->ev[1], st));
+  if (ev) HIPCHK(hipEventRecord(c->ev[1], st));
   // 6. class rows
   for (int d = 0; d < 2; d++) {
     DirDev& dd = c->dir[d];
@@ -1216,7 +1240,7 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
       else k_class_rows<true, false><<<g, 256, 0, st>>>(ra);
     }
   }
-  HIPCHK(hipEventRecord(c->ev[2], st));
+  if (ev) HIPCHK(hipEventRecord(c->ev[2], st));
   // 7. emit
   if (hi > lo && K && W) {
     EmitArgs ea{};
@@ -1246,10 +1270,49 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
         default: k_emit<true, 8, true><<<g, 256, 0, st>>>(ea); break;
       }
   }
-  HIPCHK(hipEventRecord(c->ev[3], st));
+  if (ev) HIPCHK(hipEventRecord(c->ev[3], st));
   if (d_status && uint64_t(P) * K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(P) * K, hipMemcpyDeviceToDevice, st));
-  c->timed = true;
+}
+
+static void drop_graph(cyc_ctx* c) {
+  if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+  c->graph_exec = nullptr;
+}
+
+static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
+                        int64_t hi) {
+  Problem& pb = c->pb;
+  const uint32_t P = pb.P, K = pb.K, W = pb.W;
+  if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
+  if (c->order_lo != lo || c->order_hi != hi) drop_graph(c);  // range plan buffers are re-made
+  ensure_range(c, lo, hi);
+  if (c->use_graphs && !pb.may_err) {
+    // The whole pipeline as one hipGraph (captured once per output buffers / row range):
+    // removes the host launch cost of ~16 launches per run (dominant on small problems).
+    const void* key[5] = {d_in, d_eg, d_status, reinterpret_cast<void*>(lo), reinterpret_cast<void*>(hi)};
+    if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
+      drop_graph(c);
+      if (!c->cap_stream) HIPCHK(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
+      hipGraph_t g = nullptr;
+      HIPCHK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
+      enqueue_pipeline(c, c->cap_stream, d_in, d_eg, d_status, lo, hi, false);
+      HIPCHK(hipStreamEndCapture(c->cap_stream, &g));
+      hipError_t ie = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPCHK(ie);
+      memcpy(c->graph_key, key, sizeof(key));
+    }
+    HIPCHK(hipEventRecord(c->ev[0], st));
+    HIPCHK(hipGraphLaunch(c->graph_exec, st));
+    HIPCHK(hipEventRecord(c->ev[3], st));
+    c->timed = true;
+    c->timed_graph = true;
+  } else {
+    enqueue_pipeline(c, st, d_in, d_eg, d_status, lo, hi, true);
+    c->timed = true;
+    c->timed_graph = false;
+  }
 
   // 8. panic path: the first panicking job in job order, as the reference would hit it
   if (pb.may_err) {
@@ -1389,7 +1452,9 @@ void cyc_ctx_destroy(cyc_ctx* c) {
   if (!c) return;
   if (c->stream) {
     (void)hipSetDevice(c->device);
+    drop_graph(c);
     destroy_events(c);
+    if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -1449,6 +1514,7 @@ int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* s
     }
     auto probes = load_probes(json::parse(js, len));
     c->pb = build_problem(c->policy, c->res, probes);
+    drop_graph(c);
     build_identities(c);
     prepare_device(c);
     c->prepared = true;
@@ -1508,9 +1574,11 @@ int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
     HIPCHK(hipEventSynchronize(c->ev[3]));
     float a = 0, b = 0, r = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[3]));
-    HIPCHK(hipEventElapsedTime(&b, c->ev[2], c->ev[3]));
-    HIPCHK(hipEventElapsedTime(&r, c->ev[1], c->ev[2]));
-    double v[3] = {a, b, r};
+    if (!c->timed_graph) {
+      HIPCHK(hipEventElapsedTime(&b, c->ev[2], c->ev[3]));
+      HIPCHK(hipEventElapsedTime(&r, c->ev[1], c->ev[2]));
+    }
+    double v[3] = {a, c->timed_graph ? -1.0 : b, c->timed_graph ? -1.0 : r};
     for (int i = 0; i < n && i < 3; i++) ms[i] = v[i];
     return (int)CYC_OK;
   });
@@ -1520,6 +1588,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return CYC_ERR_ARG;
   if (std::string(name) == "emit_variant") {
     c->emit_variant = int(value);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
+  if (std::string(name) == "graphs") {
+    c->use_graphs = value != 0;
+    drop_graph(c);
     return (int)CYC_OK;
   }
   return fail(c, CYC_ERR_ARG, std::string("unknown option ") + name);

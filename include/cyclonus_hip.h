@@ -109,7 +109,9 @@ int cyc_probe_run_host(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_
  * stream: [0] whole pipeline, [1] emit kernel (the HBM-roofline kernel), [2] class rows. */
 int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 
-/* Tuning knobs (no effect on results): "emit_variant" 0..3 selects the emit store pattern. */
+/* Tuning knobs (no effect on results): "emit_variant" 0..5 selects the emit store pattern;
+ * "graphs" (default 1) replays the pipeline as one captured hipGraph when the inputs cannot
+ * panic (then cyc_last_timings reports only the whole-pipeline time). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
 
 /* Single-cell API (policy.go:131-174): traffic_json is a JSON array of matcher.Traffic objects;

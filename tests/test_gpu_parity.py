@@ -213,3 +213,25 @@ def test_config5_generate_sweep_batched(gpu):
             k = want[0].shape[1]
             got = (got[0][:, :k], got[1][:, :k], got[2][:, :k])
         assert_same(want, got, f"step {b} ({step['description']})")
+
+
+def test_graph_and_eager_paths_agree(gpu):
+    import torch
+
+    eng = Engine(0)
+    for seed in range(30):
+        pols, res, probes = random_problem(30_000 + seed, n_pods=50)
+        eng.build_policies(pols).load_resources(res)
+        sh = eng.prepare(probes)
+        P, K, W = sh["pods"], sh["slots"], sh["words"]
+        outs = []
+        for graphs in (0, 1, 1):
+            eng.set_option("graphs", graphs)
+            d_in = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
+            d_eg = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
+            d_st = torch.zeros((P, K), dtype=torch.uint8, device="cuda")
+            eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            outs.append((d_in.cpu(), d_eg.cpu(), d_st.cpu()))
+        for o in outs[1:]:
+            assert all(torch.equal(a, b) for a, b in zip(outs[0], o)), seed
