@@ -181,8 +181,11 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = cells / (dt / args.steps)
 
-    emit_bytes = 2 * rows * K * W * 8  # both planes of this rank's rows, written once
-    achieved = emit_bytes / (emit_ms * 1e-3) / 1e9
+    # k_emit launches once per plane (ingress, egress): per launch it writes one plane of this
+    # rank's rows once (rows x K x W x 8 B = 2 bits per cell); emit_ms covers both launches
+    emit_bytes = rows * K * W * 8
+    emit_launch_ms = emit_ms / 2
+    achieved = emit_bytes / (emit_launch_ms * 1e-3) / 1e9
 
     # HBM traffic of k_emit from the committed PMC passes for this same workload (rocprofv3
     # --pmc FETCH_SIZE / WRITE_SIZE, corrected per MI355X_MICROARCH.md; scripts/pmc_summary.py)
@@ -230,10 +233,11 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": emit_bytes,
-                "emit_ms": emit_ms,
+                "emit_ms_per_launch": emit_launch_ms,
+                "launches_per_step": 2,
                 "fill_ceiling_GBs": fill_gbs,
             },
-            "launch": "one captured hipGraph per step (cyc_set_option graphs=1)",
+            "launch": "one captured hipGraph per step (cyc_set_option graphs=1): shared front, then ingress and egress branches on two streams",
             "pipeline_ms": {"total": pipe_ms, "emit": emit_ms, "class_rows": rows_ms, "front": pipe_ms - emit_ms - rows_ms},
         }
         if world == 1 and not args.no_cpu_baseline:

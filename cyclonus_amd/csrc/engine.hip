@@ -238,6 +238,102 @@ __global__ __launch_bounds__(256) void k_ip_rows(uint32_t Ri, uint32_t P, uint32
   }
 }
 
+// Fast IP rows (no-panic inputs: every pod address parses).  One wave = (IP peer, 64
+// consecutive words); lane = word.  A CIDR (and each except) is an address interval of its
+// family, so a word is decided per family from the [min, max] address of its pods of that family
+// (an IPv4 network never contains an IPv6 address and vice versa, ippeermatcher / net.Contains):
+// fully outside, fully inside (then each except of the family fully out / fully in), or mixed.
+// Only mixed words fall back to the lane-per-pod test.  Pods numbered in address order (the
+// usual case: addresses handed out per namespace) leave almost no mixed words.
+struct DWordIP {
+  uint32_t min4, max4;         // over the word's IPv4 pods
+  uint64_t m4, m6;             // bits of the IPv4 / IPv6 pods
+  uint32_t min6[4], max6[4];   // over the word's IPv6 pods (big-endian 128-bit)
+  uint64_t pad;
+};
+static_assert(sizeof(DWordIP) == 64, "DWordIP is one 64-byte record");
+
+__device__ __forceinline__ bool lt128(const uint32_t* a, const uint32_t* b) {
+  for (int i = 0; i < 4; i++)
+    if (a[i] != b[i]) return a[i] < b[i];
+  return false;
+}
+
+// Position of the interval [mn, mx] against the network c of the same family:
+// 0 disjoint, 1 inside, 2 straddles.
+__device__ __forceinline__ uint32_t span_vs_cidr4(uint32_t mn, uint32_t mx, const DCidr& c) {
+  const uint32_t lo = c.net[3] & c.mask[3], hi = lo | ~c.mask[3];
+  if (mx < lo || mn > hi) return 0;
+  return (mn >= lo && mx <= hi) ? 1 : 2;
+}
+__device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint32_t* mx, const DCidr& c) {
+  uint32_t lo[4], hi[4];
+  for (int i = 0; i < 4; i++) {
+    lo[i] = c.net[i] & c.mask[i];
+    hi[i] = lo[i] | ~c.mask[i];
+  }
+  if (lt128(mx, lo) || lt128(hi, mn)) return 0;
+  return (!lt128(mn, lo) && !lt128(hi, mx)) ? 1 : 2;
+}
+
+__global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
+                                                      const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
+                                                      const DWordIP* __restrict__ words, uint64_t* __restrict__ PM) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t chunks = (W + 63) / 64;
+  const uint32_t r = gw / chunks;
+  if (r >= Ri) return;
+  const DIPTest t = tests[r];
+  const uint32_t w = (gw % chunks) * 64 + lane;
+  const bool valid = w < W;
+  bool uniform = true;
+  uint64_t res = 0;
+  if (valid) {
+    const DWordIP wd = words[w];
+    const bool v4 = t.cidr.fam == 4;
+    const uint64_t fm = v4 ? wd.m4 : wd.m6;  // pods of the network's family; the others never match
+    if (fm) {
+      uint32_t pos = v4 ? span_vs_cidr4(wd.min4, wd.max4, t.cidr) : span_vs_cidr6(wd.min6, wd.max6, t.cidr);
+      if (pos == 2) uniform = false;
+      else if (pos == 1) {
+        res = fm;
+        for (uint32_t e = 0; e < t.excnt; e++) {
+          const DCidr x = ip_ex[t.exoff + e];
+          if (x.fam != t.cidr.fam) continue;
+          uint32_t xp = v4 ? span_vs_cidr4(wd.min4, wd.max4, x) : span_vs_cidr6(wd.min6, wd.max6, x);
+          if (xp == 0) continue;
+          if (xp == 1) res = 0;
+          else uniform = false;
+          break;
+        }
+      }
+    }
+  }
+  if (valid && uniform) PM[uint64_t(t.peer) * W + w] = res;
+  uint64_t mixed = __ballot(valid && !uniform);
+  while (mixed) {
+    const uint32_t wl = __ffsll((unsigned long long)mixed) - 1;
+    mixed &= mixed - 1;
+    const uint32_t ww = (gw % chunks) * 64 + wl;
+    const uint32_t q = ww * 64 + lane;
+    uint32_t o = 0;
+    if (q < P) {
+      const DIP ip = pod_ip[q];
+      if (cidr_contains(t.cidr, ip)) {
+        o = 1;
+        for (uint32_t e = 0; e < t.excnt; e++)
+          if (cidr_contains(ip_ex[t.exoff + e], ip)) {
+            o = 0;
+            break;
+          }
+      }
+    }
+    const uint64_t m = __ballot(o == 1);
+    if (lane == 0) PM[uint64_t(t.peer) * W + ww] = m;
+  }
+}
+
 // PortMatcher.Allows(ResolvedPort, ResolvedPortName, Protocol) — portmatcher.go:10-92, 190-199.
 __global__ void k_portok(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents, const DDesc* descs,
                          uint8_t* __restrict__ portok) {
@@ -544,65 +640,68 @@ struct EmitArgs {
   uint32_t n_rows;            // pods in [row_lo, row_hi)
   uint32_t row_lo;
   uint32_t per_xcd;
-  const uint32_t* order;      // pods in [row_lo,row_hi) clustered by class
-  const uint32_t *pod_iid, *pod_eid, *class_in, *class_eg;
-  const uint64_t *A_in, *A_eg;
-  uint64_t *out_in, *out_eg;
+  const uint32_t* order;      // pods in [row_lo,row_hi) clustered by this direction's class
+  const uint32_t *pod_id, *class_of;
+  const uint64_t* A;
+  uint64_t* out;
   uint64_t row_words;         // K * W
+  uint32_t blocks_per_xcd;    // persistent launch: blocks of one XCD stride over its row segment
 };
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
-// VEC: 16-byte accesses (pitch even); UNROLL: 16-byte chunks per thread per plane kept in
-// flight before the stores; NT: non-temporal stores (the planes are write-once streams).
-template <bool VEC, int UNROLL, bool NT, bool XCD = true>
-__global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
-  uint32_t b = blockIdx.x;
-  uint32_t r = XCD ? (b & 7) * a.per_xcd + (b >> 3) : b;
-  if (r >= a.n_rows) return;
-  uint32_t p = a.order[r];
-  uint64_t orow = uint64_t(p - a.row_lo) * a.row_words;
-  const uint64_t* src_in = a.A_in + uint64_t(a.class_in[a.pod_iid[p]]) * a.row_words;
-  const uint64_t* src_eg = a.A_eg + uint64_t(a.class_eg[a.pod_eid[p]]) * a.row_words;
-  uint64_t* dst_in = a.out_in + orow;
-  uint64_t* dst_eg = a.out_eg + orow;
+template <bool VEC, int UNROLL, bool NT>
+__device__ __forceinline__ void emit_row(const EmitArgs& a, uint32_t p) {
+  const uint64_t* src = a.A + uint64_t(a.class_of[a.pod_id[p]]) * a.row_words;
+  uint64_t* dst = a.out + uint64_t(p - a.row_lo) * a.row_words;
   if (VEC) {
     const uint64_t n2 = a.row_words / 2;
-    const u64x2* si = reinterpret_cast<const u64x2*>(src_in);
-    const u64x2* se = reinterpret_cast<const u64x2*>(src_eg);
-    u64x2* di = reinterpret_cast<u64x2*>(dst_in);
-    u64x2* de = reinterpret_cast<u64x2*>(dst_eg);
+    const u64x2* si = reinterpret_cast<const u64x2*>(src);
+    u64x2* di = reinterpret_cast<u64x2*>(dst);
     const uint64_t step = uint64_t(blockDim.x) * UNROLL;
     for (uint64_t x0 = threadIdx.x; x0 < n2; x0 += step) {
-      u64x2 vi[UNROLL], ve[UNROLL];
+      u64x2 v[UNROLL];
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) {
         uint64_t x = x0 + uint64_t(u) * blockDim.x;
-        if (x < n2) {
-          vi[u] = si[x];
-          ve[u] = se[x];
-        }
+        if (x < n2) v[u] = si[x];
       }
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) {
         uint64_t x = x0 + uint64_t(u) * blockDim.x;
         if (x < n2) {
-          if (NT) {
-            __builtin_nontemporal_store(vi[u], &di[x]);
-            __builtin_nontemporal_store(ve[u], &de[x]);
-          } else {
-            di[x] = vi[u];
-            de[x] = ve[u];
-          }
+          if (NT) __builtin_nontemporal_store(v[u], &di[x]);
+          else di[x] = v[u];
         }
       }
     }
   } else {
-    for (uint64_t x = threadIdx.x; x < a.row_words; x += blockDim.x) {
-      dst_in[x] = src_in[x];
-      dst_eg[x] = src_eg[x];
-    }
+    for (uint64_t x = threadIdx.x; x < a.row_words; x += blockDim.x) dst[x] = src[x];
   }
+}
+
+// One plane: row r of the output = its pod's class row.  VEC: 16-byte accesses (pitch even);
+// UNROLL: 16-byte chunks per thread kept in flight before the stores; NT: non-temporal stores
+// (the planes are write-once streams); XCD: consecutive (class-clustered) rows go to the same
+// XCD (blocks b, b+8, ... share one), so each class row is read from HBM about once per XCD.
+// Default grid = one block per row; option "emit_blocks" bounds it (persistent blocks striding
+// over their XCD's row segment) to leave CU slots to the other graph branch — measured slower
+// on config #3/#4 (profiles/r01_emit_sweep.txt), so off by default.
+template <bool VEC, int UNROLL, bool NT, bool XCD = true>
+__global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
+  const uint32_t b = blockIdx.x;
+  uint32_t r, r_end, r_step;
+  if (XCD) {  // block b runs on XCD b % 8: rows [x*per_xcd, (x+1)*per_xcd), stride blocks_per_xcd
+    const uint32_t x = b & 7;
+    r = x * a.per_xcd + (b >> 3);
+    r_end = min(a.n_rows, (x + 1) * a.per_xcd);
+    r_step = a.blocks_per_xcd;
+  } else {
+    r = b;
+    r_end = a.n_rows;
+    r_step = a.blocks_per_xcd * 8;
+  }
+  for (; r < r_end; r += r_step) emit_row<VEC, UNROLL, NT>(a, a.order[r]);
 }
 
 // ---------------------------------------------------------------- panic path (rare)
@@ -830,16 +929,20 @@ struct cyc_ctx {
   // device tables
   DevBuf ls_off, ls_key, ls_val, sel_off, reqs, req_vals, pod_ns, pod_ls, pod_nsls, pod_ip, cidrs, ipbs, ipb_ex, pms,
       pents, peers, descs, slot_desc, slot_status, slot_cfg, slot_idx;
-  DevBuf selres, PM, ER, portok, VALID, DESCW, DM, first_err, order;
+  DevBuf selres, PM, ER, portok, VALID, DESCW, DM, first_err, order[2];
   // peer-row stage: pod peers in identity space + per-word identity runs; IP peers per pod
-  DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido;
+  DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words;
   uint32_t Rp = 0, Ri = 0;
+  uint32_t rp_off[3] = {0, 0, 0}, ri_off[3] = {0, 0, 0};  // per-direction sub-lists (ingress, egress)
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
   DevBuf act[2], sel_list;
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
   int emit_variant = 0;  // tuning knob (cyc_set_option "emit_variant")
+  int64_t emit_blocks = 0;  // cyc_set_option "emit_blocks": persistent emit grid (0 = a block per row)
   bool use_graphs = true;  // cyc_set_option "graphs"
-  hipStream_t cap_stream = nullptr;
+  bool graph_branches = true;  // cyc_set_option "graph_branches": ingress / egress as two graph branches
+  hipStream_t cap_stream = nullptr, cap_stream2 = nullptr;  // graph capture: ingress / egress branches
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   const void* graph_key[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   bool timed_graph = false;
@@ -993,6 +1096,29 @@ static void prepare_device(cyc_ctx* c) {
     upload(c->run_e, pl.run_e);
     upload(c->run_mask, pl.run_mask);
     upload(c->id_nsls, c->ids[1].nsls);
+    {  // per-word, per-family address intervals for k_ip_rows_fast
+      std::vector<DWordIP> wi(pb.W);
+      for (uint32_t w = 0; w < pb.W; w++) {
+        DWordIP d{};
+        d.min4 = 0xFFFFFFFFu;
+        for (int i = 0; i < 4; i++) d.min6[i] = 0xFFFFFFFFu;
+        for (uint32_t q = w * 64; q < std::min<uint32_t>(pb.P, w * 64 + 64); q++) {
+          const DIP& ip = pb.pod_ip[q];
+          if (!ip.valid) continue;  // only with may_err, where the fast kernel is not used
+          if (ip.fam == 4) {
+            d.m4 |= 1ull << (q - w * 64);
+            d.min4 = std::min(d.min4, ip.w[3]);
+            d.max4 = std::max(d.max4, ip.w[3]);
+          } else {
+            d.m6 |= 1ull << (q - w * 64);
+            if (std::lexicographical_compare(ip.w, ip.w + 4, d.min6, d.min6 + 4)) std::copy(ip.w, ip.w + 4, d.min6);
+            if (std::lexicographical_compare(d.max6, d.max6 + 4, ip.w, ip.w + 4)) std::copy(ip.w, ip.w + 4, d.max6);
+          }
+        }
+        wi[w] = d;
+      }
+      upload(c->ip_words, wi);
+    }
     c->ido.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * c->ids[1].ns.size(), 16));
   }
   c->portok.alloc(std::max<uint64_t>(pb.pms.size() * D, 16));
@@ -1065,15 +1191,18 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
 static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   if (c->order_lo == lo && c->order_hi == hi) return;
   Problem& pb = c->pb;
-  std::vector<uint32_t> ord(size_t(hi - lo));
-  std::iota(ord.begin(), ord.end(), uint32_t(lo));
-  const auto& iin = c->ids[0].of_pod;
-  const auto& ieg = c->ids[1].of_pod;
-  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
-    return iin[x] != iin[y] ? iin[x] < iin[y] : ieg[x] < ieg[y];
-  });
-  upload(c->order, ord);
-  std::vector<uint8_t> peer_needed(pb.peers.size(), 0);
+  for (int d = 0; d < 2; d++) {  // emit row order: clustered by this direction's identity
+    std::vector<uint32_t> ord(size_t(hi - lo));
+    std::iota(ord.begin(), ord.end(), uint32_t(lo));
+    const auto& i1 = c->ids[d].of_pod;
+    const auto& i2 = c->ids[1 - d].of_pod;
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](uint32_t x, uint32_t y) { return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y]; });
+    upload(c->order[d], ord);
+  }
+  std::vector<uint8_t> peer_needed(pb.peers.size(), 0), peer_dir(pb.peers.size(), 0);
+  for (const DTarget& t : pb.tgt[1])
+    for (uint32_t j = t.poff; j < t.poff + t.pcnt; j++) peer_dir[j] = 1;
   for (int d = 0; d < 2; d++) {
     const Identities& I = c->ids[d];
     std::vector<uint8_t> used(I.ns.size(), 0);
@@ -1121,13 +1250,19 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   upload(c->sel_list, sl);
   std::vector<uint32_t> pp, ip;
   std::vector<DIPTest> tests;
-  for (uint32_t j : c->plan.pod_peers)
-    if (peer_needed[j]) pp.push_back(j);
-  for (size_t r = 0; r < c->plan.ip_peers.size(); r++)
-    if (peer_needed[c->plan.ip_peers[r]]) {
-      ip.push_back(c->plan.ip_peers[r]);
-      tests.push_back(c->plan.ip_tests[r]);
-    }
+  for (int d = 0; d < 2; d++) {  // ingress peers first, then egress: one sub-list per branch
+    c->rp_off[d] = uint32_t(pp.size());
+    c->ri_off[d] = uint32_t(ip.size());
+    for (uint32_t j : c->plan.pod_peers)
+      if (peer_needed[j] && peer_dir[j] == d) pp.push_back(j);
+    for (size_t r = 0; r < c->plan.ip_peers.size(); r++)
+      if (peer_needed[c->plan.ip_peers[r]] && peer_dir[c->plan.ip_peers[r]] == d) {
+        ip.push_back(c->plan.ip_peers[r]);
+        tests.push_back(c->plan.ip_tests[r]);
+      }
+  }
+  c->rp_off[2] = uint32_t(pp.size());
+  c->ri_off[2] = uint32_t(ip.size());
   c->Rp = uint32_t(pp.size());
   c->Ri = uint32_t(ip.size());
   upload(c->pod_peers, pp);
@@ -1138,49 +1273,18 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   c->order_hi = hi;
 }
 
-// Enqueue steps 1-7 (+ the status copy) on `st`.  `ev` = record the timing events (not when
-// the stream is being captured into a graph).
-static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
-                             int64_t hi, bool ev) {
+// Pipeline pieces.  Steps 1, 3, 4 are shared; steps 2 and 5-7 run per direction (ingress peers,
+// targets, class rows and plane are disjoint from egress ones), so the two directions can run
+// as two independent branches: one direction's front hides under the other's HBM-bound emit.
+static void enq_common(cyc_ctx* c, hipStream_t st) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size());
-  if (ev) HIPCHK(hipEventRecord(c->ev[0], st));
-
   // 1. selectors x label sets
   if (uint64_t(c->n_sel) * pb.L)
     k_selectors<<<grid1(uint64_t(c->n_sel) * pb.L, 256), 256, 0, st>>>(
         c->n_sel, pb.L, c->sel_off.as<uint32_t>(), c->reqs.as<DReq>(), c->req_vals.as<uint32_t>(), c->ls_off.as<uint32_t>(),
         c->ls_key.as<uint32_t>(), c->ls_val.as<uint32_t>(), c->selres.as<uint8_t>(), c->sel_list.as<uint32_t>());
-  // 2. peer rows: pod peers in identity space, expanded over word runs; IP peers per pod
-  const uint32_t E = c->dir[1].n;
-  if (c->Rp && E && W) {
-    k_peer_ident<<<grid1(uint64_t(c->Rp) * E, 256), 256, 0, st>>>(
-        c->Rp, E, c->pod_peers.as<uint32_t>(), c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
-        c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(), c->ido.as<uint8_t>());
-    unsigned g = unsigned(uint64_t((W + 255) / 256) * c->Rp);
-    if (pb.may_err)
-      k_pod_rows<true><<<g, 256, 0, st>>>(c->Rp, E, W, c->pod_peers.as<uint32_t>(), c->ido.as<uint8_t>(),
-                                          c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(), c->run_mask.as<uint64_t>(),
-                                          c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
-    else
-      k_pod_rows<false><<<g, 256, 0, st>>>(c->Rp, E, W, c->pod_peers.as<uint32_t>(), c->ido.as<uint8_t>(),
-                                           c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(), c->run_mask.as<uint64_t>(),
-                                           c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
-  }
-  if (c->Ri && W) {
-    // batch size: as many peers per block as keep >= ~2048 blocks in flight, at most IPB_BATCH
-    const uint64_t wch = (W + 3) / 4;
-    const uint64_t nb_want = (2048 + wch - 1) / wch;
-    const uint32_t bat = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(IPB_BATCH, (c->Ri + nb_want - 1) / nb_want)));
-    unsigned g = unsigned(wch * ((c->Ri + bat - 1) / bat));
-    if (pb.may_err)
-      k_ip_rows<true><<<g, 256, 0, st>>>(c->Ri, P, W, c->ip_tests.as<DIPTest>(), c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(),
-                                         c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), bat);
-    else
-      k_ip_rows<false><<<g, 256, 0, st>>>(c->Ri, P, W, c->ip_tests.as<DIPTest>(), c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(),
-                                          c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), bat);
-  }
   // 3. port matchers x job descriptors
   if (M && pb.descs.size())
     k_portok<<<grid1(uint64_t(M) * D, 256), 256, 0, st>>>(M, D, c->pms.as<DPortM>(), c->pents.as<DPortEntry>(),
@@ -1190,89 +1294,170 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
     k_slot_words<<<unsigned((uint64_t(K) * W + 3) / 4), 256, 0, st>>>(
         P, K, W, D, c->slot_desc.as<int32_t>(), c->slot_status.as<uint8_t>(), c->VALID.as<uint64_t>(),
         c->DESCW.as<int32_t>(), c->DM.as<uint64_t>());
-  // 5. membership + classes per direction
-  for (int d = 0; d < 2; d++) {
-    DirDev& dd = c->dir[d];
-    if (!dd.n) continue;
-    HIPCHK(hipMemsetAsync(dd.ht_key.p, 0xFF, dd.ht_key.bytes, st));  // keys and reps: one buffer
-    MemberArgs ma = member_args(c, d);
-    if (!c->n_act[d]) continue;
-    k_member<<<grid1(c->n_act[d], 128), 128, 0, st>>>(ma);
-    k_classify<<<grid1(c->n_act[d], 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
+}
+
+// 2. peer rows of direction d's peers: pod peers in identity space, expanded over word runs;
+// IP peers per pod
+static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st) {
+  Problem& pb = c->pb;
+  const uint32_t P = pb.P, W = pb.W;
+  const uint32_t E = c->dir[1].n;
+  const uint32_t r0 = c->rp_off[d], Rp = c->rp_off[d + 1] - r0;
+  if (Rp && E && W) {
+    const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
+    uint8_t* ido = c->ido.as<uint8_t>() + uint64_t(r0) * E;
+    k_peer_ident<<<grid1(uint64_t(Rp) * E, 256), 256, 0, st>>>(Rp, E, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(),
+                                                               pb.L, c->dir[1].id_ns.as<uint32_t>(),
+                                                               c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(), ido);
+    unsigned g = unsigned(uint64_t((W + 255) / 256) * Rp);
+    if (pb.may_err)
+      k_pod_rows<true><<<g, 256, 0, st>>>(Rp, E, W, plist, ido, c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(),
+                                          c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
+    else
+      k_pod_rows<false><<<g, 256, 0, st>>>(Rp, E, W, plist, ido, c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(),
+                                           c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
   }
-  if (ev) HIPCHK(hipEventRecord(c->ev[1], st));
-  // 6. class rows
-  for (int d = 0; d < 2; d++) {
-    DirDev& dd = c->dir[d];
-    if (!dd.n || !K || !W) continue;
-    RowArgs ra{};
-    ra.tgt = dd.tgt.as<DTarget>();
-    ra.peers = c->peers.as<DPeer>();
-    ra.PM = c->PM.as<uint64_t>();
-    ra.ER = c->ER.as<uint64_t>();
-    ra.portok = c->portok.as<uint8_t>();
-    ra.D = D;
-    ra.n_ident = dd.n;
-    ra.act = c->act[d].as<uint32_t>();
-    ra.n_act = c->n_act[d];
-    ra.K = K;
-    ra.W = W;
-    ra.P = P;
-    ra.class_of = dd.class_of.as<uint32_t>();
-    ra.cnt = dd.cnt.as<uint32_t>();
-    ra.list_off = dd.list_off.as<uint32_t>();
-    ra.list = dd.list.as<uint32_t>();
-    ra.id_err = dd.err.as<uint8_t>();
-    ra.id_desc = dd.id_desc.as<int32_t>();
-    ra.id_status = dd.id_status.as<uint8_t>();
-    ra.VALID = c->VALID.as<uint64_t>();
-    ra.DESCW = c->DESCW.as<int32_t>();
-    ra.DM = c->DM.as<uint64_t>();
-    ra.A = dd.A.as<uint64_t>();
-    ra.AE = pb.may_err ? dd.AE.as<uint64_t>() : nullptr;
-    if (!c->n_act[d]) continue;
-    unsigned g = unsigned(uint64_t((W + 255) / 256) * c->n_act[d] * ((K + KC - 1) / KC));
-    if (d == 0) {
-      if (pb.may_err) k_class_rows<false, true><<<g, 256, 0, st>>>(ra);
-      else k_class_rows<false, false><<<g, 256, 0, st>>>(ra);
+  const uint32_t i0 = c->ri_off[d], Ri = c->ri_off[d + 1] - i0;
+  if (Ri && W) {
+    const DIPTest* tests = c->ip_tests.as<DIPTest>() + i0;
+    if (pb.may_err) {
+      // batch size: as many peers per block as keep >= ~2048 blocks in flight, at most IPB_BATCH
+      const uint64_t wch = (W + 3) / 4;
+      const uint64_t nb_want = (2048 + wch - 1) / wch;
+      const uint32_t bat = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(IPB_BATCH, (Ri + nb_want - 1) / nb_want)));
+      unsigned g = unsigned(wch * ((Ri + bat - 1) / bat));
+      k_ip_rows<true><<<g, 256, 0, st>>>(Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->PM.as<uint64_t>(),
+                                         c->ER.as<uint64_t>(), bat);
     } else {
-      if (pb.may_err) k_class_rows<true, true><<<g, 256, 0, st>>>(ra);
-      else k_class_rows<true, false><<<g, 256, 0, st>>>(ra);
+      k_ip_rows_fast<<<unsigned((uint64_t((W + 63) / 64) * Ri + 3) / 4), 256, 0, st>>>(
+          Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>());
     }
   }
-  if (ev) HIPCHK(hipEventRecord(c->ev[2], st));
-  // 7. emit
-  if (hi > lo && K && W) {
-    EmitArgs ea{};
-    ea.n_rows = uint32_t(hi - lo);
-    ea.row_lo = uint32_t(lo);
-    ea.order = c->order.as<uint32_t>();
-    ea.pod_iid = c->dir[0].pod_id.as<uint32_t>();
-    ea.pod_eid = c->dir[1].pod_id.as<uint32_t>();
-    ea.class_in = c->dir[0].class_of.as<uint32_t>();
-    ea.class_eg = c->dir[1].class_of.as<uint32_t>();
-    ea.A_in = c->dir[0].A.as<uint64_t>();
-    ea.A_eg = c->dir[1].A.as<uint64_t>();
-    ea.out_in = d_in;
-    ea.out_eg = d_eg;
-    ea.row_words = uint64_t(K) * W;
-    ea.per_xcd = (ea.n_rows + 7) / 8;
-    bool vec = (ea.row_words % 2 == 0) && (reinterpret_cast<uintptr_t>(d_in) % 16 == 0) &&
-               (reinterpret_cast<uintptr_t>(d_eg) % 16 == 0);
-    unsigned g = ea.per_xcd * 8;
-    if (!vec) k_emit<false, 1, false><<<g, 256, 0, st>>>(ea);
-    else switch (c->emit_variant) {  // 0 = default (measured fastest: UNROLL 8, nt, XCD-mapped)
-        case 1: k_emit<true, 1, true><<<g, 256, 0, st>>>(ea); break;
-        case 2: k_emit<true, 4, false><<<g, 256, 0, st>>>(ea); break;
-        case 3: k_emit<true, 4, true><<<g, 256, 0, st>>>(ea); break;
-        case 4: k_emit<true, 16, true><<<g, 256, 0, st>>>(ea); break;
-        case 5: k_emit<true, 8, true, false><<<g, 256, 0, st>>>(ea); break;
-        default: k_emit<true, 8, true><<<g, 256, 0, st>>>(ea); break;
-      }
+}
+
+// 5. membership + classes of direction d
+static void enq_member(cyc_ctx* c, int d, hipStream_t st) {
+  DirDev& dd = c->dir[d];
+  if (!dd.n) return;
+  HIPCHK(hipMemsetAsync(dd.ht_key.p, 0xFF, dd.ht_key.bytes, st));  // keys and reps: one buffer
+  MemberArgs ma = member_args(c, d);
+  if (!c->n_act[d]) return;
+  k_member<<<grid1(c->n_act[d], 128), 128, 0, st>>>(ma);
+  k_classify<<<grid1(c->n_act[d], 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
+}
+
+// 6. class rows of direction d
+static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
+  Problem& pb = c->pb;
+  const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
+  DirDev& dd = c->dir[d];
+  if (!dd.n || !K || !W || !c->n_act[d]) return;
+  RowArgs ra{};
+  ra.tgt = dd.tgt.as<DTarget>();
+  ra.peers = c->peers.as<DPeer>();
+  ra.PM = c->PM.as<uint64_t>();
+  ra.ER = c->ER.as<uint64_t>();
+  ra.portok = c->portok.as<uint8_t>();
+  ra.D = D;
+  ra.n_ident = dd.n;
+  ra.act = c->act[d].as<uint32_t>();
+  ra.n_act = c->n_act[d];
+  ra.K = K;
+  ra.W = W;
+  ra.P = P;
+  ra.class_of = dd.class_of.as<uint32_t>();
+  ra.cnt = dd.cnt.as<uint32_t>();
+  ra.list_off = dd.list_off.as<uint32_t>();
+  ra.list = dd.list.as<uint32_t>();
+  ra.id_err = dd.err.as<uint8_t>();
+  ra.id_desc = dd.id_desc.as<int32_t>();
+  ra.id_status = dd.id_status.as<uint8_t>();
+  ra.VALID = c->VALID.as<uint64_t>();
+  ra.DESCW = c->DESCW.as<int32_t>();
+  ra.DM = c->DM.as<uint64_t>();
+  ra.A = dd.A.as<uint64_t>();
+  ra.AE = pb.may_err ? dd.AE.as<uint64_t>() : nullptr;
+  unsigned g = unsigned(uint64_t((W + 255) / 256) * c->n_act[d] * ((K + KC - 1) / KC));
+  if (d == 0) {
+    if (pb.may_err) k_class_rows<false, true><<<g, 256, 0, st>>>(ra);
+    else k_class_rows<false, false><<<g, 256, 0, st>>>(ra);
+  } else {
+    if (pb.may_err) k_class_rows<true, true><<<g, 256, 0, st>>>(ra);
+    else k_class_rows<true, false><<<g, 256, 0, st>>>(ra);
   }
-  if (ev) HIPCHK(hipEventRecord(c->ev[3], st));
-  if (d_status && uint64_t(P) * K)
-    HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(P) * K, hipMemcpyDeviceToDevice, st));
+}
+
+// 7. emit of direction d's plane
+static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t lo, int64_t hi) {
+  Problem& pb = c->pb;
+  const uint32_t K = pb.K, W = pb.W;
+  if (hi <= lo || !K || !W) return;
+  EmitArgs ea{};
+  ea.n_rows = uint32_t(hi - lo);
+  ea.row_lo = uint32_t(lo);
+  ea.order = c->order[d].as<uint32_t>();
+  ea.pod_id = c->dir[d].pod_id.as<uint32_t>();
+  ea.class_of = c->dir[d].class_of.as<uint32_t>();
+  ea.A = c->dir[d].A.as<uint64_t>();
+  ea.out = out;
+  ea.row_words = uint64_t(K) * W;
+  ea.per_xcd = (ea.n_rows + 7) / 8;
+  // persistent grid: emit_blocks per launch (0 = one block per row)
+  ea.blocks_per_xcd = c->emit_blocks ? std::min<uint32_t>(ea.per_xcd, std::max<uint32_t>(1, uint32_t(c->emit_blocks / 8)))
+                                     : ea.per_xcd;
+  bool vec = (ea.row_words % 2 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+  unsigned g = ea.blocks_per_xcd * 8;
+  if (!vec) k_emit<false, 1, false><<<g, 256, 0, st>>>(ea);
+  else switch (c->emit_variant) {  // 0 = default (measured fastest, profiles/r01_emit_sweep.txt:
+                                   // UNROLL 16 x 16 B in flight per thread, nt stores, XCD-mapped)
+      case 1: k_emit<true, 1, true><<<g, 256, 0, st>>>(ea); break;
+      case 2: k_emit<true, 4, false><<<g, 256, 0, st>>>(ea); break;
+      case 3: k_emit<true, 4, true><<<g, 256, 0, st>>>(ea); break;
+      case 4: k_emit<true, 8, true><<<g, 256, 0, st>>>(ea); break;
+      case 5: k_emit<true, 16, true, false><<<g, 256, 0, st>>>(ea); break;
+      default: k_emit<true, 16, true><<<g, 256, 0, st>>>(ea); break;
+    }
+}
+
+// Eager launch, in phase order with the timing events: [0] start, [1] after the front (peer
+// rows, classes), [2] after the class rows, [3] after both emits.
+static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
+                             int64_t hi) {
+  Problem& pb = c->pb;
+  HIPCHK(hipEventRecord(c->ev[0], st));
+  enq_common(c, st);
+  for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st);
+  for (int d = 0; d < 2; d++) enq_member(c, d, st);
+  HIPCHK(hipEventRecord(c->ev[1], st));
+  for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
+  HIPCHK(hipEventRecord(c->ev[2], st));
+  enq_emit(c, 0, st, d_in, lo, hi);
+  enq_emit(c, 1, st, d_eg, lo, hi);
+  HIPCHK(hipEventRecord(c->ev[3], st));
+  if (d_status && uint64_t(pb.P) * pb.K)
+    HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
+}
+
+// Graph capture: shared front on st, then the ingress branch on st and the egress branch on st2
+// (fork / join through events, recorded into the graph as dependencies).
+static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status,
+                             int64_t lo, int64_t hi) {
+  Problem& pb = c->pb;
+  if (!c->graph_branches) st2 = st;
+  enq_common(c, st);
+  HIPCHK(hipEventRecord(c->fork_ev, st));
+  HIPCHK(hipStreamWaitEvent(st2, c->fork_ev, 0));
+  for (int d = 0; d < 2; d++) {
+    hipStream_t s = d ? st2 : st;
+    enq_peer_rows(c, d, s);
+    enq_member(c, d, s);
+    enq_class_rows(c, d, s);
+    enq_emit(c, d, s, d ? d_eg : d_in, lo, hi);
+  }
+  HIPCHK(hipEventRecord(c->join_ev, st2));
+  HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
+  if (d_status && uint64_t(pb.P) * pb.K)
+    HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
 }
 
 static void drop_graph(cyc_ctx* c) {
@@ -1293,10 +1478,15 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     const void* key[5] = {d_in, d_eg, d_status, reinterpret_cast<void*>(lo), reinterpret_cast<void*>(hi)};
     if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
       drop_graph(c);
-      if (!c->cap_stream) HIPCHK(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
+      if (!c->cap_stream) {
+        HIPCHK(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->cap_stream2, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+      }
       hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
-      enqueue_pipeline(c, c->cap_stream, d_in, d_eg, d_status, lo, hi, false);
+      capture_pipeline(c, c->cap_stream, c->cap_stream2, d_in, d_eg, d_status, lo, hi);
       HIPCHK(hipStreamEndCapture(c->cap_stream, &g));
       hipError_t ie = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
       (void)hipGraphDestroy(g);
@@ -1309,7 +1499,7 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     c->timed = true;
     c->timed_graph = true;
   } else {
-    enqueue_pipeline(c, st, d_in, d_eg, d_status, lo, hi, true);
+    enqueue_pipeline(c, st, d_in, d_eg, d_status, lo, hi);
     c->timed = true;
     c->timed_graph = false;
   }
@@ -1455,6 +1645,9 @@ void cyc_ctx_destroy(cyc_ctx* c) {
     drop_graph(c);
     destroy_events(c);
     if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
+    if (c->cap_stream2) (void)hipStreamDestroy(c->cap_stream2);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->join_ev) (void)hipEventDestroy(c->join_ev);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -1588,6 +1781,17 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return CYC_ERR_ARG;
   if (std::string(name) == "emit_variant") {
     c->emit_variant = int(value);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
+  if (std::string(name) == "emit_blocks") {
+    if (value < 0) return fail(c, CYC_ERR_ARG, "emit_blocks must be >= 0");
+    c->emit_blocks = value;
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
+  if (std::string(name) == "graph_branches") {
+    c->graph_branches = value != 0;
     drop_graph(c);
     return (int)CYC_OK;
   }

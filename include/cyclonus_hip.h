@@ -106,10 +106,13 @@ int cyc_probe_run_host(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_
                        int64_t row_hi);
 
 /* Average device time (ms) of the last run's kernels, measured with HIP events on the launch
- * stream: [0] whole pipeline, [1] emit kernel (the HBM-roofline kernel), [2] class rows. */
+ * stream: [0] whole pipeline, [1] both emit launches (the HBM-roofline kernel, one launch per
+ * plane), [2] class rows of both directions. */
 int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 
 /* Tuning knobs (no effect on results): "emit_variant" 0..5 selects the emit store pattern;
+ * "emit_blocks" the persistent emit grid (0 = one block per row); "graph_branches" (default 1)
+ * runs ingress and egress as two concurrent branches of the step graph;
  * "graphs" (default 1) replays the pipeline as one captured hipGraph when the inputs cannot
  * panic (then cyc_last_timings reports only the whole-pipeline time). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);

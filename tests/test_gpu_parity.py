@@ -225,8 +225,14 @@ def test_graph_and_eager_paths_agree(gpu):
         sh = eng.prepare(probes)
         P, K, W = sh["pods"], sh["slots"], sh["words"]
         outs = []
-        for graphs in (0, 1, 1):
+        # (graphs, graph_branches, emit_blocks, emit_variant): eager, two-branch graph (replayed),
+        # single-branch graph, tiny persistent emit grid, one block per row, other store variants
+        for graphs, branches, blocks, variant in ((0, 1, 1024, 0), (1, 1, 1024, 0), (1, 1, 1024, 0), (1, 0, 1024, 0),
+                                                  (1, 1, 8, 0), (0, 1, 0, 0), (0, 1, 16, 3), (1, 1, 0, 5)):
             eng.set_option("graphs", graphs)
+            eng.set_option("graph_branches", branches)
+            eng.set_option("emit_blocks", blocks)
+            eng.set_option("emit_variant", variant)
             d_in = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_eg = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_st = torch.zeros((P, K), dtype=torch.uint8, device="cuda")
@@ -235,3 +241,64 @@ def test_graph_and_eager_paths_agree(gpu):
             outs.append((d_in.cpu(), d_eg.cpu(), d_st.cpu()))
         for o in outs[1:]:
             assert all(torch.equal(a, b) for a, b in zip(outs[0], o)), seed
+
+
+def _ip_interval_problem(seed, n_pods=700):
+    """Pods with address-ordered IPv4 / IPv6 / v4-mapped addresses in runs (so most 64-pod words
+    are one interval, some straddle), and IPBlock peers whose CIDRs and excepts start and end on,
+    inside and across word boundaries — exercises every branch of the per-word interval test."""
+    import ipaddress
+
+    rng = np.random.default_rng(seed)
+    pods, fams = [], []
+    for n in range(n_pods):
+        run = (n // 96) % 3  # family runs that do not align with 64-pod words
+        if rng.random() < 0.03:
+            run = int(rng.integers(0, 3))  # a few stray addresses of another family
+        fams.append(run)
+        if run == 0:
+            ip = str(ipaddress.IPv4Address((10 << 24) + 4 * n))
+        elif run == 1:
+            ip = str(ipaddress.IPv6Address((0xFD00 << 112) + 4 * n))
+        else:
+            ip = "::ffff:" + str(ipaddress.IPv4Address((10 << 24) + (1 << 16) + 4 * n))
+        pods.append({"Namespace": "x", "Name": f"p{n}", "Labels": {"i": str(n % 7)}, "IP": ip,
+                     "Containers": [{"Name": "c", "Port": 80, "Protocol": "TCP", "PortName": "serve-80-tcp"}]})
+    res = {"Namespaces": {"x": {"ns": "x"}}, "Pods": pods}
+
+    def cidr(fam, lo_pod, plen):
+        if fam == 1:
+            base = (0xFD00 << 112) + 4 * lo_pod
+            net = ipaddress.IPv6Network((base >> (128 - plen) << (128 - plen), plen))
+            return str(net)
+        off = (1 << 16) if fam == 2 else 0
+        base = (10 << 24) + off + 4 * lo_pod
+        net = ipaddress.IPv4Network((base >> (32 - plen) << (32 - plen), plen))
+        return str(net)
+
+    pols = []
+    for i in range(12):
+        peers = []
+        for _ in range(int(rng.integers(1, 4))):
+            fam = int(rng.integers(0, 3))
+            lo = int(rng.integers(0, n_pods))
+            plen = int(rng.integers(20, 28)) if fam != 1 else int(rng.integers(116, 124))
+            ib = {"cidr": cidr(fam, lo, plen)}
+            ex = []
+            for _ in range(int(rng.integers(0, 3))):
+                eplen = min(plen + int(rng.integers(1, 6)), 32 if fam != 1 else 128)
+                ex.append(cidr(fam, lo + int(rng.integers(0, 64)), eplen))
+            if ex:
+                ib["except"] = ex
+            peers.append({"ipBlock": ib})
+        spec = {"podSelector": {"matchLabels": {"i": str(i % 7)}}, "policyTypes": ["Ingress", "Egress"],
+                "ingress": [{"from": peers}], "egress": [{"to": peers[::-1]}]}
+        pols.append({"metadata": {"name": f"ipb{i}", "namespace": "x"}, "spec": spec})
+    return pols, res, [{"AllAvailable": True}]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_ip_interval_words(gpu, seed):
+    pols, res, probes = _ip_interval_problem(seed)
+    o, g = run_both(pols, res, probes)
+    assert_same(o, g, f"ip intervals seed {seed}")
