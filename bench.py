@@ -40,7 +40,7 @@ def load_workload(name: str):
 
 
 def cpu_baseline(data, seconds: float, seed: int = 1):
-    """Time the per-cell CPU oracle (restated reference walk, 1 thread) on random cells."""
+    """Time the per-cell CPU oracle (restated reference walk) on random cells, 1 and N threads."""
     import numpy as np
 
     from oracle.oracle import Oracle
@@ -61,23 +61,34 @@ def cpu_baseline(data, seconds: float, seed: int = 1):
     build_s = time.perf_counter() - t0
     P, K = orc.shape(data["probes"])
     rng = np.random.default_rng(seed)
-    cells, elapsed, chunk = 0, 0.0, 64
-    while elapsed < seconds:
-        s = rng.integers(0, P, chunk)
-        d = rng.integers(0, P, chunk)
-        k = rng.integers(0, K, chunk)
-        t = time.perf_counter()
-        orc.cells(data["probes"], s, d, k)
-        elapsed += time.perf_counter() - t
-        cells += chunk
-        chunk = min(chunk * 2, 4096)
+
+    def timed(threads, budget):
+        cells, elapsed, chunk = 0, 0.0, 64 * threads
+        while elapsed < budget:
+            s = rng.integers(0, P, chunk)
+            d = rng.integers(0, P, chunk)
+            k = rng.integers(0, K, chunk)
+            t = time.perf_counter()
+            orc.cells(data["probes"], s, d, k, threads=threads)
+            elapsed += time.perf_counter() - t
+            cells += chunk
+            chunk = min(chunk * 2, 4096 * threads)
+        return cells, elapsed
+
+    # 1 thread and all host threads (std::thread, static split of the sampled cells);
+    # the GPU box exports its CPU share as OMP_NUM_THREADS
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1, 64))
+    c1, e1 = timed(1, seconds / 2)
+    cn, en = timed(threads, seconds / 2) if threads > 1 else (c1, e1)
     return {
-        "value": cells / elapsed,
+        "value": cn / en,
         "unit": "verdicts/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"{cells} uniformly random (src, dst, slot) cells of {data['name']} through the oracle's per-cell "
-        f"IsTrafficAllowed walk (oracle/oracle.cpp), {elapsed:.1f} s of CPU time, 1 thread; policy build {build_s:.1f} s excluded",
+        "single_thread_value": c1 / e1,
+        "sample": f"uniformly random (src, dst, slot) cells of {data['name']} through the oracle's per-cell "
+        f"IsTrafficAllowed walk (oracle/oracle.cpp): {cn} cells in {en:.1f} s on {threads} threads (std::thread, "
+        f"static split) and {c1} cells in {e1:.1f} s on 1 thread; policy build {build_s:.1f} s excluded",
     }
 
 
@@ -87,8 +98,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4", "config5"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-assemble", action="store_true", help="skip the N>1 all-gather timing")
     args = ap.parse_args()
 
     import numpy as np
@@ -126,8 +138,11 @@ def main():
     lo, hi = row_range(P, world, rank)
     rows = hi - lo
 
-    d_in = torch.empty((max(rows, 1), K, W), dtype=torch.int64, device="cuda")
-    d_eg = torch.empty((max(rows, 1), K, W), dtype=torch.int64, device="cuda")
+    # shards differ by at most one row: every rank allocates the largest, so the optional
+    # all-gather (assembled table) moves the planes as they are
+    maxrows = max(b - a for a, b in (row_range(P, world, r) for r in range(world)))
+    d_in = torch.empty((max(maxrows, 1), K, W), dtype=torch.int64, device="cuda")
+    d_eg = torch.empty((max(maxrows, 1), K, W), dtype=torch.int64, device="cuda")
     d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -149,6 +164,42 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+
+    # assembled table (not part of `value`): RCCL all-gather of both planes' row shards into the
+    # full table on every rank, timed separately (max over ranks)
+    assembled = None
+    if dist is not None and not args.no_assemble:
+        try:
+            out_in = torch.empty((world * maxrows, K, W), dtype=torch.int64, device="cuda" if backend == "nccl" else "cpu")
+            out_eg = torch.empty_like(out_in)
+            src_in, src_eg = (d_in, d_eg) if backend == "nccl" else (d_in.cpu(), d_eg.cpu())
+
+            def gather():
+                for src, out in ((src_in, out_in), (src_eg, out_eg)):
+                    if backend == "nccl":
+                        dist.all_gather_into_tensor(out, src)
+                    else:
+                        dist.all_gather(list(out.chunk(world)), src)
+
+            gather()
+            torch.cuda.synchronize()
+            barrier()
+            ta = time.perf_counter()
+            reps = 3
+            for _ in range(reps):
+                gather()
+            torch.cuda.synchronize()
+            barrier()
+            ga = torch.tensor([(time.perf_counter() - ta) / reps], dtype=torch.float64,
+                              device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(ga, op=dist.ReduceOp.MAX)
+            ga = float(ga.item())
+            assembled = {"all_gather_ms": ga * 1e3,
+                         "bytes_received_per_rank": 2 * (world - 1) * maxrows * K * W * 8,
+                         "xgmi_GBs_per_rank": 2 * (world - 1) * maxrows * K * W * 8 / ga / 1e9}
+            del out_in, out_eg
+        except Exception as e:  # the assembled figure is informational; never lose the bench line
+            assembled = {"error": f"{type(e).__name__}: {e}"}
 
     # per-kernel device times from HIP events on the launch stream (separate, synchronised runs)
     eng.set_option("graphs", 0)  # per-kernel events need the non-graph launch path
@@ -240,6 +291,10 @@ def main():
             "launch": "one captured hipGraph per step (cyc_set_option graphs=1): shared front, then ingress and egress branches on two streams",
             "pipeline_ms": {"total": pipe_ms, "emit": emit_ms, "class_rows": rows_ms, "front": pipe_ms - emit_ms - rows_ms},
         }
+        if assembled is not None:
+            if "all_gather_ms" in assembled:  # whole-table-on-every-rank throughput
+                assembled["value"] = cells / (dt / args.steps + assembled["all_gather_ms"] * 1e-3)
+            line["assembled"] = assembled
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(data, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -34,6 +34,8 @@ EXPORTS = [
     "cyc_last_timings",
     "cyc_set_option",
     "cyc_query_traffic",
+    "cyc_query_traffic_targets",
+    "cyc_query_targets",
 ]
 
 
@@ -86,6 +88,8 @@ def lib():
         L.cyc_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i]
         L.cyc_set_option.argtypes = [vp, cp, i64]
         L.cyc_query_traffic.argtypes = [vp, cp, sz, vp, i64]
+        L.cyc_query_traffic_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]
+        L.cyc_query_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]
         _lib = L
     return _lib
 

@@ -760,13 +760,16 @@ struct QueryArgs {
   const uint32_t* ipb_ex;
   uint8_t* res;
   uint32_t *pan, *pid;
+  uint8_t* tflags;        // optional: per (traffic, direction) matching-target verdicts
+  const uint64_t* toff;   // [n][2] offsets into tflags (entry t - tns_lo: 0 no match, 1 allows, 2 denies)
+  uint32_t members_only;  // query-target: TargetsApplyingToPod only (flag 1 = applies)
 };
 
 enum { QP_NONE = 0, QP_SELECTOR = 1, QP_IP = 2, QP_CIDR = 3 };
 
 // returns 1 allowed / 0 denied, or sets *code and returns 2 (panic)
 __device__ uint32_t query_direction(const QueryArgs& a, int dir, uint32_t T, uint32_t Q, uint32_t desc, uint32_t* code,
-                                    uint32_t* sid) {
+                                    uint32_t* sid, uint8_t* fl) {
   if (a.ext[T]) return 1;  // policy.go:151-153
   const uint32_t ns = a.pod_ns[T], ls = a.pod_ls[T];
   const uint32_t lo = a.tns_lo[dir][ns], hi = a.tns_hi[dir][ns];
@@ -779,21 +782,27 @@ __device__ uint32_t query_direction(const QueryArgs& a, int dir, uint32_t T, uin
     }
     nmatch += r;
   }
+  if (a.members_only) {  // analyze.go:189-192 TargetsApplyingToPod
+    if (fl)
+      for (uint32_t t = lo; t < hi; t++) fl[t - lo] = a.selres[uint64_t(a.tgt[dir][t].sel) * a.L + ls];
+    return 1;
+  }
   if (nmatch == 0) return 1;  // :158-160
   uint32_t allowed = 0;
   for (uint32_t t = lo; t < hi; t++) {
     if (a.selres[uint64_t(a.tgt[dir][t].sel) * a.L + ls] != 1) continue;
     DTarget tg = a.tgt[dir][t];
+    uint32_t tallow = 0;  // policy.go:165-171: this target goes to AllowingTargets or DenyingTargets
     for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {  // Target.Allows: every matching target runs
       DPeer pr = a.peers[j];
       if (pr.kind == 0) {
-        allowed = 1;
+        tallow = 1;
         break;
       }
       bool pok = a.portok[uint64_t(pr.port) * a.D + desc] != 0;
       if (pr.kind == 1) {
         if (pok) {
-          allowed = 1;
+          tallow = 1;
           break;
         }
         continue;
@@ -833,10 +842,12 @@ __device__ uint32_t query_direction(const QueryArgs& a, int dir, uint32_t T, uin
         }
       }
       if (o == 1 && pok) {
-        allowed = 1;
+        tallow = 1;
         break;
       }
     }
+    allowed |= tallow;
+    if (fl) fl[t - lo] = tallow ? 1 : 2;
   }
   return allowed;
 }
@@ -845,9 +856,11 @@ __global__ void k_query(QueryArgs a) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   uint32_t code = 0, sid = 0;
-  uint32_t in = query_direction(a, 0, 2 * i + 1, 2 * i, a.tdesc[i], &code, &sid);
+  uint8_t* fi = a.tflags ? a.tflags + a.toff[2 * i] : nullptr;
+  uint8_t* fe = a.tflags ? a.tflags + a.toff[2 * i + 1] : nullptr;
+  uint32_t in = query_direction(a, 0, 2 * i + 1, 2 * i, a.tdesc[i], &code, &sid, fi);
   uint32_t eg = 0;
-  if (in != 2) eg = query_direction(a, 1, 2 * i, 2 * i + 1, a.tdesc[i], &code, &sid);
+  if (in != 2) eg = query_direction(a, 1, 2 * i, 2 * i + 1, a.tdesc[i], &code, &sid, fe);
   a.res[i] = uint8_t((in == 1 ? 1 : 0) | (eg == 1 ? 2 : 0));
   a.pan[i] = code;
   a.pid[i] = sid;
@@ -1803,6 +1816,130 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   return fail(c, CYC_ERR_ARG, std::string("unknown option ") + name);
 }
 
+// Shared single-cell runner (k_query).  tlist (optional): per (traffic, direction) the matching
+// targets in primary-key order, t for an allowing target and -t-1 for a denying one.
+static int run_query(cyc_ctx* c, const std::vector<QueryTraffic>& ts, uint8_t* out,
+                     std::vector<std::vector<int64_t>>* tlist, bool members_only = false) {
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<uint32_t> ext, tdesc;
+  Problem q = build_query_problem(c->policy, ts, ext, tdesc);
+  DevBuf ls_off, ls_key, ls_val, sel_off, reqs, req_vals, pod_ns, pod_ls, pod_nsls, pod_ip, cidrs, ipbs, ipb_ex, pms, pents,
+      peers, descs, dext, dtdesc, tgt0, tgt1, lo0, lo1, hi0, hi1, selres, portok, res, pan, pid;
+  upload(ls_off, q.ls_off);
+  upload(ls_key, q.ls_key);
+  upload(ls_val, q.ls_val);
+  upload(sel_off, q.sel_off);
+  upload(reqs, q.reqs);
+  upload(req_vals, q.req_vals);
+  upload(pod_ns, q.pod_ns);
+  upload(pod_ls, q.pod_ls);
+  upload(pod_nsls, q.pod_nsls);
+  upload(pod_ip, q.pod_ip);
+  upload(cidrs, q.cidrs);
+  upload(ipbs, q.ipbs);
+  upload(ipb_ex, q.ipb_ex);
+  upload(pms, q.pms);
+  upload(pents, q.pents);
+  upload(peers, q.peers);
+  upload(descs, q.descs);
+  upload(dext, ext);
+  upload(dtdesc, tdesc);
+  upload(tgt0, q.tgt[0]);
+  upload(tgt1, q.tgt[1]);
+  upload(lo0, q.tns_lo[0]);
+  upload(lo1, q.tns_lo[1]);
+  upload(hi0, q.tns_hi[0]);
+  upload(hi1, q.tns_hi[1]);
+  const uint32_t D = uint32_t(std::max<size_t>(q.descs.size(), 1)), M = uint32_t(q.pms.size());
+  selres.alloc(std::max<uint64_t>(uint64_t(q.S) * q.L, 16));
+  portok.alloc(std::max<uint64_t>(uint64_t(M) * D, 16));
+  res.alloc(std::max<size_t>(ts.size(), 16));
+  pan.alloc(std::max<size_t>(ts.size() * 4, 16));
+  pid.alloc(std::max<size_t>(ts.size() * 4, 16));
+  hipStream_t st = nullptr;
+  if (uint64_t(q.S) * q.L)
+    k_selectors<<<grid1(uint64_t(q.S) * q.L, 256), 256, 0, st>>>(q.S, q.L, sel_off.as<uint32_t>(), reqs.as<DReq>(),
+                                                                  req_vals.as<uint32_t>(), ls_off.as<uint32_t>(),
+                                                                  ls_key.as<uint32_t>(), ls_val.as<uint32_t>(),
+                                                                  selres.as<uint8_t>());
+  if (M) k_portok<<<grid1(uint64_t(M) * D, 256), 256, 0, st>>>(M, D, pms.as<DPortM>(), pents.as<DPortEntry>(), descs.as<DDesc>(),
+                                                              portok.as<uint8_t>());
+  QueryArgs qa{};
+  qa.n = uint32_t(ts.size());
+  qa.L = q.L;
+  qa.D = D;
+  qa.pod_ns = pod_ns.as<uint32_t>();
+  qa.pod_ls = pod_ls.as<uint32_t>();
+  qa.pod_nsls = pod_nsls.as<uint32_t>();
+  qa.ext = dext.as<uint32_t>();
+  qa.tdesc = dtdesc.as<uint32_t>();
+  qa.pod_ip = pod_ip.as<DIP>();
+  qa.selres = selres.as<uint8_t>();
+  qa.portok = portok.as<uint8_t>();
+  qa.tgt[0] = tgt0.as<DTarget>();
+  qa.tgt[1] = tgt1.as<DTarget>();
+  qa.tns_lo[0] = lo0.as<uint32_t>();
+  qa.tns_lo[1] = lo1.as<uint32_t>();
+  qa.tns_hi[0] = hi0.as<uint32_t>();
+  qa.tns_hi[1] = hi1.as<uint32_t>();
+  qa.peers = peers.as<DPeer>();
+  qa.ipbs = ipbs.as<DIPBlock>();
+  qa.cidrs = cidrs.as<DCidr>();
+  qa.ipb_ex = ipb_ex.as<uint32_t>();
+  qa.res = res.as<uint8_t>();
+  qa.pan = pan.as<uint32_t>();
+  qa.pid = pid.as<uint32_t>();
+  // per (traffic, direction): one flag per target of the end's namespace
+  std::vector<uint64_t> hoff;
+  DevBuf doff, dfl;
+  uint64_t nfl = 0;
+  if (tlist) {
+    for (size_t i = 0; i < ts.size(); i++)
+      for (int d = 0; d < 2; d++) {
+        uint32_t T = uint32_t(d == 0 ? 2 * i + 1 : 2 * i);  // ingress target = dst, egress = src
+        uint32_t ns = q.pod_ns[T];
+        hoff.push_back(nfl);
+        nfl += q.tns_hi[d][ns] - q.tns_lo[d][ns];
+      }
+    upload(doff, hoff);
+    dfl.alloc(std::max<uint64_t>(nfl, 16));
+    HIPCHK(hipMemsetAsync(dfl.p, 0, std::max<uint64_t>(nfl, 16), st));
+    qa.tflags = dfl.as<uint8_t>();
+    qa.toff = doff.as<uint64_t>();
+  }
+  qa.members_only = members_only ? 1u : 0u;
+  k_query<<<grid1(ts.size(), 128), 128, 0, st>>>(qa);
+  std::vector<uint8_t> hres(ts.size());
+  std::vector<uint32_t> hpan(ts.size()), hpid(ts.size());
+  HIPCHK(hipMemcpy(hres.data(), res.p, ts.size(), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hpan.data(), pan.p, ts.size() * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(hpid.data(), pid.p, ts.size() * 4, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < ts.size(); i++) {
+    if (hpan[i]) {  // analyze.go:209-225 prints the earlier traffics, then the reference panics
+      if (hpan[i] == QP_SELECTOR) return fail(c, CYC_ERR_PANIC_SELECTOR, "invalid operator");
+      if (hpan[i] == QP_IP) return fail(c, CYC_ERR_PANIC_IP, "unable to parse IP '" + q.pod_ip_str[hpid[i]] + "'");
+      const std::string& cs = q.cidr_str[hpid[i]];
+      return fail(c, CYC_ERR_PANIC_CIDR, "unable to parse CIDR '" + cs + "': invalid CIDR address: " + cs);
+    }
+    out[i] = hres[i];
+  }
+  if (tlist) {
+    std::vector<uint8_t> hfl(nfl);
+    if (nfl) HIPCHK(hipMemcpy(hfl.data(), dfl.p, nfl, hipMemcpyDeviceToHost));
+    tlist->assign(ts.size() * 2, {});
+    for (size_t i = 0; i < ts.size(); i++)
+      for (int d = 0; d < 2; d++) {
+        uint32_t T = uint32_t(d == 0 ? 2 * i + 1 : 2 * i);
+        uint32_t lo = q.tns_lo[d][q.pod_ns[T]], hi = q.tns_hi[d][q.pod_ns[T]];
+        for (uint32_t t = lo; t < hi; t++) {
+          uint8_t f = hfl[hoff[2 * i + d] + (t - lo)];
+          if (f) (*tlist)[2 * i + d].push_back(f == 1 ? int64_t(t) : -int64_t(t) - 1);
+        }
+      }
+  }
+  return (int)CYC_OK;
+}
+
 int cyc_query_traffic(cyc_ctx* c, const char* js, size_t len, uint8_t* out, int64_t n) {
   if (!c || !js) return CYC_ERR_ARG;
   if (!c->have_policy) return fail(c, CYC_ERR_ARG, "load a policy first");
@@ -1810,90 +1947,98 @@ int cyc_query_traffic(cyc_ctx* c, const char* js, size_t len, uint8_t* out, int6
     auto ts = load_traffics(json::parse(js, len));
     if (int64_t(ts.size()) > n) return fail(c, CYC_ERR_ARG, "output buffer smaller than the traffic list");
     if (ts.empty()) return (int)CYC_OK;
-    HIPCHK(hipSetDevice(c->device));
-    std::vector<uint32_t> ext, tdesc;
-    Problem q = build_query_problem(c->policy, ts, ext, tdesc);
-    DevBuf ls_off, ls_key, ls_val, sel_off, reqs, req_vals, pod_ns, pod_ls, pod_nsls, pod_ip, cidrs, ipbs, ipb_ex, pms, pents,
-        peers, descs, dext, dtdesc, tgt0, tgt1, lo0, lo1, hi0, hi1, selres, portok, res, pan, pid;
-    upload(ls_off, q.ls_off);
-    upload(ls_key, q.ls_key);
-    upload(ls_val, q.ls_val);
-    upload(sel_off, q.sel_off);
-    upload(reqs, q.reqs);
-    upload(req_vals, q.req_vals);
-    upload(pod_ns, q.pod_ns);
-    upload(pod_ls, q.pod_ls);
-    upload(pod_nsls, q.pod_nsls);
-    upload(pod_ip, q.pod_ip);
-    upload(cidrs, q.cidrs);
-    upload(ipbs, q.ipbs);
-    upload(ipb_ex, q.ipb_ex);
-    upload(pms, q.pms);
-    upload(pents, q.pents);
-    upload(peers, q.peers);
-    upload(descs, q.descs);
-    upload(dext, ext);
-    upload(dtdesc, tdesc);
-    upload(tgt0, q.tgt[0]);
-    upload(tgt1, q.tgt[1]);
-    upload(lo0, q.tns_lo[0]);
-    upload(lo1, q.tns_lo[1]);
-    upload(hi0, q.tns_hi[0]);
-    upload(hi1, q.tns_hi[1]);
-    const uint32_t D = uint32_t(std::max<size_t>(q.descs.size(), 1)), M = uint32_t(q.pms.size());
-    selres.alloc(std::max<uint64_t>(uint64_t(q.S) * q.L, 16));
-    portok.alloc(std::max<uint64_t>(uint64_t(M) * D, 16));
-    res.alloc(std::max<size_t>(ts.size(), 16));
-    pan.alloc(std::max<size_t>(ts.size() * 4, 16));
-    pid.alloc(std::max<size_t>(ts.size() * 4, 16));
-    hipStream_t st = nullptr;
-    if (uint64_t(q.S) * q.L)
-      k_selectors<<<grid1(uint64_t(q.S) * q.L, 256), 256, 0, st>>>(q.S, q.L, sel_off.as<uint32_t>(), reqs.as<DReq>(),
-                                                                    req_vals.as<uint32_t>(), ls_off.as<uint32_t>(),
-                                                                    ls_key.as<uint32_t>(), ls_val.as<uint32_t>(),
-                                                                    selres.as<uint8_t>());
-    if (M) k_portok<<<grid1(uint64_t(M) * D, 256), 256, 0, st>>>(M, D, pms.as<DPortM>(), pents.as<DPortEntry>(), descs.as<DDesc>(),
-                                                                portok.as<uint8_t>());
-    QueryArgs qa{};
-    qa.n = uint32_t(ts.size());
-    qa.L = q.L;
-    qa.D = D;
-    qa.pod_ns = pod_ns.as<uint32_t>();
-    qa.pod_ls = pod_ls.as<uint32_t>();
-    qa.pod_nsls = pod_nsls.as<uint32_t>();
-    qa.ext = dext.as<uint32_t>();
-    qa.tdesc = dtdesc.as<uint32_t>();
-    qa.pod_ip = pod_ip.as<DIP>();
-    qa.selres = selres.as<uint8_t>();
-    qa.portok = portok.as<uint8_t>();
-    qa.tgt[0] = tgt0.as<DTarget>();
-    qa.tgt[1] = tgt1.as<DTarget>();
-    qa.tns_lo[0] = lo0.as<uint32_t>();
-    qa.tns_lo[1] = lo1.as<uint32_t>();
-    qa.tns_hi[0] = hi0.as<uint32_t>();
-    qa.tns_hi[1] = hi1.as<uint32_t>();
-    qa.peers = peers.as<DPeer>();
-    qa.ipbs = ipbs.as<DIPBlock>();
-    qa.cidrs = cidrs.as<DCidr>();
-    qa.ipb_ex = ipb_ex.as<uint32_t>();
-    qa.res = res.as<uint8_t>();
-    qa.pan = pan.as<uint32_t>();
-    qa.pid = pid.as<uint32_t>();
-    k_query<<<grid1(ts.size(), 128), 128, 0, st>>>(qa);
-    std::vector<uint8_t> hres(ts.size());
-    std::vector<uint32_t> hpan(ts.size()), hpid(ts.size());
-    HIPCHK(hipMemcpy(hres.data(), res.p, ts.size(), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(hpan.data(), pan.p, ts.size() * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(hpid.data(), pid.p, ts.size() * 4, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < ts.size(); i++) {
-      if (hpan[i]) {  // analyze.go:209-225 prints the earlier traffics, then the reference panics
-        if (hpan[i] == QP_SELECTOR) return fail(c, CYC_ERR_PANIC_SELECTOR, "invalid operator");
-        if (hpan[i] == QP_IP) return fail(c, CYC_ERR_PANIC_IP, "unable to parse IP '" + q.pod_ip_str[hpid[i]] + "'");
-        const std::string& cs = q.cidr_str[hpid[i]];
-        return fail(c, CYC_ERR_PANIC_CIDR, "unable to parse CIDR '" + cs + "': invalid CIDR address: " + cs);
-      }
-      out[i] = hres[i];
+    return run_query(c, ts, out, nullptr);
+  });
+}
+
+static void json_str(std::string& o, const std::string& v) {
+  o += '"';
+  for (unsigned char ch : v) {
+    if (ch == '"' || ch == '\\') {
+      o += '\\';
+      o += char(ch);
+    } else if (ch < 0x20) {
+      char b[8];
+      snprintf(b, sizeof(b), "\\u%04x", ch);
+      o += b;
+    } else {
+      o += char(ch);
     }
+  }
+  o += '"';
+}
+
+int cyc_query_traffic_targets(cyc_ctx* c, const char* js, size_t len, char* out_json, size_t cap, size_t* needed) {
+  if (!c || !js) return CYC_ERR_ARG;
+  if (!c->have_policy) return fail(c, CYC_ERR_ARG, "load a policy first");
+  return guarded(c, [&]() -> int {
+    auto ts = load_traffics(json::parse(js, len));
+    std::vector<uint8_t> res(ts.size());
+    std::vector<std::vector<int64_t>> tl;
+    if (!ts.empty()) {
+      int rc = run_query(c, ts, res.data(), &tl);
+      if (rc != CYC_OK) return rc;
+    }
+    std::string o = "[";
+    for (size_t i = 0; i < ts.size(); i++) {
+      if (i) o += ',';
+      o += '{';
+      for (int d = 0; d < 2; d++) {
+        o += d ? ",\"Egress\":{" : "\"Ingress\":{";
+        for (int allow = 1; allow >= 0; allow--) {
+          o += allow ? "\"AllowingTargets\":[" : ",\"DenyingTargets\":[";
+          bool first = true;
+          for (int64_t t : tl[2 * i + d]) {
+            if ((t >= 0) != bool(allow)) continue;
+            if (!first) o += ',';
+            first = false;
+            json_str(o, c->policy.dir[d][size_t(t >= 0 ? t : -t - 1)].pk);
+          }
+          o += ']';
+        }
+        o += ",\"IsAllowed\":";
+        o += (res[i] >> d) & 1 ? "true" : "false";
+        o += '}';
+      }
+      o += ",\"IsAllowed\":";
+      o += (res[i] & 3) == 3 ? "true" : "false";
+      o += '}';
+    }
+    o += ']';
+    if (needed) *needed = o.size() + 1;
+    if (!out_json || cap < o.size() + 1) return fail(c, CYC_ERR_ARG, "output buffer too small (see *needed)");
+    memcpy(out_json, o.c_str(), o.size() + 1);
+    return (int)CYC_OK;
+  });
+}
+
+int cyc_query_targets(cyc_ctx* c, const char* js, size_t len, char* out_json, size_t cap, size_t* needed) {
+  if (!c || !js) return CYC_ERR_ARG;
+  if (!c->have_policy) return fail(c, CYC_ERR_ARG, "load a policy first");
+  return guarded(c, [&]() -> int {
+    auto ts = load_target_pods(json::parse(js, len));
+    std::vector<uint8_t> res(ts.size());
+    std::vector<std::vector<int64_t>> tl;
+    if (!ts.empty()) {
+      int rc = run_query(c, ts, res.data(), &tl, true);
+      if (rc != CYC_OK) return rc;
+    }
+    std::string o = "[";
+    for (size_t i = 0; i < ts.size(); i++) {
+      o += i ? ",{" : "{";
+      for (int d = 0; d < 2; d++) {
+        o += d ? "],\"Egress\":[" : "\"Ingress\":[";
+        for (size_t x = 0; x < tl[2 * i + d].size(); x++) {
+          if (x) o += ',';
+          json_str(o, c->policy.dir[d][size_t(tl[2 * i + d][x])].pk);
+        }
+      }
+      o += "]}";
+    }
+    o += ']';
+    if (needed) *needed = o.size() + 1;
+    if (!out_json || cap < o.size() + 1) return fail(c, CYC_ERR_ARG, "output buffer too small (see *needed)");
+    memcpy(out_json, o.c_str(), o.size() + 1);
     return (int)CYC_OK;
   });
 }

@@ -1193,6 +1193,25 @@ std::vector<QueryTraffic> load_traffics(const Node& n) {
   return out;
 }
 
+// analyze --mode query-target input (analyze.go:163-187): a JSON list of QueryTargetPod
+// {Namespace, Labels}; each becomes a traffic from the pod to itself (only membership is used).
+std::vector<QueryTraffic> load_target_pods(const Node& n) {
+  std::vector<QueryTraffic> out;
+  if (!n.is_arr()) return out;
+  for (auto& t : n.a) {
+    QueryEnd e;
+    e.external = false;
+    if (auto ns = t.val("Namespace")) e.ns = ns->str();
+    bool nil;
+    decode_labels(t.val("Labels"), nil, e.labels);
+    QueryTraffic q;
+    q.src = e;
+    q.dst = e;
+    out.push_back(std::move(q));
+  }
+  return out;
+}
+
 // Query mode (analyze --mode query-traffic, analyze.go:209-225): endpoint 2i is traffic i's
 // source, 2i+1 its destination; namespace labels come from the Traffic itself.
 Problem build_query_problem(const PolicyIR& ir, const std::vector<QueryTraffic>& ts, std::vector<uint32_t>& ext,

@@ -107,6 +107,28 @@ class Engine:
         check(self._ctx, lib().cyc_query_traffic(self._ctx, b, len(b), out.ctypes.data, n))
         return [(bool(o & 1), bool(o & 2)) for o in out[:n]]
 
+    def _json_out(self, fn, doc):
+        b = _bytes(doc)
+        need = ctypes.c_size_t(0)
+        cap = 1 << 16
+        while True:
+            buf = ctypes.create_string_buffer(cap)
+            rc = fn(self._ctx, b, len(b), buf, cap, ctypes.byref(need))
+            if rc == _lib.ERR_ARG and need.value > cap:
+                cap = need.value
+                continue
+            check(self._ctx, rc)
+            return json.loads(buf.value.decode())
+
+    def query_traffic_targets(self, traffics):
+        """IsTrafficAllowed with the DirectionResult lists: per traffic
+        {"Ingress": {"AllowingTargets": [pk..], "DenyingTargets": [pk..], "IsAllowed": b}, "Egress": .., "IsAllowed": b}."""
+        return self._json_out(lib().cyc_query_traffic_targets, list(traffics))
+
+    def query_targets(self, pods):
+        """TargetsApplyingToPod per direction for QueryTargetPod dicts {Namespace, Labels}."""
+        return self._json_out(lib().cyc_query_targets, list(pods))
+
     def set_option(self, name: str, value: int):
         check(self._ctx, lib().cyc_set_option(self._ctx, name.encode(), int(value)))
 

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import json
 from dataclasses import dataclass
-from typing import Optional
+from typing import List, Optional
 
 from .engine import Engine
 
@@ -58,8 +58,12 @@ def _traffic_json(t):
 
 
 @dataclass
-class DirectionResult:  # policy.go:84-91 (allowing / denying target lists are not materialised)
+class DirectionResult:  # policy.go:84-91
     allowed: bool
+    # primary keys of the matching targets that allow / deny (None when not requested); the
+    # reference walks a Go map, so its order is random — these are in primary-key order
+    allowing_targets: Optional[List[str]] = None
+    denying_targets: Optional[List[str]] = None
 
     def is_allowed(self) -> bool:
         return self.allowed
@@ -93,11 +97,31 @@ class Policy:
         return self.to_json()["Egress"]
 
     def is_traffic_allowed(self, traffic) -> AllowedResult:
-        return self.is_traffic_allowed_batch([traffic])[0]
+        """policy.go:131-136, with the allowing / denying target lists."""
+        return self.is_traffic_allowed_batch([traffic], targets=True)[0]
 
-    def is_traffic_allowed_batch(self, traffics):
-        res = self.engine.query_traffic([_traffic_json(t) for t in traffics])
-        return [AllowedResult(DirectionResult(i), DirectionResult(e)) for i, e in res]
+    def is_traffic_allowed_batch(self, traffics, targets: bool = False):
+        """One GPU batch; targets=True also returns the DirectionResult target lists."""
+        docs = [_traffic_json(t) for t in traffics]
+        if not targets:
+            res = self.engine.query_traffic(docs)
+            return [AllowedResult(DirectionResult(i), DirectionResult(e)) for i, e in res]
+        out = []
+        for r in self.engine.query_traffic_targets(docs):
+            dirs = [DirectionResult(r[k]["IsAllowed"], r[k]["AllowingTargets"], r[k]["DenyingTargets"])
+                    for k in ("Ingress", "Egress")]
+            out.append(AllowedResult(*dirs))
+        return out
+
+    def targets_applying_to_pod(self, is_ingress: bool, namespace: str, pod_labels) -> List[str]:
+        """policy.go:68-82 (primary keys, in primary-key order)."""
+        r = self.engine.query_targets([{"Namespace": namespace, "Labels": pod_labels}])[0]
+        return r["Ingress" if is_ingress else "Egress"]
+
+    def query_targets(self, pods):
+        """analyze --mode query-target (analyze.go:163-187): per QueryTargetPod {Namespace, Labels},
+        the targets applying to it per direction."""
+        return self.engine.query_targets(list(pods))
 
 
 def build_network_policies(simplify: bool, netpols, device: int = 0) -> Policy:

@@ -121,6 +121,23 @@ int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
  * out[i] = ingress | egress << 1 (allowed bits).  Needs only a loaded policy. */
 int cyc_query_traffic(cyc_ctx* ctx, const char* traffic_json, size_t len, uint8_t* out, int64_t n);
 
+/* query-traffic with the DirectionResult target lists (replaces Policy.IsTrafficAllowed's
+ * AllowedResult, policy.go:84-96,131-174, as printed by analyze.go:209-225).  out_json gets a
+ * JSON array, one object per traffic:
+ *   {"Ingress": {"AllowingTargets": [pk, ...], "DenyingTargets": [pk, ...], "IsAllowed": b},
+ *    "Egress": {...}, "IsAllowed": b}
+ * pk = the target's primary key (target.go:57-62, the key of Policy.Ingress / Policy.Egress).
+ * Lists are in primary-key order (Go walks the target map in random order).  *needed = bytes
+ * required incl. the NUL; CYC_ERR_ARG when cap is smaller.  Panics as cyc_query_traffic. */
+int cyc_query_traffic_targets(cyc_ctx* ctx, const char* traffic_json, size_t len, char* out_json, size_t cap,
+                              size_t* needed);
+
+/* query-target (analyze.go:163-204 QueryTargets / QueryTargetHelper): pods_json is a JSON list
+ * of {"Namespace": ns, "Labels": {...}} (QueryTargetPod); out_json gets, per pod,
+ * {"Ingress": [pk, ...], "Egress": [pk, ...]} = Policy.TargetsApplyingToPod (policy.go:68-82) per
+ * direction, in primary-key order.  An invalid selector operator panics ("invalid operator"). */
+int cyc_query_targets(cyc_ctx* ctx, const char* pods_json, size_t len, char* out_json, size_t cap, size_t* needed);
+
 #ifdef __cplusplus
 }
 #endif

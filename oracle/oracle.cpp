@@ -32,6 +32,7 @@
 #include <set>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gonet.hpp"
@@ -721,6 +722,20 @@ struct Policy {
     }
     return allowers > 0 || deniers == 0;  // DirectionResult.IsAllowed :89-91
   }
+
+  // IsIngressOrEgressAllowed with its DirectionResult lists (policy.go:138-174), as primary keys
+  // (the map keys) in map order.
+  void direction_result(const Traffic& tr, bool isIngress, std::vector<std::string>& allow,
+                        std::vector<std::string>& deny) const {
+    const TrafficPeer& target = isIngress ? tr.dst : tr.src;
+    const TrafficPeer& peer = isIngress ? tr.src : tr.dst;
+    if (!target.internal) return;
+    const auto& dict = isIngress ? ingress : egress;
+    std::vector<std::pair<std::string, const Target*>> matching;
+    for (auto& kv : dict)
+      if (kv.second->is_match(target.internal->ns, target.internal->podLabels)) matching.push_back({kv.first, kv.second.get()});
+    for (auto& m : matching) (m.second->allows(peer, tr.port, tr.portName, tr.protocol) ? allow : deny).push_back(m.first);
+  }
 };
 
 // builder.go:11-26 BuildNetworkPolicies + :35-61 BuildTarget
@@ -1147,8 +1162,154 @@ int orc_probe_cells(void* hv, const char* probes_json, const int32_t* ss, const 
   }
 }
 
+// Same as orc_probe_cells with the cells split statically over `threads` std::threads (the
+// multi-core CPU baseline of SURVEY §8d).  The per-cell walk is read-only on the Policy, so the
+// threads share it; each thread decodes the probe configs itself.
+int orc_probe_cells_mt(void* hv, const char* probes_json, const int32_t* ss, const int32_t* dd, const int32_t* kk, int n,
+                       uint8_t* out, int threads, char* err, size_t errcap) {
+  if (threads <= 1) return orc_probe_cells(hv, probes_json, ss, dd, kk, n, out, err, errcap);
+  std::vector<std::thread> pool;
+  std::vector<int> rc(threads, 0);
+  std::vector<std::string> msg(threads);
+  for (int t = 0; t < threads; t++) {
+    int lo = int(int64_t(n) * t / threads), hi = int(int64_t(n) * (t + 1) / threads);
+    pool.emplace_back([&, t, lo, hi] {
+      char e[1024] = {0};
+      rc[t] = orc_probe_cells(hv, probes_json, ss + lo, dd + lo, kk + lo, hi - lo, out + lo, e, sizeof(e));
+      msg[t] = e;
+    });
+  }
+  for (auto& th : pool) th.join();
+  for (int t = 0; t < threads; t++)
+    if (rc[t] != 0) {
+      set_err(err, errcap, msg[t]);
+      return rc[t];
+    }
+  return 0;
+}
+
 // analyze --mode query-traffic (analyze.go:209-225): JSON list of matcher.Traffic.
 // out[i] = ingress | egress<<1 | panic<<2
+static std::vector<Traffic> decode_traffics(const char* traffic_json) {
+  VP v = ojson::parse(traffic_json);
+  auto peer = [](const Value* p) {
+    TrafficPeer tp;
+    if (!p || p->is_null()) return tp;
+    if (auto ip = p->get("IP"); ip && !ip->is_null()) tp.ip = ip->as_str();
+    if (auto in = p->get("Internal"); in && !in->is_null()) {
+      tp.internal = std::make_shared<InternalPeer>();
+      tp.internal->podLabels = decode_labels(in->get("PodLabels"));
+      tp.internal->nsLabels = decode_labels(in->get("NamespaceLabels"));
+      if (auto ns = in->get("Namespace"); ns && !ns->is_null()) tp.internal->ns = ns->as_str();
+    }
+    return tp;
+  };
+  std::vector<Traffic> out;
+  for (auto& t : v->arr) {
+    Traffic tr;
+    tr.src = peer(t->get("Source"));
+    tr.dst = peer(t->get("Destination"));
+    if (auto x = t->get("ResolvedPort"); x && !x->is_null()) tr.port = int(x->as_int());
+    if (auto x = t->get("ResolvedPortName"); x && !x->is_null()) tr.portName = x->as_str();
+    if (auto x = t->get("Protocol"); x && !x->is_null()) tr.protocol = x->as_str();
+    out.push_back(std::move(tr));
+  }
+  return out;
+}
+
+// AllowedResult lists per traffic as JSON (same shape as cyc_query_traffic_targets):
+// [{"Ingress": {"AllowingTargets": [pk..], "DenyingTargets": [..], "IsAllowed": b}, "Egress": {..},
+//   "IsAllowed": b}, ..].  Returns 0, 1 on a Go panic (message in err), -1 on bad input / small buffer.
+int orc_query_traffic_targets(void* hv, const char* traffic_json, char* out, size_t cap, char* err, size_t errcap) {
+  auto* h = static_cast<Handle*>(hv);
+  try {
+    std::string o = "[";
+    bool first = true;
+    for (auto& tr : decode_traffics(traffic_json)) {
+      o += first ? "{" : ",{";
+      first = false;
+      bool all = true;
+      for (int d = 0; d < 2; d++) {
+        std::vector<std::string> allow, deny;
+        try {
+          h->policy->direction_result(tr, d == 0, allow, deny);
+        } catch (GoPanic& p) {
+          set_err(err, errcap, p.msg);
+          return 1;
+        }
+        bool ok = !allow.empty() || deny.empty();
+        all = all && ok;
+        o += d ? ",\"Egress\":{" : "\"Ingress\":{";
+        for (int a = 0; a < 2; a++) {
+          o += a == 0 ? "\"AllowingTargets\":[" : ",\"DenyingTargets\":[";
+          auto& L = a == 0 ? allow : deny;
+          for (size_t i = 0; i < L.size(); i++) {
+            if (i) o += ',';
+            o += ojson::go_quote(L[i]);
+          }
+          o += ']';
+        }
+        o += std::string(",\"IsAllowed\":") + (ok ? "true" : "false") + "}";
+      }
+      o += std::string(",\"IsAllowed\":") + (all ? "true" : "false") + "}";
+    }
+    o += "]";
+    if (o.size() + 1 > cap) {
+      set_err(err, errcap, "buffer too small: need " + std::to_string(o.size() + 1));
+      return -1;
+    }
+    memcpy(out, o.c_str(), o.size() + 1);
+    return 0;
+  } catch (std::exception& e) {
+    set_err(err, errcap, e.what());
+    return -1;
+  }
+}
+
+// analyze --mode query-target (analyze.go:163-204): per QueryTargetPod {Namespace, Labels},
+// TargetsApplyingToPod per direction as primary keys: [{"Ingress": [..], "Egress": [..]}, ..].
+int orc_query_targets(void* hv, const char* pods_json, char* out, size_t cap, char* err, size_t errcap) {
+  auto* h = static_cast<Handle*>(hv);
+  try {
+    VP v = ojson::parse(pods_json);
+    std::string o = "[";
+    bool first = true;
+    for (auto& p : v->arr) {
+      std::string ns;
+      if (auto x = p->get("Namespace"); x && !x->is_null()) ns = x->as_str();
+      auto labels = decode_labels(p->get("Labels"));
+      o += first ? "{" : ",{";
+      first = false;
+      for (int d = 0; d < 2; d++) {
+        o += d ? "],\"Egress\":[" : "\"Ingress\":[";
+        bool f2 = true;
+        try {
+          for (auto& kv : d == 0 ? h->policy->ingress : h->policy->egress)  // policy.go:68-82
+            if (kv.second->is_match(ns, labels)) {
+              o += f2 ? "" : ",";
+              f2 = false;
+              o += ojson::go_quote(kv.first);
+            }
+        } catch (GoPanic& e) {
+          set_err(err, errcap, e.msg);
+          return 1;
+        }
+      }
+      o += "]}";
+    }
+    o += "]";
+    if (o.size() + 1 > cap) {
+      set_err(err, errcap, "buffer too small: need " + std::to_string(o.size() + 1));
+      return -1;
+    }
+    memcpy(out, o.c_str(), o.size() + 1);
+    return 0;
+  } catch (std::exception& e) {
+    set_err(err, errcap, e.what());
+    return -1;
+  }
+}
+
 int orc_query_traffic(void* hv, const char* traffic_json, uint8_t* out, int n, char* err, size_t errcap) {
   auto* h = static_cast<Handle*>(hv);
   try {

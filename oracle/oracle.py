@@ -47,7 +47,10 @@ def lib():
         L.orc_probe_shape.argtypes = [vp, c, ctypes.POINTER(i), ctypes.POINTER(i), c, sz]
         L.orc_probe_run.argtypes = [vp, c, vp, vp, vp, ctypes.POINTER(ctypes.c_longlong), c, sz]
         L.orc_probe_cells.argtypes = [vp, c, vp, vp, vp, i, vp, c, sz]
+        L.orc_probe_cells_mt.argtypes = [vp, c, vp, vp, vp, i, vp, i, c, sz]
         L.orc_query_traffic.argtypes = [vp, c, vp, i, c, sz]
+        L.orc_query_traffic_targets.argtypes = [vp, c, c, sz, c, sz]
+        L.orc_query_targets.argtypes = [vp, c, c, sz, c, sz]
         L.orc_ip_in_cidr.argtypes = [c, c]
         L.orc_ipblock_match.argtypes = [c, c, ctypes.POINTER(c), i]
         L.orc_selector_match.argtypes = [c, c]
@@ -115,17 +118,42 @@ class Oracle:
             raise ValueError(err.value.decode())
         return status, inp, egp
 
-    def cells(self, probes, s, d, k):
-        """Sampled cells -> u8 array: status | ingress<<4 | egress<<5 | panic<<6."""
+    def cells(self, probes, s, d, k, threads=1):
+        """Sampled cells -> u8 array: status | ingress<<4 | egress<<5 | panic<<6.
+        threads > 1 splits the cells over std::threads (read-only walk over the shared policy)."""
         s = np.ascontiguousarray(s, np.int32)
         d = np.ascontiguousarray(d, np.int32)
         k = np.ascontiguousarray(k, np.int32)
         out = np.zeros(len(s), np.uint8)
         err = ctypes.create_string_buffer(4096)
-        rc = lib().orc_probe_cells(self._h, _j(probes), s.ctypes.data, d.ctypes.data, k.ctypes.data, len(s), out.ctypes.data, err, 4096)
+        rc = lib().orc_probe_cells_mt(self._h, _j(probes), s.ctypes.data, d.ctypes.data, k.ctypes.data, len(s),
+                                      out.ctypes.data, int(threads), err, 4096)
         if rc != 0:
             raise ValueError(err.value.decode())
         return out
+
+    def _json_call(self, fn, doc):
+        err = ctypes.create_string_buffer(4096)
+        cap = 1 << 16
+        while True:
+            buf = ctypes.create_string_buffer(cap)
+            rc = fn(self._h, _j(doc), buf, cap, err, 4096)
+            if rc == 1:
+                raise OraclePanic(err.value.decode())
+            if rc < 0 and err.value.startswith(b"buffer too small"):
+                cap = int(err.value.split()[-1])
+                continue
+            if rc < 0:
+                raise ValueError(err.value.decode())
+            return json.loads(buf.value.decode())
+
+    def query_traffic_targets(self, traffics):
+        """AllowedResult with target lists per traffic (pk order); raises OraclePanic."""
+        return self._json_call(lib().orc_query_traffic_targets, traffics)
+
+    def query_targets(self, pods):
+        """TargetsApplyingToPod per direction for QueryTargetPod dicts; raises OraclePanic."""
+        return self._json_call(lib().orc_query_targets, pods)
 
     def query_traffic(self, traffics):
         """List of matcher.Traffic JSON objects -> list of (ingress, egress) or OraclePanic."""

@@ -44,6 +44,43 @@ def readme_combined_table():
     return {"header": header[1:], "rows": table, "text": "\n".join(raw) + "\n"}
 
 
+def readme_queries():
+    """README.md:218-287 (analyze --mode query-target / query-traffic on simple-example),
+    transcribed: the query-traffic example's traffic (its Traffic table, :262-268) with the
+    Type / Action / Target rows of its result table (:271-287), and the query-target example
+    (:229-246) as the SOURCE RULES of the targets combined per direction."""
+    lines = open(os.path.join(REF, "README.md")).read().splitlines()
+    assert "192.168.1.99" in lines[264] and "192.168.1.100" in lines[266] and "IS ALLOWED?" in lines[285]
+    traffic = {
+        "Source": {"Internal": {"PodLabels": {"app": "c"}, "NamespaceLabels": {"ns": "y"}, "Namespace": "y"},
+                   "IP": "192.168.1.99"},
+        "Destination": {"Internal": {"PodLabels": {"pod": "b"}, "NamespaceLabels": {"ns": "y"}, "Namespace": "y"},
+                        "IP": "192.168.1.100"},
+        "ResolvedPort": 80, "ResolvedPortName": "serve-80-tcp", "Protocol": "TCP",
+    }
+    all_pods = {"namespace": "y", "selector": {}}
+    pod_b = {"namespace": "y", "selector": {"matchLabels": {"pod": "b"}}}
+    return {
+        "query_traffic": {
+            "source": "README.md:251-287",
+            "traffic": traffic,
+            "expected": {"Ingress": {"AllowingTargets": [pod_b], "DenyingTargets": [all_pods]},
+                         "Egress": {"AllowingTargets": [], "DenyingTargets": [all_pods]},
+                         "IsAllowed": False},
+        },
+        "query_target": {
+            "source": "README.md:218-246",
+            "pod": {"Namespace": "y", "Labels": {"pod": "a"}},
+            "expected_source_rules": {
+                "Ingress": ["y/allow-label-to-label", "y/deny-all-for-label", "y/deny-all"],
+                "Egress": ["y/deny-all-egress", "y/allow-all-egress-by-label"],
+            },
+        },
+        "examples_targets": json.load(open(os.path.join(REF, "examples/targets.json"))),
+        "examples_traffic": json.load(open(os.path.join(REF, "examples/traffic.json"))),
+    }
+
+
 def config1():
     files = sorted(glob.glob(os.path.join(REF, "networkpolicies/simple-example/*.yaml")))
     policies = []
@@ -56,6 +93,7 @@ def config1():
         "resources": probe["Resources"],
         "probes": probe["Probes"],
         "readme_combined_tcp80": readme_combined_table(),
+        "readme_queries": readme_queries(),
     }
 
 

@@ -70,6 +70,57 @@ def test_query_traffic_random(gpu, bad):
             assert pol.engine.query_traffic(traffics) == want, seed
 
 
+def test_readme_queries_gpu(gpu):
+    """README.md:218-287 query-traffic / query-target examples through the GPU entry points."""
+    from test_oracle_golden import check_readme_queries
+
+    c = json.load(open(os.path.join(GOLD, "config1.json")))
+    q = c["readme_queries"]
+    pol = build_network_policies(True, c["policies"])
+    ir = pol.to_json()
+    (tr,) = pol.engine.query_traffic_targets([q["query_traffic"]["traffic"]])
+    (tg,) = pol.query_targets([q["query_target"]["pod"]])
+    check_readme_queries(ir, tr, tg, q)
+    res = pol.is_traffic_allowed(q["query_traffic"]["traffic"])
+    assert not res.is_allowed() and res.ingress.is_allowed() and not res.egress.is_allowed()
+    orc = Oracle(c["policies"], c["resources"])
+    assert pol.engine.query_traffic_targets(q["examples_traffic"]) == orc.query_traffic_targets(q["examples_traffic"])
+    assert pol.query_targets(q["examples_targets"]) == orc.query_targets(q["examples_targets"])
+
+
+@pytest.mark.parametrize("bad", [False, True])
+def test_query_targets_random(gpu, bad):
+    """Target lists (query-traffic) and TargetsApplyingToPod (query-target) vs the oracle,
+    including the first panicking traffic / pod."""
+    r = random.Random(7 + bad)
+    for seed in range(80):
+        pols, _, _ = random_problem(40_000 + seed + 1000 * bad, bad=bad)
+        try:
+            orc = Oracle(pols)
+        except OraclePanic:
+            continue
+        pol = build_network_policies(True, pols)
+        traffics = [_random_traffic(r, bad) for _ in range(30)]
+        try:
+            want = orc.query_traffic_targets(traffics)
+        except OraclePanic as e:
+            with pytest.raises(CyclonusPanic) as g:
+                pol.engine.query_traffic_targets(traffics)
+            assert g.value.msg == str(e), seed
+        else:
+            assert pol.engine.query_traffic_targets(traffics) == want, seed
+        pods = [{"Namespace": r.choice(NS), "Labels": {k: r.choice(VALS) for k in r.sample(KEYS, r.randint(0, 3))}}
+                for _ in range(20)]
+        try:
+            want = orc.query_targets(pods)
+        except OraclePanic as e:
+            with pytest.raises(CyclonusPanic) as g:
+                pol.query_targets(pods)
+            assert g.value.msg == str(e), seed
+        else:
+            assert pol.query_targets(pods) == want, seed
+
+
 def test_runner_tables_match_oracle_render(gpu):
     c = json.load(open(os.path.join(GOLD, "config1.json")))
     pol = build_network_policies(True, c["policies"])

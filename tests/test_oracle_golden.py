@@ -117,3 +117,50 @@ def test_compile_panics():
                                                        "ingress": [{"ports": [{"port": 90, "endPort": 80}]}]}}]
     with pytest.raises(O.OraclePanic, match="end port < start port"):
         O.Oracle(bad_range)
+
+
+def _describe(ir, direction, pks):
+    """Primary keys -> {namespace, selector} of the targets (the README tables' TARGET column)."""
+    return [{"namespace": ir[direction][pk]["Namespace"], "selector": ir[direction][pk]["PodSelector"]} for pk in pks]
+
+
+def _source_rules(ir, direction, pks):
+    out = set()
+    for pk in pks:
+        t = ir[direction][pk]
+        for r in t["SourceRules"]:  # a target's rules all live in the target's namespace
+            out.add(f"{t['Namespace']}/{r['metadata']['name']}")
+    return out
+
+
+def _key(d):
+    return json.dumps(d, sort_keys=True)
+
+
+def check_readme_queries(ir, traffic_result, target_result, q):
+    """README.md:218-287 query-traffic / query-target examples against a result in the shape of
+    cyc_query_traffic_targets / cyc_query_targets (target lists as primary keys)."""
+    exp = q["query_traffic"]["expected"]
+    for d in ("Ingress", "Egress"):
+        for lst in ("AllowingTargets", "DenyingTargets"):
+            got = sorted(map(_key, _describe(ir, d, traffic_result[d][lst])))
+            assert got == sorted(map(_key, exp[d][lst])), (d, lst)
+    assert traffic_result["IsAllowed"] == exp["IsAllowed"]
+    for d in ("Ingress", "Egress"):
+        assert _source_rules(ir, d, target_result[d]) == set(q["query_target"]["expected_source_rules"][d]), d
+
+
+def test_readme_queries_oracle():
+    c = json.load(open(os.path.join(GOLD, "config1.json")))
+    q = c["readme_queries"]
+    orc = O.Oracle(c["policies"], c["resources"])
+    ir = orc.policy_json()
+    (tr,) = orc.query_traffic_targets([q["query_traffic"]["traffic"]])
+    (tg,) = orc.query_targets([q["query_target"]["pod"]])
+    check_readme_queries(ir, tr, tg, q)
+    # the lists agree with the pinned per-direction verdicts (policy.go:89-91)
+    for t, (i, e) in zip(orc.query_traffic_targets(q["examples_traffic"]), orc.query_traffic(q["examples_traffic"])):
+        assert t["Ingress"]["IsAllowed"] == i and t["Egress"]["IsAllowed"] == e
+        for d in ("Ingress", "Egress"):
+            assert t[d]["IsAllowed"] == (bool(t[d]["AllowingTargets"]) or not t[d]["DenyingTargets"])
+    assert len(orc.query_targets(q["examples_targets"])) == len(q["examples_targets"])
