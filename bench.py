@@ -210,6 +210,7 @@ def main():
     eng.set_option("graphs", 1)
     tm = np.array(tm)
     pipe_ms, emit_ms, rows_ms = (float(x) for x in tm.mean(axis=0))
+    classes_in, classes_eg = eng.classes()
 
     # practical write ceiling for the same bytes: torch's fill kernel over both output planes
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -271,6 +272,8 @@ def main():
                 "peers": shape["peers"],
                 "identities_in": shape["classes_in"],
                 "identities_eg": shape["classes_eg"],
+                "classes_in": classes_in,
+                "classes_eg": classes_eg,
                 "parallelism": f"target-row shards x{world}",
                 "rows_per_rank": rows,
             },

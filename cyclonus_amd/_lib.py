@@ -32,6 +32,7 @@ EXPORTS = [
     "cyc_probe_run",
     "cyc_probe_run_host",
     "cyc_last_timings",
+    "cyc_last_classes",
     "cyc_set_option",
     "cyc_query_traffic",
     "cyc_query_traffic_targets",
@@ -86,6 +87,7 @@ def lib():
         L.cyc_probe_run.argtypes = [vp, vp, vp, vp, vp, i64, i64]
         L.cyc_probe_run_host.argtypes = [vp, vp, vp, vp, i64, i64]
         L.cyc_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i]
+        L.cyc_last_classes.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), i]
         L.cyc_set_option.argtypes = [vp, cp, i64]
         L.cyc_query_traffic.argtypes = [vp, cp, sz, vp, i64]
         L.cyc_query_traffic_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]

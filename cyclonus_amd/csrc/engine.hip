@@ -412,6 +412,8 @@ struct MemberArgs {
   uint32_t ht_cap;
   const uint32_t* act;        // identities used by the rows of this run (range plan)
   uint32_t n_act;
+  uint32_t* reps;             // class representatives, act[] order within each block (k_classify)
+  uint32_t* rep_cnt;          // starts at ~0 (hash-table memset): ends at count - 1
 };
 
 __device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* keys, uint32_t cap, uint64_t h) {
@@ -467,31 +469,36 @@ __global__ void k_member(MemberArgs a) {
   a.cnt[i] = n;
   a.hash[i] = h;
   a.err[i] = e;
-  // Many identities share a class (e.g. every pod no policy selects): lanes of a wave with the
-  // same key elect their lowest lane (= lowest identity, act[] is sorted) to do the atomics, so
-  // a popular key costs one CAS + one atomicMin per wave instead of one per identity.
-  bool want = !e;
+  // Many identities share a class (e.g. every pod no policy selects): only the lowest lane of a
+  // wave holding a key (= lowest identity, act[] is sorted) does the atomics, so a popular key
+  // costs one CAS + one atomicMin per wave instead of one per identity, while distinct keys
+  // still insert in parallel.  Duplicates are found with register shuffles, not atomics.
+  const bool want = !e;
   const uint32_t lane = threadIdx.x & 63;
-  uint64_t pending = __ballot(want);
-  while (pending) {
-    const int leader = __ffsll((unsigned long long)pending) - 1;
-    const uint64_t hk = __shfl(h, leader);
-    const uint64_t same = __ballot(want && h == hk);
-    if (int(lane) == leader) {
-      uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
-      atomicMin(&a.ht_rep[s], i);
-    }
-    pending &= ~same;
-    if (h == hk) want = false;
+  const uint64_t live = __ballot(want);
+  bool leader = want;
+  for (uint32_t j = 0; j < 64; j++) {
+    const uint64_t hj = __shfl(h, int(j));
+    if (j < lane && ((live >> j) & 1) && hj == h) leader = false;
+  }
+  if (leader) {
+    uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
+    atomicMin(&a.ht_rep[s], i);
   }
 }
 
-__global__ void k_classify(MemberArgs a, uint32_t* __restrict__ class_of) {
-  uint32_t ii = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ii >= a.n_act) return;
-  const uint32_t i = a.act[ii];
+// Also compacts the class representatives: each block appends its representatives, in act[]
+// order (ascending identity), at a base taken with one atomicAdd — consecutive identities (one
+// namespace) stay adjacent, so consecutive class-row blocks share their targets' peer rows in
+// L2.  The counter starts at ~0 (hash-table memset), so it ends at count - 1.
+__global__ __launch_bounds__(256) void k_classify(MemberArgs a, uint32_t* __restrict__ class_of) {
+  __shared__ uint32_t wsum[4], base;
+  const uint32_t ii = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool live = ii < a.n_act;
+  const uint32_t i = live ? a.act[ii] : 0;
   uint32_t c = i;
-  if (!a.err[i]) {
+  if (live && !a.err[i]) {
     uint32_t s = ht_find(a.ht_key, a.ht_cap, a.hash[i]);
     uint32_t r = s == 0xFFFFFFFFu ? i : a.ht_rep[s];
     if (r != i) {  // verify (a 64-bit hash collision must never merge distinct classes)
@@ -506,15 +513,25 @@ __global__ void k_classify(MemberArgs a, uint32_t* __restrict__ class_of) {
       c = eq ? r : i;
     }
   }
-  class_of[i] = c;
+  if (live) class_of[i] = c;
+  const bool f = live && c == i;
+  const uint64_t m = __ballot(f);
+  if (lane == 0) wsum[wv] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) base = atomicAdd(a.rep_cnt, wsum[0] + wsum[1] + wsum[2] + wsum[3]) + 1u;
+  __syncthreads();
+  uint32_t off = base;
+  for (uint32_t x = 0; x < wv; x++) off += wsum[x];
+  if (f) a.reps[off + __popcll(m & ((1ull << lane) - 1))] = i;
 }
+
 
 // Class rows.  For a class representative i, a chunk of KC job slots and one 64-pod word w, walk
 // each of its targets' peers in slice order (target.go:29-36: short-circuit on the first
 // allowing peer; a panicking peer ends the walk with a panic, ippeermatcher.go:46-48) for 64
 // peer pods at once with bit operations, per slot because the port check differs per slot.
 // A peer's PM/ER word is loaded once and used for all KC slots.
-constexpr int KC = 8;
+// KC (template): job slots per thread, 8 or 4.
 
 struct RowArgs {
   const DTarget* tgt;
@@ -523,8 +540,9 @@ struct RowArgs {
   const uint8_t* portok;
   uint32_t D;
   uint32_t n_ident, K, W, P;
-  const uint32_t* act;  // active identities (range plan)
-  uint32_t n_act;
+  const uint32_t* reps;     // class representatives (k_classify)
+  const uint32_t* rep_cnt;  // count = value + 1
+  uint32_t rep_blocks;      // block rows of the grid; they stride over the representatives
   const uint32_t* class_of;
   const uint32_t *cnt, *list_off, *list;
   const uint8_t* id_err;
@@ -537,15 +555,8 @@ struct RowArgs {
   uint64_t* AE;              // [n_ident][K][W] (ERR builds only)
 };
 
-template <bool EGRESS, bool ERR>
-__global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
-  const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
-  const uint32_t ii = blockIdx.x / (chunks * nkc);
-  const uint32_t kc = (blockIdx.x / chunks) % nkc;
-  const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
-  if (ii >= a.n_act) return;
-  const uint32_t i = a.act[ii];
-  if (a.class_of[i] != i || w >= a.W) return;
+template <bool EGRESS, bool ERR, int KC>
+__device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uint32_t kc, uint32_t w) {
   const uint32_t k0 = kc * KC;
   const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
   const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
@@ -604,7 +615,7 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
             okm = pok[du[kk]] ? ~0ull : 0ull;
           } else if (!EGRESS || du[kk] == -2) {
             okm = 0;
-          } else {  // egress word whose destinations have mixed job descriptors
+          } else {  // egress word whose destinations have mixed job descriptors (rare)
             okm = 0;
             const uint64_t* dm = a.DM + uint64_t(k0 + kk) * a.D * a.W + w;
             for (uint32_t d = 0; d < a.D; d++)
@@ -629,6 +640,27 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
       a.A[idx] = allow[kk] & valid[kk];
       if (ERR) a.AE[idx] = err[kk] & valid[kk];
     }
+  }
+}
+
+// Grid = rep_blocks x slot chunks x 256-word chunks; block rows stride over the compacted class
+// representatives (their number is only known on the device), so no block is spent on the
+// identities that merely share a class.
+// LOOP = false: one block row per representative slot (rep_blocks >= the count of identities;
+// surplus rows exit at once) — keeps the per-word body loop-free, which the egress variant
+// needs to stay at 3 waves/SIMD.
+template <bool EGRESS, bool ERR, int KC, bool LOOP>
+__global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
+  const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
+  const uint32_t kc = (blockIdx.x / chunks) % nkc;
+  const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
+  if (w >= a.W) return;
+  const uint32_t n_reps = *a.rep_cnt + 1u;
+  uint32_t r = blockIdx.x / (chunks * nkc);
+  if (LOOP) {
+    for (; r < n_reps; r += a.rep_blocks) class_row_word<EGRESS, ERR, KC>(a, a.reps[r], kc, w);
+  } else if (r < n_reps) {
+    class_row_word<EGRESS, ERR, KC>(a, a.reps[r], kc, w);
   }
 }
 
@@ -919,8 +951,11 @@ struct Identities {  // pod identities for one direction
 
 struct DirDev {
   DevBuf id_ns, id_ls, id_desc, id_status, list_off, list, cnt, hash, err, ht_key, ht_rep, class_of, A, AE, tns_lo,
-      tns_hi, tgt, pod_id;
+      tns_hi, tgt, pod_id, reps;
   uint32_t n = 0, ht_cap = 0;
+  // hash table buffer = [cap] u64 keys, [cap] u32 reps, 1 u32 representative counter: one
+  // 0xFF memset per run empties the table and sets the counter to ~0 (= count - 1 for 0)
+  uint32_t* rep_cnt() { return reinterpret_cast<uint32_t*>(static_cast<char*>(ht_key.p) + uint64_t(ht_cap) * 12); }
 };
 }  // namespace
 
@@ -952,6 +987,8 @@ struct cyc_ctx {
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
   int emit_variant = 0;  // tuning knob (cyc_set_option "emit_variant")
   int64_t emit_blocks = 0;  // cyc_set_option "emit_blocks": persistent emit grid (0 = a block per row)
+  int class_variant[2] = {3, 1};  // cyc_set_option "class_variant_in" / "_eg" (enq_class_rows;
+                                  // defaults measured best on configs #3/#4: profiles/r01_class_sweep.txt)
   bool use_graphs = true;  // cyc_set_option "graphs"
   bool graph_branches = true;  // cyc_set_option "graph_branches": ingress / egress as two graph branches
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr;  // graph capture: ingress / egress branches
@@ -1157,7 +1194,8 @@ static void prepare_device(cyc_ctx* c) {
     dd.cnt.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.hash.alloc(std::max<uint64_t>(dd.n * 8ull, 16));
     dd.err.alloc(std::max<uint64_t>(dd.n, 16));
-    dd.ht_key.alloc(uint64_t(dd.ht_cap) * 12);  // [cap] u64 keys (empty = ~0) then [cap] u32 reps
+    dd.ht_key.alloc(uint64_t(dd.ht_cap) * 12 + 16);  // [cap] u64 keys (empty = ~0), [cap] u32 reps, counter
+    dd.reps.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.class_of.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.A.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
     if (pb.may_err) dd.AE.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
@@ -1193,6 +1231,8 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   a.ht_cap = dd.ht_cap;
   a.act = c->act[d].as<uint32_t>();
   a.n_act = c->n_act[d];
+  a.reps = dd.reps.as<uint32_t>();
+  a.rep_cnt = dd.rep_cnt();
   return a;
 }
 
@@ -1373,8 +1413,6 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   ra.portok = c->portok.as<uint8_t>();
   ra.D = D;
   ra.n_ident = dd.n;
-  ra.act = c->act[d].as<uint32_t>();
-  ra.n_act = c->n_act[d];
   ra.K = K;
   ra.W = W;
   ra.P = P;
@@ -1390,14 +1428,29 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   ra.DM = c->DM.as<uint64_t>();
   ra.A = dd.A.as<uint64_t>();
   ra.AE = pb.may_err ? dd.AE.as<uint64_t>() : nullptr;
-  unsigned g = unsigned(uint64_t((W + 255) / 256) * c->n_act[d] * ((K + KC - 1) / KC));
-  if (d == 0) {
-    if (pb.may_err) k_class_rows<false, true><<<g, 256, 0, st>>>(ra);
-    else k_class_rows<false, false><<<g, 256, 0, st>>>(ra);
+  // variant (cyc_set_option "class_variant_in" / "class_variant_eg"): bit 0 = 4 slots per
+  // thread instead of 8, bit 1 = block rows stride over the representatives (bounded grid)
+  const int var = d == 0 ? c->class_variant[0] : c->class_variant[1];
+  const uint32_t kct = (var & 1) ? 4 : 8;
+  const bool loop = (var & 2) != 0;
+  const uint64_t per_rep = uint64_t((W + 255) / 256) * ((K + kct - 1) / kct);
+  ra.rep_blocks = loop ? uint32_t(std::min<uint64_t>(c->n_act[d], std::max<uint64_t>(64, (16384 + per_rep - 1) / per_rep)))
+                       : c->n_act[d];
+  ra.reps = dd.reps.as<uint32_t>();
+  ra.rep_cnt = dd.rep_cnt();
+  unsigned g = unsigned(per_rep * ra.rep_blocks);
+#define CYC_ROWS(EG, ERR, KCT, LOOP) k_class_rows<EG, ERR, KCT, LOOP><<<g, 256, 0, st>>>(ra)
+  if (pb.may_err) {
+    if (d == 0) CYC_ROWS(false, true, 8, false);
+    else CYC_ROWS(true, true, 8, false);
+  } else if (d == 0) {
+    if (kct == 4) loop ? CYC_ROWS(false, false, 4, true) : CYC_ROWS(false, false, 4, false);
+    else loop ? CYC_ROWS(false, false, 8, true) : CYC_ROWS(false, false, 8, false);
   } else {
-    if (pb.may_err) k_class_rows<true, true><<<g, 256, 0, st>>>(ra);
-    else k_class_rows<true, false><<<g, 256, 0, st>>>(ra);
+    if (kct == 4) loop ? CYC_ROWS(true, false, 4, true) : CYC_ROWS(true, false, 4, false);
+    else loop ? CYC_ROWS(true, false, 8, true) : CYC_ROWS(true, false, 8, false);
   }
+#undef CYC_ROWS
 }
 
 // 7. emit of direction d's plane
@@ -1790,6 +1843,21 @@ int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
   });
 }
 
+int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
+  if (!c || !out || n < 2) return CYC_ERR_ARG;
+  if (!c->timed) return fail(c, CYC_ERR_ARG, "no run yet");
+  return guarded(c, [&]() -> int {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    for (int d = 0; d < 2; d++) {
+      uint32_t v = 0xFFFFFFFFu;
+      if (c->dir[d].n && c->n_act[d]) HIPCHK(hipMemcpy(&v, c->dir[d].rep_cnt(), 4, hipMemcpyDeviceToHost));
+      out[d] = int64_t(uint32_t(v + 1u));
+    }
+    return (int)CYC_OK;
+  });
+}
+
 int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return CYC_ERR_ARG;
   if (std::string(name) == "emit_variant") {
@@ -1800,6 +1868,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   if (std::string(name) == "emit_blocks") {
     if (value < 0) return fail(c, CYC_ERR_ARG, "emit_blocks must be >= 0");
     c->emit_blocks = value;
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
+  if (std::string(name) == "class_variant_in" || std::string(name) == "class_variant_eg") {
+    if (value < 0 || value > 3) return fail(c, CYC_ERR_ARG, "class_variant must be 0..3");
+    c->class_variant[std::string(name) == "class_variant_eg" ? 1 : 0] = int(value);
     drop_graph(c);
     return (int)CYC_OK;
   }

@@ -129,6 +129,12 @@ class Engine:
         """TargetsApplyingToPod per direction for QueryTargetPod dicts {Namespace, Labels}."""
         return self._json_out(lib().cyc_query_targets, list(pods))
 
+    def classes(self):
+        """(ingress, egress) number of distinct classes of the last run."""
+        out = (ctypes.c_int64 * 2)()
+        check(self._ctx, lib().cyc_last_classes(self._ctx, out, 2))
+        return int(out[0]), int(out[1])
+
     def set_option(self, name: str, value: int):
         check(self._ctx, lib().cyc_set_option(self._ctx, name.encode(), int(value)))
 

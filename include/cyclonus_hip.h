@@ -110,7 +110,13 @@ int cyc_probe_run_host(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_
  * plane), [2] class rows of both directions. */
 int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 
+/* Diagnostic: number of distinct classes (class rows computed) of the last run, [0] ingress,
+ * [1] egress (synchronises the device). */
+int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
+
 /* Tuning knobs (no effect on results): "emit_variant" 0..5 selects the emit store pattern;
+ * "class_variant_in" / "class_variant_eg" 0..3 the class-row kernel shape (bit 0: 4 job slots
+ * per thread instead of 8; bit 1: block rows stride over the class representatives);
  * "emit_blocks" the persistent emit grid (0 = one block per row); "graph_branches" (default 1)
  * runs ingress and egress as two concurrent branches of the step graph;
  * "graphs" (default 1) replays the pipeline as one captured hipGraph when the inputs cannot

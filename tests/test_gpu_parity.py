@@ -227,12 +227,15 @@ def test_graph_and_eager_paths_agree(gpu):
         outs = []
         # (graphs, graph_branches, emit_blocks, emit_variant): eager, two-branch graph (replayed),
         # single-branch graph, tiny persistent emit grid, one block per row, other store variants
-        for graphs, branches, blocks, variant in ((0, 1, 1024, 0), (1, 1, 1024, 0), (1, 1, 1024, 0), (1, 0, 1024, 0),
-                                                  (1, 1, 8, 0), (0, 1, 0, 0), (0, 1, 16, 3), (1, 1, 0, 5)):
+        for graphs, branches, blocks, variant, cls in ((0, 1, 1024, 0, 0), (1, 1, 1024, 0, 0), (1, 1, 1024, 0, 0),
+                                                       (1, 0, 1024, 0, 1), (1, 1, 8, 0, 2), (0, 1, 0, 0, 3),
+                                                       (0, 1, 16, 3, 1), (1, 1, 0, 5, 2)):
             eng.set_option("graphs", graphs)
             eng.set_option("graph_branches", branches)
             eng.set_option("emit_blocks", blocks)
             eng.set_option("emit_variant", variant)
+            eng.set_option("class_variant_in", cls)
+            eng.set_option("class_variant_eg", 3 - cls)
             d_in = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_eg = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_st = torch.zeros((P, K), dtype=torch.uint8, device="cuda")
