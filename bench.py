@@ -233,10 +233,12 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = cells / (dt / args.steps)
 
-    # k_emit launches once per plane (ingress, egress): per launch it writes one plane of this
-    # rank's rows once (rows x K x W x 8 B = 2 bits per cell); emit_ms covers both launches
-    emit_bytes = rows * K * W * 8
-    emit_launch_ms = emit_ms / 2
+    # k_emit writes each plane (ingress, egress) of this rank's rows once: rows x K x W x 8 B per
+    # plane = 2 bits per cell.  Merged (default): ONE launch writes both planes; else one launch
+    # per plane.  emit_ms covers every emit launch of the step.
+    launches = 1 if eng.get_option("emit_merged") else 2
+    emit_bytes = rows * K * W * 8 * (2 // launches)
+    emit_launch_ms = emit_ms / launches
     achieved = emit_bytes / (emit_launch_ms * 1e-3) / 1e9
 
     # HBM traffic of k_emit from the committed PMC passes for this same workload (rocprofv3
@@ -288,10 +290,10 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": emit_bytes,
                 "emit_ms_per_launch": emit_launch_ms,
-                "launches_per_step": 2,
+                "launches_per_step": launches,
                 "fill_ceiling_GBs": fill_gbs,
             },
-            "launch": "one captured hipGraph per step (cyc_set_option graphs=1): shared front, then ingress and egress branches on two streams",
+            "launch": "one captured hipGraph per step (cyc_set_option graphs=1): shared front, ingress and egress fronts as two graph branches, then one emit launch writing both planes",
             "pipeline_ms": {"total": pipe_ms, "emit": emit_ms, "class_rows": rows_ms, "front": pipe_ms - emit_ms - rows_ms},
         }
         if assembled is not None:

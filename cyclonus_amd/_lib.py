@@ -34,6 +34,7 @@ EXPORTS = [
     "cyc_last_timings",
     "cyc_last_classes",
     "cyc_set_option",
+    "cyc_get_option",
     "cyc_query_traffic",
     "cyc_query_traffic_targets",
     "cyc_query_targets",
@@ -54,7 +55,8 @@ class CyclonusPanic(CyclonusError):
 class ProbeShape(ctypes.Structure):
     _fields_ = [
         (n, ctypes.c_int64)
-        for n in ("pods", "slots", "words", "configs", "targets_in", "targets_eg", "peers", "classes_in", "classes_eg", "may_panic")
+        for n in ("pods", "slots", "words", "configs", "targets_in", "targets_eg", "peers", "classes_in", "classes_eg", "may_panic",
+                  "selectors", "label_sets", "pod_peers", "ip_peers", "descriptors", "max_word_runs")
     ]
 
     def as_dict(self):
@@ -89,6 +91,7 @@ def lib():
         L.cyc_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i]
         L.cyc_last_classes.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), i]
         L.cyc_set_option.argtypes = [vp, cp, i64]
+        L.cyc_get_option.argtypes = [vp, cp, ctypes.POINTER(i64)]
         L.cyc_query_traffic.argtypes = [vp, cp, sz, vp, i64]
         L.cyc_query_traffic_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]
         L.cyc_query_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]

@@ -22,7 +22,13 @@
 //                   the roofline kernel)
 //   k_first_error / k_error_detail   only when the inputs can panic: first panicking job in
 //                   the reference's job order and the panic message.
+#include <dlfcn.h>
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+
+#include <csignal>
+#include <cstdlib>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -96,6 +102,71 @@ __global__ void k_selectors(uint32_t S, uint32_t L, const uint32_t* sel_off, con
     if (sel_list) s = sel_list[s];
     selres[uint64_t(s) * L + l] = eval_selector(sel_off, reqs, req_vals, ls_off, ls_key, ls_val, s, l);
   }
+}
+
+// Same evaluation over a dense label table: LVT[kx][l] = value id of dense key kx in label set l
+// (~0 = key absent; column NK is all-absent for selector keys no label set has), and dreqs with
+// the key replaced by its dense index.  One coalesced load per requirement instead of a binary
+// search over the label set (a chain of dependent loads).
+constexpr uint32_t SEL_LPT = 4;  // label sets per thread in k_selectors_dense (independent loads in flight)
+__global__ __launch_bounds__(256) void k_selectors_dense(uint32_t S, uint32_t L, const uint32_t* __restrict__ sel_off,
+                                                         const DReq* __restrict__ dreqs, const uint32_t* __restrict__ req_vals,
+                                                         const uint32_t* __restrict__ LVT, uint8_t* __restrict__ selres,
+                                                         const uint32_t* __restrict__ sel_list) {
+  // block = (selector, 256 * SEL_LPT label sets): the requirement walk is block-uniform (scalar
+  // loads); each thread evaluates SEL_LPT label sets with their table loads issued together
+  const uint32_t lchunks = (L + 256 * SEL_LPT - 1) / (256 * SEL_LPT);
+  uint32_t s = blockIdx.x / lchunks;
+  const uint32_t l0 = (blockIdx.x % lchunks) * 256 * SEL_LPT + threadIdx.x;
+  if (s >= S) return;
+  if (sel_list) s = sel_list[s];
+  uint8_t res[SEL_LPT];
+#pragma unroll
+  for (uint32_t x = 0; x < SEL_LPT; x++) res[x] = 1;
+  for (uint32_t r = sel_off[s]; r < sel_off[s + 1]; r++) {
+    const DReq q = dreqs[r];
+    if (q.op == REQ_INVALID) {  // reached only by label sets every earlier requirement matched
+#pragma unroll
+      for (uint32_t x = 0; x < SEL_LPT; x++) res[x] = res[x] == 1 ? 2 : res[x];
+      break;
+    }
+    uint32_t v[SEL_LPT];
+#pragma unroll
+    for (uint32_t x = 0; x < SEL_LPT; x++) {
+      const uint32_t l = l0 + x * 256;
+      v[x] = l < L ? LVT[uint64_t(q.key) * L + l] : 0xFFFFFFFFu;
+    }
+    const uint32_t v0 = (q.op == REQ_EQ || q.op == REQ_EQ_EMPTY) ? req_vals[q.voff] : 0u;
+#pragma unroll
+    for (uint32_t x = 0; x < SEL_LPT; x++) {
+      const bool present = v[x] != 0xFFFFFFFFu;
+      bool ok;
+      switch (q.op) {
+        case REQ_EQ: ok = present && v[x] == v0; break;
+        case REQ_EQ_EMPTY: ok = !present || v[x] == v0; break;
+        case REQ_IN:
+        case REQ_NOTIN: {
+          bool in = false;
+          for (uint32_t j = 0; j < q.vcnt; j++) in |= (req_vals[q.voff + j] == v[x]);
+          ok = present && (q.op == REQ_IN ? in : !in);
+          break;
+        }
+        case REQ_EXISTS: ok = present; break;
+        default: ok = !present; break;  // REQ_DNE
+      }
+      if (!ok && res[x] == 1) res[x] = 0;
+    }
+  }
+#pragma unroll
+  for (uint32_t x = 0; x < SEL_LPT; x++) {
+    const uint32_t l = l0 + x * 256;
+    if (l < L) selres[uint64_t(s) * L + l] = res[x];
+  }
+}
+
+__global__ void k_fill_u32(uint32_t* p, uint64_t n, uint32_t v) {
+  const uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  if (i < n) p[i] = v;
 }
 
 // IPNet.Contains after To4 collapse (ipaddress.go:10-20): families must agree.
@@ -276,9 +347,14 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
   return (!lt128(mn, lo) && !lt128(hi, mx)) ? 1 : 2;
 }
 
+// Also records each IP peer's nonzero word span in rng[2 * peer] (first word) and
+// rng[2 * peer + 1] (~last word), both atomicMin'd from 0xFFFFFFFF: CIDRs are address ranges and
+// pods of a namespace have neighbouring addresses, so a peer's row is mostly zero words the
+// class rows can skip without loading them.
 __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
-                                                      const DWordIP* __restrict__ words, uint64_t* __restrict__ PM) {
+                                                      const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
+                                                      uint32_t* __restrict__ rng) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t chunks = (W + 63) / 64;
@@ -311,6 +387,10 @@ __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, u
     }
   }
   if (valid && uniform) PM[uint64_t(t.peer) * W + w] = res;
+  const uint64_t nz = __ballot(valid && uniform && res != 0);
+  const uint32_t w0 = (gw % chunks) * 64;
+  uint32_t lo = nz ? w0 + __ffsll((unsigned long long)nz) - 1 : 0xFFFFFFFFu;
+  uint32_t hi = nz ? w0 + 63 - __clzll((long long)nz) : 0u;
   uint64_t mixed = __ballot(valid && !uniform);
   while (mixed) {
     const uint32_t wl = __ffsll((unsigned long long)mixed) - 1;
@@ -331,6 +411,14 @@ __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, u
     }
     const uint64_t m = __ballot(o == 1);
     if (lane == 0) PM[uint64_t(t.peer) * W + ww] = m;
+    if (m) {
+      lo = min(lo, ww);
+      hi = max(hi, ww);
+    }
+  }
+  if (lane == 0 && lo != 0xFFFFFFFFu) {
+    atomicMin(&rng[2 * t.peer], lo);
+    atomicMin(&rng[2 * t.peer + 1], ~hi);
   }
 }
 
@@ -553,7 +641,126 @@ struct RowArgs {
   const uint64_t* DM;        // egress only [K][D][W]
   uint64_t* A;               // [n_ident][K][W]
   uint64_t* AE;              // [n_ident][K][W] (ERR builds only)
+  // IDO builds (no panic possible, every 64-pod word holds <= IDO_MAX_RUNS identity runs):
+  // pod peers are folded per class into identity-space sets B by k_class_ident, and the class
+  // rows expand B through each word's runs; only IP peers are walked per pod word.
+  const uint64_t* IDOB;      // [pod peers][EW] u64: pod peer matches egress identity e (bit e)
+  const uint32_t* peer_ido;  // peer id -> IDOB row
+  const struct WordRuns* runs;  // [W] each 64-pod word's identity runs (<= IDO_MAX_RUNS)
+  uint64_t* B;               // [n_ident][NB][EW]; NB = K (ingress, per slot) or D (egress, per descriptor)
+  const uint32_t* ip_off;    // [n_ident] host upper bound: IP peers of the identity's namespace's targets
+  uint32_t* ip_cnt;          // [n_ident] IP peers of the class's targets, listed in ip_list as
+  uint4* ip_list;            // (peer, port matcher, first, last nonzero PM word)
+  const uint32_t* ip_rng;    // [R][2] first word, ~last word of each IP peer's nonzero PM words (no-panic runs)
+  uint32_t E, EW, NB;
 };
+
+// Most 64-pod words hold 1-2 identity runs (pods of a deployment are contiguous); IDO builds are
+// used only when no word holds more than IDO_MAX_RUNS runs (host-checked, plan_peers).
+constexpr uint32_t IDO_MAX_RUNS = 4;
+struct WordRuns {
+  uint32_t e[IDO_MAX_RUNS];   // egress identity of each run
+  uint64_t m[IDO_MAX_RUNS];   // its pods in the word (0 = unused run)
+};
+constexpr uint32_t IDO_LDS_BYTES = 48 * 1024;  // staged identity sets per class-row block
+
+// Pod-peer outcomes packed over egress identities: one wave per (64 identities, PB_GROUP pod
+// peers): the identities' (namespace, namespace labels, labels) are loaded once and the group's
+// outcomes (podpeermatcher.go:21-28: namespace then pod matcher) are independent selres gathers;
+// one ballot per peer -> IDOB (no-panic runs only).
+constexpr uint32_t PB_GROUP = 8;
+__global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
+                                                   const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres, uint32_t L,
+                                                   const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
+                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob) {
+  const uint32_t wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t groups = (Rp + PB_GROUP - 1) / PB_GROUP;
+  if (wv >= groups * EW) return;
+  const uint32_t g = wv / EW, ew = wv % EW;
+  const uint32_t e = ew * 64 + lane;
+  const bool live = e < E;
+  const uint32_t ns = live ? id_ns[e] : 0u, nsls = live ? id_nsls[e] : 0u, ls = live ? id_ls[e] : 0u;
+  uint64_t mine = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < PB_GROUP; x++) {
+    const uint32_t p = g * PB_GROUP + x;
+    if (p >= Rp) break;
+    const DPeer pr = peers[pod_peers[p]];
+    const bool m = live && pod_peer_outcome(pr, selres, L, ns, nsls, ls) == 1;
+    const uint64_t b = __ballot(m);
+    if (lane == x) mine = b;
+  }
+  const uint32_t p = g * PB_GROUP + lane;
+  if (lane < PB_GROUP && p < Rp) idob[uint64_t(p) * EW + ew] = mine;
+}
+
+// Per class representative and NB index (ingress: job slot, egress: job descriptor): the set of
+// egress identities its targets' pod / all / ports-for-all peers allow on that port (target.go:29-36
+// is an OR over peers; without a panic its order only matters for early exit).  One wave per
+// (representative, NB index), lanes over 64-identity words.
+template <bool EGRESS, int G>
+__global__ __launch_bounds__(256) void k_class_ident(RowArgs a) {
+  // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
+  const uint32_t wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t nbc = (a.NB + G - 1) / G;
+  const uint32_t r = wv / nbc, nb0 = (wv % nbc) * G;
+  if (r >= *a.rep_cnt + 1u) return;
+  const uint32_t i = a.reps[r];
+  int32_t du[G];
+#pragma unroll
+  for (uint32_t x = 0; x < uint32_t(G); x++) {
+    const uint32_t nb = nb0 + x;
+    du[x] = -1;
+    if (nb < a.NB) {
+      if (EGRESS) du[x] = int32_t(nb);
+      else if (a.id_status[uint64_t(i) * a.K + nb] == CYC_JOB_VALID) du[x] = a.id_desc[uint64_t(i) * a.K + nb];
+    }
+  }
+  const uint32_t n = a.cnt[i];
+  const uint32_t* lst = a.list + a.list_off[i];
+  for (uint32_t ew0 = 0; ew0 < a.EW; ew0 += 64) {
+    const uint32_t ew = ew0 + lane;
+    uint64_t b[G];
+#pragma unroll
+    for (uint32_t x = 0; x < uint32_t(G); x++) b[x] = (n == 0 && du[x] >= 0) ? ~0ull : 0ull;  // no target: allowed (policy.go:158-160)
+    for (uint32_t tj = 0; tj < n; tj++) {
+      const DTarget tg = a.tgt[lst[tj]];
+      for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
+        const DPeer pr = a.peers[j];
+        if (pr.kind == 3) continue;  // IP peers: per pod word, in the class rows
+        const uint8_t* pok = a.portok + uint64_t(pr.port) * a.D;
+        if (pr.kind == 0) {  // AllPeersMatcher
+#pragma unroll
+          for (uint32_t x = 0; x < uint32_t(G); x++) b[x] = du[x] >= 0 ? ~0ull : 0ull;
+          break;
+        }
+        const uint64_t v = pr.kind == 1 ? ~0ull : (ew < a.EW ? a.IDOB[uint64_t(a.peer_ido[j]) * a.EW + ew] : 0ull);
+#pragma unroll
+        for (uint32_t x = 0; x < uint32_t(G); x++)
+          if (du[x] >= 0 && pok[du[x]]) b[x] |= v;  // PortsForAllPeers / pod peer on an allowed port
+      }
+    }
+    if (ew < a.EW) {
+#pragma unroll
+      for (uint32_t x = 0; x < uint32_t(G); x++)
+        if (nb0 + x < a.NB) a.B[(uint64_t(i) * a.NB + nb0 + x) * a.EW + ew] = b[x];
+    }
+  }
+  if (nb0 == 0 && lane == 0) {
+    // the class's IP peers (whatever the port) with nonzero rows, walked per pod word by the class rows
+    uint4* il = a.ip_list + a.ip_off[i];
+    uint32_t m = 0;
+    for (uint32_t tj = 0; tj < n; tj++) {
+      const DTarget tg = a.tgt[lst[tj]];
+      for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
+        const DPeer pr = a.peers[j];
+        if (pr.kind == 0) break;  // AllPeers: the identity sets already allow everything
+        if (pr.kind == 3 && a.ip_rng[2 * j] != 0xFFFFFFFFu) il[m++] = make_uint4(j, pr.port, a.ip_rng[2 * j], ~a.ip_rng[2 * j + 1]);
+      }
+    }
+    a.ip_cnt[i] = m;
+  }
+}
 
 template <bool EGRESS, bool ERR, int KC>
 __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uint32_t kc, uint32_t w) {
@@ -602,6 +809,7 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
           break;
         }
         uint64_t pm = ~0ull, er = 0;
+        if (!ERR && pr.kind == 3 && (w < a.ip_rng[2 * j] || w > ~a.ip_rng[2 * j + 1])) continue;  // zero word
         if (pr.kind >= 2) {
           pm = a.PM[uint64_t(j) * a.W + w];
           if (ERR) er = a.ER[uint64_t(j) * a.W + w];
@@ -664,28 +872,120 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
   }
 }
 
+// Class rows from identity sets (IDO builds).  Block = (class representative, KC job slots,
+// 256 pod words); the representative's identity sets for those slots (ingress) or for every job
+// descriptor (egress) are staged in LDS, each thread expands them over its word's identity runs
+// (one 48-byte record), then ORs in the class's IP peers (PM words; the only per-pod peers).
+__device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const WordRuns& wr) {
+  uint64_t m = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < IDO_MAX_RUNS; x++) {
+    const uint32_t e = wr.e[x];
+    m |= ((brow[e >> 6] >> (e & 63)) & 1) ? wr.m[x] : 0ull;
+  }
+  return m;
+}
+
+template <bool EGRESS, int KC>
+__global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) {
+  extern __shared__ uint64_t sB[];
+  const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
+  const uint32_t kc = (blockIdx.x / chunks) % nkc;
+  const uint32_t r = blockIdx.x / (chunks * nkc);
+  if (r >= *a.rep_cnt + 1u) return;  // whole block
+  const uint32_t i = a.reps[r], k0 = kc * KC;
+  const uint32_t nrow = EGRESS ? a.NB : min(uint32_t(KC), a.K - k0);
+  const uint64_t* src = a.B + (uint64_t(i) * a.NB + (EGRESS ? 0u : k0)) * a.EW;
+  for (uint32_t x = threadIdx.x; x < nrow * a.EW; x += blockDim.x) sB[x] = src[x];
+  __syncthreads();
+  const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
+  if (w >= a.W) return;
+  const WordRuns wr = a.runs[w];
+  const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
+  const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
+  uint64_t valid[KC], allow[KC];
+  int32_t du[KC];
+#pragma unroll
+  for (int kk = 0; kk < KC; kk++) {
+    const uint32_t k = k0 + kk;
+    valid[kk] = 0;
+    allow[kk] = 0;
+    du[kk] = -2;
+    if (k < a.K) {
+      if (EGRESS) {
+        valid[kk] = a.VALID[uint64_t(k) * a.W + w];
+        du[kk] = a.DESCW[uint64_t(k) * a.W + w];
+      } else {
+        const bool v = a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID;
+        valid[kk] = v ? wmask : 0ull;
+        du[kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
+      }
+      if (du[kk] >= 0) {
+        allow[kk] = expand_runs(sB + uint64_t(EGRESS ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wr);
+      } else if (EGRESS && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
+        const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
+        for (uint32_t d = 0; d < a.D; d++) allow[kk] |= expand_runs(sB + uint64_t(d) * a.EW, wr) & dm[uint64_t(d) * a.W];
+      }
+    }
+  }
+  // IP peers (ippeermatcher.go:43-50): per pod word through the PM rows
+  const uint32_t m = a.cnt[i] ? a.ip_cnt[i] : 0u;
+  const uint4* il = a.ip_list + a.ip_off[i];
+  for (uint32_t x = 0; x < m; x++) {
+    const uint4 jp = il[x];
+    if (w < jp.z || w > jp.w) continue;  // outside the peer's nonzero words
+    const uint64_t pm = a.PM[uint64_t(jp.x) * a.W + w];
+    const uint8_t* pok = a.portok + uint64_t(jp.y) * a.D;
+    uint64_t undecided = 0;
+#pragma unroll
+    for (int kk = 0; kk < KC; kk++) {
+      uint64_t okm = 0;
+      if (du[kk] >= 0) {
+        okm = pok[du[kk]] ? ~0ull : 0ull;
+      } else if (EGRESS && du[kk] == -1) {
+        const uint64_t* dm = a.DM + uint64_t(k0 + kk) * a.D * a.W + w;
+        for (uint32_t d = 0; d < a.D; d++)
+          if (pok[d]) okm |= dm[uint64_t(d) * a.W];
+      }
+      allow[kk] |= pm & okm;
+      undecided |= valid[kk] & ~allow[kk];
+    }
+    if (!undecided) break;
+  }
+#pragma unroll
+  for (int kk = 0; kk < KC; kk++) {
+    const uint32_t k = k0 + kk;
+    if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
+  }
+}
+
 // The HBM-bound kernel: every target pod's plane rows are a copy of its class rows.
 // One block per pod.  Blocks are dealt round-robin over the 8 XCDs, so block b works on row
 // (b % 8) * per_xcd + b / 8: each XCD streams a contiguous, class-clustered range of rows and
 // re-reads a class row from its own L2.  16-byte non-temporal stores when the pitch allows.
+// One launch writes `planes` planes (1, or 2 = ingress then egress rows as one row list).
 struct EmitArgs {
-  uint32_t n_rows;            // pods in [row_lo, row_hi)
+  uint32_t n_rows;            // pods in [row_lo, row_hi) per plane
+  uint32_t planes;
   uint32_t row_lo;
-  uint32_t per_xcd;
-  const uint32_t* order;      // pods in [row_lo,row_hi) clustered by this direction's class
-  const uint32_t *pod_id, *class_of;
-  const uint64_t* A;
-  uint64_t* out;
+  uint32_t per_xcd;           // of the planes * n_rows row list
+  const uint32_t* order[2];   // pods in [row_lo,row_hi) clustered by the plane's class
+  const uint32_t *pod_id[2], *class_of[2];
+  const uint64_t* A[2];
+  uint64_t* out[2];
   uint64_t row_words;         // K * W
   uint32_t blocks_per_xcd;    // persistent launch: blocks of one XCD stride over its row segment
+  uint32_t chunk;             // CHUNK variant: rows per XCD chunk
 };
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 template <bool VEC, int UNROLL, bool NT>
-__device__ __forceinline__ void emit_row(const EmitArgs& a, uint32_t p) {
-  const uint64_t* src = a.A + uint64_t(a.class_of[a.pod_id[p]]) * a.row_words;
-  uint64_t* dst = a.out + uint64_t(p - a.row_lo) * a.row_words;
+__device__ __forceinline__ void emit_row(const EmitArgs& a, uint32_t r) {
+  const uint32_t pl = r >= a.n_rows ? 1u : 0u;
+  const uint32_t p = a.order[pl][r - pl * a.n_rows];
+  const uint64_t* src = a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words;
+  uint64_t* dst = a.out[pl] + uint64_t(p - a.row_lo) * a.row_words;
   if (VEC) {
     const uint64_t n2 = a.row_words / 2;
     const u64x2* si = reinterpret_cast<const u64x2*>(src);
@@ -719,21 +1019,30 @@ __device__ __forceinline__ void emit_row(const EmitArgs& a, uint32_t p) {
 // Default grid = one block per row; option "emit_blocks" bounds it (persistent blocks striding
 // over their XCD's row segment) to leave CU slots to the other graph branch — measured slower
 // on config #3/#4 (profiles/r01_emit_sweep.txt), so off by default.
-template <bool VEC, int UNROLL, bool NT, bool XCD = true>
+// CHUNK (variant 6): one block per row, rows dealt to the XCDs in chunks of a.chunk consecutive
+// rows (chunk c -> XCD c % 8), so the 8 XCDs stream neighbouring chunks instead of 8 row ranges
+// a whole plane apart, while consecutive (same-class) rows still share one XCD's L2.
+template <bool VEC, int UNROLL, bool NT, bool XCD = true, bool CHUNK = false>
 __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = blockIdx.x, n = a.n_rows * a.planes;
   uint32_t r, r_end, r_step;
+  if (CHUNK) {
+    const uint32_t j = b >> 3;
+    r = ((j / a.chunk) * 8 + (b & 7)) * a.chunk + j % a.chunk;
+    if (r < n) emit_row<VEC, UNROLL, NT>(a, r);
+    return;
+  }
   if (XCD) {  // block b runs on XCD b % 8: rows [x*per_xcd, (x+1)*per_xcd), stride blocks_per_xcd
     const uint32_t x = b & 7;
     r = x * a.per_xcd + (b >> 3);
-    r_end = min(a.n_rows, (x + 1) * a.per_xcd);
+    r_end = min(n, (x + 1) * a.per_xcd);
     r_step = a.blocks_per_xcd;
   } else {
     r = b;
-    r_end = a.n_rows;
+    r_end = n;
     r_step = a.blocks_per_xcd * 8;
   }
-  for (; r < r_end; r += r_step) emit_row<VEC, UNROLL, NT>(a, a.order[r]);
+  for (; r < r_end; r += r_step) emit_row<VEC, UNROLL, NT>(a, r);
 }
 
 // ---------------------------------------------------------------- panic path (rare)
@@ -951,7 +1260,7 @@ struct Identities {  // pod identities for one direction
 
 struct DirDev {
   DevBuf id_ns, id_ls, id_desc, id_status, list_off, list, cnt, hash, err, ht_key, ht_rep, class_of, A, AE, tns_lo,
-      tns_hi, tgt, pod_id, reps;
+      tns_hi, tgt, pod_id, reps, B, ip_off, ip_cnt, ip_list;
   uint32_t n = 0, ht_cap = 0;
   // hash table buffer = [cap] u64 keys, [cap] u32 reps, 1 u32 representative counter: one
   // 0xFF memset per run empties the table and sets the counter to ~0 (= count - 1 for 0)
@@ -964,6 +1273,8 @@ struct PeerPlan {
   std::vector<uint64_t> run_mask;
   std::vector<DIPTest> ip_tests;
   std::vector<DCidr> ip_ex;
+  uint32_t max_runs = 0;  // most identity runs in one 64-pod word
+  std::vector<WordRuns> runs;  // [W] when max_runs <= IDO_MAX_RUNS
 };
 struct cyc_ctx {
   int device = 0;
@@ -979,20 +1290,30 @@ struct cyc_ctx {
       pents, peers, descs, slot_desc, slot_status, slot_cfg, slot_idx;
   DevBuf selres, PM, ER, portok, VALID, DESCW, DM, first_err, order[2];
   // peer-row stage: pod peers in identity space + per-word identity runs; IP peers per pod
-  DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words;
+  DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
+  bool dense_sel = false;  // k_selectors_dense (LVT fits)
   uint32_t Rp = 0, Ri = 0;
   uint32_t rp_off[3] = {0, 0, 0}, ri_off[3] = {0, 0, 0};  // per-direction sub-lists (ingress, egress)
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
   DevBuf act[2], sel_list;
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
   int emit_variant = 0;  // tuning knob (cyc_set_option "emit_variant")
+  int64_t emit_chunk = 64;  // cyc_set_option "emit_chunk": rows per XCD chunk (emit_variant 6)
   int64_t emit_blocks = 0;  // cyc_set_option "emit_blocks": persistent emit grid (0 = a block per row)
-  int class_variant[2] = {3, 1};  // cyc_set_option "class_variant_in" / "_eg" (enq_class_rows;
+  int class_variant[2] = {3, 3};  // cyc_set_option "class_variant_in" / "_eg" (enq_class_rows;
                                   // defaults measured best on configs #3/#4: profiles/r01_class_sweep.txt)
   bool use_graphs = true;  // cyc_set_option "graphs"
+  int pod_words = -1;  // cyc_set_option "pod_words": pod-peer words in the class rows from IDO (1), from
+                       // materialised PM rows (0), or IDO when every word has <= IDO_MAX_RUNS runs (-1)
+  int graph_stagger = 1;  // cyc_set_option "graph_stagger": 1 = egress class rows wait for the ingress
+                          // ones (they run under the ingress emit), 0 = branches unordered
+  hipEvent_t stagger_ev = nullptr;
+  int emit_merged = 1;  // cyc_set_option "emit_merged": both planes in ONE emit launch after both
+                        // directions' class rows.  A plane's emit grid fills every CU, so a second
+                        // branch's front queued behind it would only run once that emit drains.
   bool graph_branches = true;  // cyc_set_option "graph_branches": ingress / egress as two graph branches
-  hipStream_t cap_stream = nullptr, cap_stream2 = nullptr;  // graph capture: ingress / egress branches
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr, sel_ev = nullptr, ports_ev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   const void* graph_key[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   bool timed_graph = false;
@@ -1108,8 +1429,32 @@ static PeerPlan plan_peers(const Problem& pb, const Identities& eg) {
       pl.run_mask[hit] |= 1ull << (q - q0);
     }
     pl.word_off.push_back(uint32_t(pl.run_e.size()));
+    pl.max_runs = std::max(pl.max_runs, pl.word_off.back() - pl.word_off[pl.word_off.size() - 2]);
+  }
+  if (pl.max_runs <= IDO_MAX_RUNS) {
+    pl.runs.assign(pb.W, WordRuns{});
+    for (uint32_t w = 0; w < pb.W; w++)
+      for (uint32_t x = pl.word_off[w]; x < pl.word_off[w + 1]; x++) {
+        pl.runs[w].e[x - pl.word_off[w]] = pl.run_e[x];
+        pl.runs[w].m[x - pl.word_off[w]] = pl.run_mask[x];
+      }
   }
   return pl;
+}
+
+static uint64_t ido_b_bytes(const cyc_ctx* c, int d) {
+  const uint64_t EW = (c->ids[1].ns.size() + 63) / 64, D = std::max<size_t>(c->pb.descs.size(), 1);
+  return uint64_t(c->ids[d].ns.size()) * (d == 0 ? c->pb.K : D) * EW * 8;
+}
+
+static uint64_t ido_lds_bytes(const cyc_ctx* c) {  // k_class_rows_ido: staged identity-set rows
+  const uint64_t EW = (c->ids[1].ns.size() + 63) / 64, D = std::max<size_t>(c->pb.descs.size(), 1);
+  return std::max<uint64_t>(std::min<uint64_t>(8, c->pb.K), D) * EW * 8;  // KC <= 8 slot rows or D
+}
+
+static bool ido_possible(const cyc_ctx* c) {
+  return !c->pb.may_err && c->plan.max_runs <= IDO_MAX_RUNS && ido_lds_bytes(c) <= IDO_LDS_BYTES &&
+         ido_b_bytes(c, 0) + ido_b_bytes(c, 1) <= (1ull << 30);
 }
 
 static void prepare_device(cyc_ctx* c) {
@@ -1137,7 +1482,24 @@ static void prepare_device(cyc_ctx* c) {
   upload(c->slot_idx, pb.slot_idx);
   uint64_t R = pb.peers.size(), W = pb.W, D = std::max<size_t>(pb.descs.size(), 1), K = pb.K;
   c->selres.alloc(std::max<uint64_t>(uint64_t(pb.S) * pb.L, 16));
+  {  // dense label table for k_selectors_dense: label keys -> dense index kx, LVT[kx][l]
+    std::vector<int32_t> kx(pb.strings.size(), -1);
+    uint32_t nk = 0;
+    for (uint32_t k : pb.ls_key)
+      if (kx[k] < 0) kx[k] = int32_t(nk++);
+    c->dense_sel = uint64_t(nk + 1) * pb.L * 4 <= (256ull << 20);
+    if (c->dense_sel) {
+      std::vector<uint32_t> lvt(uint64_t(nk + 1) * pb.L, 0xFFFFFFFFu);
+      for (uint32_t l = 0; l < pb.L; l++)
+        for (uint32_t x = pb.ls_off[l]; x < pb.ls_off[l + 1]; x++) lvt[uint64_t(kx[pb.ls_key[x]]) * pb.L + l] = pb.ls_val[x];
+      std::vector<DReq> dr = pb.reqs;
+      for (DReq& q : dr) q.key = (q.op != REQ_INVALID && q.key < kx.size() && kx[q.key] >= 0) ? uint32_t(kx[q.key]) : nk;
+      upload(c->lvt, lvt);
+      upload(c->dreqs, dr);
+    }
+  }
   c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
+  c->ip_rng.alloc(std::max<uint64_t>(R * 8, 16));
   c->ER.alloc(pb.may_err ? std::max<uint64_t>(R * W * 8, 16) : 16);
   {
     c->plan = plan_peers(pb, c->ids[1]);
@@ -1145,6 +1507,7 @@ static void prepare_device(cyc_ctx* c) {
     upload(c->word_off, pl.word_off);
     upload(c->run_e, pl.run_e);
     upload(c->run_mask, pl.run_mask);
+    upload(c->runs, pl.runs);
     upload(c->id_nsls, c->ids[1].nsls);
     {  // per-word, per-family address intervals for k_ip_rows_fast
       std::vector<DWordIP> wi(pb.W);
@@ -1170,6 +1533,7 @@ static void prepare_device(cyc_ctx* c) {
       upload(c->ip_words, wi);
     }
     c->ido.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * c->ids[1].ns.size(), 16));
+    c->idob.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * ((c->ids[1].ns.size() + 63) / 64) * 8, 16));
   }
   c->portok.alloc(std::max<uint64_t>(pb.pms.size() * D, 16));
   c->VALID.alloc(std::max<uint64_t>(K * W * 8, 16));
@@ -1200,6 +1564,16 @@ static void prepare_device(cyc_ctx* c) {
     dd.A.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
     if (pb.may_err) dd.AE.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
     else dd.AE.alloc(0);
+    dd.B.alloc(ido_possible(c) ? std::max<uint64_t>(ido_b_bytes(c, d), 16) : 16);
+    {  // IP-peer list bounds per identity: the IP peers of its namespace's targets
+      std::vector<uint32_t> ns_ip(pb.strings.size(), 0), off(dd.n + 1, 0);
+      for (const DTarget& t : pb.tgt[d])
+        for (uint32_t j = t.poff; j < t.poff + t.pcnt; j++) ns_ip[t.ns] += pb.peers[j].kind == PK_IP;
+      for (uint32_t i = 0; i < dd.n; i++) off[i + 1] = off[i] + ns_ip[I.ns[i]];
+      upload(dd.ip_off, off);
+      dd.ip_cnt.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
+      dd.ip_list.alloc(std::max<uint64_t>(uint64_t(off[dd.n]) * 16, 16));
+    }
   }
   c->order_lo = c->order_hi = -1;
 }
@@ -1319,6 +1693,11 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   c->Rp = uint32_t(pp.size());
   c->Ri = uint32_t(ip.size());
   upload(c->pod_peers, pp);
+  {
+    std::vector<uint32_t> pi(std::max<size_t>(pb.peers.size(), 1), 0);
+    for (size_t x = 0; x < pp.size(); x++) pi[pp[x]] = uint32_t(x);
+    upload(c->peer_ido, pi);
+  }
   upload(c->ip_peers, ip);
   upload(c->ip_tests, tests);
   upload(c->ip_ex, c->plan.ip_ex);
@@ -1329,15 +1708,25 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
 // Pipeline pieces.  Steps 1, 3, 4 are shared; steps 2 and 5-7 run per direction (ingress peers,
 // targets, class rows and plane are disjoint from egress ones), so the two directions can run
 // as two independent branches: one direction's front hides under the other's HBM-bound emit.
-static void enq_common(cyc_ctx* c, hipStream_t st) {
+enum { COMMON_SELECTORS = 1, COMMON_PORTS = 2, COMMON_ALL = 3 };
+static void enq_common(cyc_ctx* c, hipStream_t st, int parts = COMMON_ALL) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size());
+  if ((parts & COMMON_PORTS) && !pb.may_err && c->Ri)  // IP-peer word spans (k_ip_rows_fast)
+    k_fill_u32<<<grid1(c->ip_rng.bytes / 4, 256), 256, 0, st>>>(c->ip_rng.as<uint32_t>(), c->ip_rng.bytes / 4, 0xFFFFFFFFu);
+  if (!(parts & COMMON_SELECTORS)) goto ports;
   // 1. selectors x label sets
-  if (uint64_t(c->n_sel) * pb.L)
+  if (uint64_t(c->n_sel) * pb.L && c->dense_sel)
+    k_selectors_dense<<<unsigned(uint64_t(c->n_sel) * ((pb.L + 256 * SEL_LPT - 1) / (256 * SEL_LPT))), 256, 0, st>>>(
+        c->n_sel, pb.L, c->sel_off.as<uint32_t>(), c->dreqs.as<DReq>(), c->req_vals.as<uint32_t>(), c->lvt.as<uint32_t>(),
+        c->selres.as<uint8_t>(), c->sel_list.as<uint32_t>());
+  else if (uint64_t(c->n_sel) * pb.L)
     k_selectors<<<grid1(uint64_t(c->n_sel) * pb.L, 256), 256, 0, st>>>(
         c->n_sel, pb.L, c->sel_off.as<uint32_t>(), c->reqs.as<DReq>(), c->req_vals.as<uint32_t>(), c->ls_off.as<uint32_t>(),
         c->ls_key.as<uint32_t>(), c->ls_val.as<uint32_t>(), c->selres.as<uint8_t>(), c->sel_list.as<uint32_t>());
+ports:
+  if (!(parts & COMMON_PORTS)) return;
   // 3. port matchers x job descriptors
   if (M && pb.descs.size())
     k_portok<<<grid1(uint64_t(M) * D, 256), 256, 0, st>>>(M, D, c->pms.as<DPortM>(), c->pents.as<DPortEntry>(),
@@ -1349,14 +1738,26 @@ static void enq_common(cyc_ctx* c, hipStream_t st) {
         c->DESCW.as<int32_t>(), c->DM.as<uint64_t>());
 }
 
-// 2. peer rows of direction d's peers: pod peers in identity space, expanded over word runs;
-// IP peers per pod
-static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st) {
+// Pod peers folded into per-class identity sets, expanded by the class rows over each word's
+// identity runs (no PM pod rows)?  Needs: no panic possible (the panic path walks PM / ER rows in
+// peer order), few runs per word, and identity sets of bounded size.
+static bool ido_mode(const cyc_ctx* c) { return c->pod_words != 0 && ido_possible(c); }
+
+// 2. peer rows of direction d's peers: pod peers in identity space, expanded over word runs
+// (skipped in IDO mode: the class rows expand them); IP peers per pod
+enum { PEERS_POD = 1, PEERS_IP = 2 };
+static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_POD | PEERS_IP) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, W = pb.W;
   const uint32_t E = c->dir[1].n;
-  const uint32_t r0 = c->rp_off[d], Rp = c->rp_off[d + 1] - r0;
-  if (Rp && E && W) {
+  const uint32_t r0 = c->rp_off[d], Rp = (which & PEERS_POD) ? c->rp_off[d + 1] - r0 : 0u;
+  if (Rp && E && W && ido_mode(c)) {
+    const uint32_t EW = (E + 63) / 64;
+    k_peer_bits<<<unsigned((uint64_t((Rp + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4), 256, 0, st>>>(
+        Rp, E, EW, c->pod_peers.as<uint32_t>() + r0, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
+        c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(),
+        c->idob.as<uint64_t>() + uint64_t(r0) * EW);
+  } else if (Rp && E && W) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
     uint8_t* ido = c->ido.as<uint8_t>() + uint64_t(r0) * E;
     k_peer_ident<<<grid1(uint64_t(Rp) * E, 256), 256, 0, st>>>(Rp, E, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(),
@@ -1370,7 +1771,7 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st) {
       k_pod_rows<false><<<g, 256, 0, st>>>(Rp, E, W, plist, ido, c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(),
                                            c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
   }
-  const uint32_t i0 = c->ri_off[d], Ri = c->ri_off[d + 1] - i0;
+  const uint32_t i0 = c->ri_off[d], Ri = (which & PEERS_IP) ? c->ri_off[d + 1] - i0 : 0u;
   if (Ri && W) {
     const DIPTest* tests = c->ip_tests.as<DIPTest>() + i0;
     if (pb.may_err) {
@@ -1383,7 +1784,8 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st) {
                                          c->ER.as<uint64_t>(), bat);
     } else {
       k_ip_rows_fast<<<unsigned((uint64_t((W + 63) / 64) * Ri + 3) / 4), 256, 0, st>>>(
-          Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>());
+          Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>(),
+          c->ip_rng.as<uint32_t>());
     }
   }
 }
@@ -1438,11 +1840,39 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
                        : c->n_act[d];
   ra.reps = dd.reps.as<uint32_t>();
   ra.rep_cnt = dd.rep_cnt();
+  ra.IDOB = c->idob.as<uint64_t>();
+  ra.peer_ido = c->peer_ido.as<uint32_t>();
+  ra.runs = c->runs.as<WordRuns>();
+  ra.B = dd.B.as<uint64_t>();
+  ra.ip_off = dd.ip_off.as<uint32_t>();
+  ra.ip_cnt = dd.ip_cnt.as<uint32_t>();
+  ra.ip_list = dd.ip_list.as<uint4>();
+  ra.ip_rng = c->ip_rng.as<uint32_t>();
+  ra.E = c->dir[1].n;
+  ra.EW = (ra.E + 63) / 64;
+  ra.NB = d == 0 ? K : D;
+  if (ido_mode(c)) {  // identity sets first (one wave per representative and 4 slots / descriptors)
+    const uint64_t waves = uint64_t(c->n_act[d]) * ((ra.NB + 3) / 4);
+    if (d == 0) k_class_ident<false, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
+    else k_class_ident<true, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
+  }
   unsigned g = unsigned(per_rep * ra.rep_blocks);
 #define CYC_ROWS(EG, ERR, KCT, LOOP) k_class_rows<EG, ERR, KCT, LOOP><<<g, 256, 0, st>>>(ra)
   if (pb.may_err) {
     if (d == 0) CYC_ROWS(false, true, 8, false);
     else CYC_ROWS(true, true, 8, false);
+  } else if (ido_mode(c)) {
+    // KC = kct job slots per thread (class_variant bit 0: 4, else 8)
+    const uint32_t rows = d == 0 ? std::min<uint32_t>(kct, K) : D;
+    const unsigned gi = unsigned(uint64_t((W + 255) / 256) * ((K + kct - 1) / kct) * c->n_act[d]);
+    const size_t lds = size_t(rows) * ra.EW * 8;
+    if (kct == 4) {
+      if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, lds, st>>>(ra);
+      else k_class_rows_ido<true, 4><<<gi, 256, lds, st>>>(ra);
+    } else {
+      if (d == 0) k_class_rows_ido<false, 8><<<gi, 256, lds, st>>>(ra);
+      else k_class_rows_ido<true, 8><<<gi, 256, lds, st>>>(ra);
+    }
   } else if (d == 0) {
     if (kct == 4) loop ? CYC_ROWS(false, false, 4, true) : CYC_ROWS(false, false, 4, false);
     else loop ? CYC_ROWS(false, false, 8, true) : CYC_ROWS(false, false, 8, false);
@@ -1453,36 +1883,49 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 #undef CYC_ROWS
 }
 
-// 7. emit of direction d's plane
-static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t lo, int64_t hi) {
+// 7. emit of direction d's plane (d = 2: both planes in one launch, out = ingress, out2 = egress)
+static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t lo, int64_t hi, uint64_t* out2 = nullptr) {
   Problem& pb = c->pb;
   const uint32_t K = pb.K, W = pb.W;
   if (hi <= lo || !K || !W) return;
   EmitArgs ea{};
   ea.n_rows = uint32_t(hi - lo);
+  ea.planes = d == 2 ? 2 : 1;
   ea.row_lo = uint32_t(lo);
-  ea.order = c->order[d].as<uint32_t>();
-  ea.pod_id = c->dir[d].pod_id.as<uint32_t>();
-  ea.class_of = c->dir[d].class_of.as<uint32_t>();
-  ea.A = c->dir[d].A.as<uint64_t>();
-  ea.out = out;
+  for (uint32_t pl = 0; pl < ea.planes; pl++) {
+    const int dd = d == 2 ? int(pl) : d;
+    ea.order[pl] = c->order[dd].as<uint32_t>();
+    ea.pod_id[pl] = c->dir[dd].pod_id.as<uint32_t>();
+    ea.class_of[pl] = c->dir[dd].class_of.as<uint32_t>();
+    ea.A[pl] = c->dir[dd].A.as<uint64_t>();
+    ea.out[pl] = pl ? out2 : out;
+  }
   ea.row_words = uint64_t(K) * W;
-  ea.per_xcd = (ea.n_rows + 7) / 8;
+  ea.per_xcd = (ea.n_rows * ea.planes + 7) / 8;
   // persistent grid: emit_blocks per launch (0 = one block per row)
   ea.blocks_per_xcd = c->emit_blocks ? std::min<uint32_t>(ea.per_xcd, std::max<uint32_t>(1, uint32_t(c->emit_blocks / 8)))
                                      : ea.per_xcd;
-  bool vec = (ea.row_words % 2 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+  const bool aligned = reinterpret_cast<uintptr_t>(out) % 16 == 0 && (!out2 || reinterpret_cast<uintptr_t>(out2) % 16 == 0);
+  const bool vec = (ea.row_words % 2 == 0) && aligned;
   unsigned g = ea.blocks_per_xcd * 8;
-  if (!vec) k_emit<false, 1, false><<<g, 256, 0, st>>>(ea);
+  ea.chunk = uint32_t(std::max<int64_t>(1, c->emit_chunk));
+  if (vec && c->emit_variant == 6) {  // one block per row slot of the chunked deal
+    const uint32_t n = ea.n_rows * ea.planes, per = 8 * ea.chunk;
+    g = (n + per - 1) / per * per;
+  }
+#define CYC_EMIT(V, U, N, X) k_emit<V, U, N, X><<<g, 256, 0, st>>>(ea)
+  if (!vec) CYC_EMIT(false, 1, false, true);
   else switch (c->emit_variant) {  // 0 = default (measured fastest, profiles/r01_emit_sweep.txt:
                                    // UNROLL 16 x 16 B in flight per thread, nt stores, XCD-mapped)
-      case 1: k_emit<true, 1, true><<<g, 256, 0, st>>>(ea); break;
-      case 2: k_emit<true, 4, false><<<g, 256, 0, st>>>(ea); break;
-      case 3: k_emit<true, 4, true><<<g, 256, 0, st>>>(ea); break;
-      case 4: k_emit<true, 8, true><<<g, 256, 0, st>>>(ea); break;
-      case 5: k_emit<true, 16, true, false><<<g, 256, 0, st>>>(ea); break;
-      default: k_emit<true, 16, true><<<g, 256, 0, st>>>(ea); break;
+      case 1: CYC_EMIT(true, 1, true, true); break;
+      case 2: CYC_EMIT(true, 4, false, true); break;
+      case 3: CYC_EMIT(true, 4, true, true); break;
+      case 4: CYC_EMIT(true, 8, true, true); break;
+      case 5: CYC_EMIT(true, 16, true, false); break;
+      case 6: k_emit<true, 16, true, true, true><<<g, 256, 0, st>>>(ea); break;
+      default: CYC_EMIT(true, 16, true, true); break;
     }
+#undef CYC_EMIT
 }
 
 // Eager launch, in phase order with the timing events: [0] start, [1] after the front (peer
@@ -1497,8 +1940,12 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
   HIPCHK(hipEventRecord(c->ev[1], st));
   for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
   HIPCHK(hipEventRecord(c->ev[2], st));
-  enq_emit(c, 0, st, d_in, lo, hi);
-  enq_emit(c, 1, st, d_eg, lo, hi);
+  if (c->emit_merged) {
+    enq_emit(c, 2, st, d_in, lo, hi, d_eg);
+  } else {
+    enq_emit(c, 0, st, d_in, lo, hi);
+    enq_emit(c, 1, st, d_eg, lo, hi);
+  }
   HIPCHK(hipEventRecord(c->ev[3], st));
   if (d_status && uint64_t(pb.P) * pb.K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
@@ -1506,22 +1953,50 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
 
 // Graph capture: shared front on st, then the ingress branch on st and the egress branch on st2
 // (fork / join through events, recorded into the graph as dependencies).
-static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status,
-                             int64_t lo, int64_t hi) {
+static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStream_t st3, uint64_t* d_in, uint64_t* d_eg,
+                             uint8_t* d_status, int64_t lo, int64_t hi) {
   Problem& pb = c->pb;
-  if (!c->graph_branches) st2 = st;
-  enq_common(c, st);
-  HIPCHK(hipEventRecord(c->fork_ev, st));
-  HIPCHK(hipStreamWaitEvent(st2, c->fork_ev, 0));
-  for (int d = 0; d < 2; d++) {
-    hipStream_t s = d ? st2 : st;
-    enq_peer_rows(c, d, s);
-    enq_member(c, d, s);
-    enq_class_rows(c, d, s);
-    enq_emit(c, d, s, d ? d_eg : d_in, lo, hi);
+  if (!c->graph_branches) st2 = st3 = st;
+  if (c->emit_merged) {
+    // DAG: [st3] IP rows of both directions + port tables || [st] selectors, then per direction
+    // pod-peer sets -> membership / classes -> (wait for st3) class rows; one emit of both planes.
+    HIPCHK(hipEventRecord(c->fork_ev, st));
+    if (st3 != st) HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
+    enq_common(c, st3, COMMON_PORTS);
+    for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st3, PEERS_IP);
+    HIPCHK(hipEventRecord(c->ports_ev, st3));
+    enq_common(c, st, COMMON_SELECTORS);
+    HIPCHK(hipEventRecord(c->sel_ev, st));
+    if (st2 != st) HIPCHK(hipStreamWaitEvent(st2, c->sel_ev, 0));
+    for (int d = 1; d >= 0; d--) {
+      hipStream_t s = d ? st2 : st;
+      enq_peer_rows(c, d, s, PEERS_POD);
+      enq_member(c, d, s);
+      HIPCHK(hipStreamWaitEvent(s, c->ports_ev, 0));
+      enq_class_rows(c, d, s);
+    }
+    HIPCHK(hipEventRecord(c->join_ev, st2));
+    HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
+    enq_emit(c, 2, st, d_in, lo, hi, d_eg);
+  } else {
+    // one branch per direction, each ending with its own plane's emit
+    enq_common(c, st);
+    HIPCHK(hipEventRecord(c->fork_ev, st));
+    HIPCHK(hipStreamWaitEvent(st2, c->fork_ev, 0));
+    const bool stagger = c->graph_stagger && st2 != st;
+    for (int d = 0; d < 2; d++) {
+      hipStream_t s = d ? st2 : st;
+      enq_peer_rows(c, d, s);
+      enq_member(c, d, s);
+      // stagger: the egress class rows start when the ingress ones are done
+      if (stagger && d == 1) HIPCHK(hipStreamWaitEvent(s, c->stagger_ev, 0));
+      enq_class_rows(c, d, s);
+      if (stagger && d == 0) HIPCHK(hipEventRecord(c->stagger_ev, s));
+      enq_emit(c, d, s, d ? d_eg : d_in, lo, hi);
+    }
+    HIPCHK(hipEventRecord(c->join_ev, st2));
+    HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
   }
-  HIPCHK(hipEventRecord(c->join_ev, st2));
-  HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
   if (d_status && uint64_t(pb.P) * pb.K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
 }
@@ -1547,12 +2022,16 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
       if (!c->cap_stream) {
         HIPCHK(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&c->cap_stream2, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->cap_stream3, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&c->sel_ev, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ports_ev, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->stagger_ev, hipEventDisableTiming));
       }
       hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
-      capture_pipeline(c, c->cap_stream, c->cap_stream2, d_in, d_eg, d_status, lo, hi);
+      capture_pipeline(c, c->cap_stream, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status, lo, hi);
       HIPCHK(hipStreamEndCapture(c->cap_stream, &g));
       hipError_t ie = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
       (void)hipGraphDestroy(g);
@@ -1694,8 +2173,34 @@ extern "C" {
 
 const char* cyc_version(void) { return "cyclonus_hip 0.1 (gfx950)"; }
 
+// Diagnostic (env CYC_SEGV_TRACE=1): on SIGSEGV print the native frames as module + offset
+// (resolve offline with addr2line -e <module> <offset>), then die with the default action.
+static void segv_trace(int sig) {
+  void* bt[64];
+  const int n = backtrace(bt, 64);
+  char line[512];
+  for (int i = 0; i < n; i++) {
+    Dl_info di{};
+    int len;
+    if (dladdr(bt[i], &di) && di.dli_fname)
+      len = snprintf(line, sizeof line, "cyc-segv #%d %s +0x%lx %s\n", i, di.dli_fname,
+                     (unsigned long)((char*)bt[i] - (char*)di.dli_fbase), di.dli_sname ? di.dli_sname : "");
+    else
+      len = snprintf(line, sizeof line, "cyc-segv #%d %p\n", i, bt[i]);
+    if (len > 0) (void)!write(2, line, size_t(len));
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int cyc_ctx_create(int device_id, cyc_ctx** out) {
   if (!out) return CYC_ERR_ARG;
+  static const bool trace = [] {
+    const char* e = getenv("CYC_SEGV_TRACE");
+    if (e && *e == '1') signal(SIGSEGV, segv_trace);
+    return true;
+  }();
+  (void)trace;
   // No HIP call here: policy compilation / IR export work on a host without a GPU; the device
   // is initialised by the first call that needs it (cyc_probe_prepare).
   auto* c = new cyc_ctx();
@@ -1712,8 +2217,12 @@ void cyc_ctx_destroy(cyc_ctx* c) {
     destroy_events(c);
     if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
     if (c->cap_stream2) (void)hipStreamDestroy(c->cap_stream2);
+    if (c->cap_stream3) (void)hipStreamDestroy(c->cap_stream3);
+    if (c->sel_ev) (void)hipEventDestroy(c->sel_ev);
+    if (c->ports_ev) (void)hipEventDestroy(c->ports_ev);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    if (c->stagger_ev) (void)hipEventDestroy(c->stagger_ev);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -1788,6 +2297,12 @@ int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* s
       shape->classes_in = c->dir[0].n;
       shape->classes_eg = c->dir[1].n;
       shape->may_panic = c->pb.may_err ? 1 : 0;
+      shape->selectors = c->pb.S;
+      shape->label_sets = c->pb.L;
+      shape->pod_peers = int64_t(c->plan.pod_peers.size());
+      shape->ip_peers = int64_t(c->plan.ip_peers.size());
+      shape->descriptors = int64_t(c->pb.descs.size());
+      shape->max_word_runs = c->plan.max_runs;
     }
     return (int)CYC_OK;
   });
@@ -1865,6 +2380,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "emit_chunk") {
+    if (value < 1) return fail(c, CYC_ERR_ARG, "emit_chunk must be >= 1");
+    c->emit_chunk = value;
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "emit_blocks") {
     if (value < 0) return fail(c, CYC_ERR_ARG, "emit_blocks must be >= 0");
     c->emit_blocks = value;
@@ -1882,12 +2403,47 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "pod_words") {
+    if (value < -1 || value > 1) return fail(c, CYC_ERR_ARG, "pod_words must be -1, 0 or 1");
+    c->pod_words = int(value);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
+  if (std::string(name) == "emit_merged") {
+    c->emit_merged = int(value != 0);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
+  if (std::string(name) == "graph_stagger") {
+    c->graph_stagger = int(value != 0);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "graphs") {
     c->use_graphs = value != 0;
     drop_graph(c);
     return (int)CYC_OK;
   }
   return fail(c, CYC_ERR_ARG, std::string("unknown option ") + name);
+}
+
+int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
+  if (!c || !name || !value) return CYC_ERR_ARG;
+  const std::string n(name);
+  if (n == "emit_variant") *value = c->emit_variant;
+  else if (n == "emit_blocks") *value = c->emit_blocks;
+  else if (n == "emit_chunk") *value = c->emit_chunk;
+  else if (n == "class_variant_in") *value = c->class_variant[0];
+  else if (n == "class_variant_eg") *value = c->class_variant[1];
+  else if (n == "graph_branches") *value = c->graph_branches;
+  else if (n == "graph_stagger") *value = c->graph_stagger;
+  else if (n == "emit_merged") *value = c->emit_merged;
+  else if (n == "graphs") *value = c->use_graphs;
+  else if (n == "pod_words") {
+    if (!c->prepared) return fail(c, CYC_ERR_ARG, "pod_words: call cyc_probe_prepare first");
+    *value = ido_mode(c) ? 1 : 0;
+  } else return fail(c, CYC_ERR_ARG, std::string("unknown option ") + name);
+  return (int)CYC_OK;
 }
 
 // Shared single-cell runner (k_query).  tlist (optional): per (traffic, direction) the matching

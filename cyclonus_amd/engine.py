@@ -138,6 +138,11 @@ class Engine:
     def set_option(self, name: str, value: int):
         check(self._ctx, lib().cyc_set_option(self._ctx, name.encode(), int(value)))
 
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64(0)
+        check(self._ctx, lib().cyc_get_option(self._ctx, name.encode(), ctypes.byref(v)))
+        return int(v.value)
+
     def timings(self):
         """(pipeline_ms, emit_ms, class_rows_ms) of the last run, from HIP events on its stream."""
         ms = (ctypes.c_double * 3)()

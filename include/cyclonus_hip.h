@@ -71,6 +71,12 @@ typedef struct {
   int64_t classes_in;  /* filled after cyc_probe_run */
   int64_t classes_eg;
   int64_t may_panic;   /* 1 if evaluation can reach a Go panic (invalid CIDR/IP/operator) */
+  int64_t selectors;   /* S: distinct label selectors */
+  int64_t label_sets;  /* L: distinct pod / namespace label sets */
+  int64_t pod_peers;   /* pod-selector peers (pod, namespace or both) */
+  int64_t ip_peers;    /* IPBlock peers */
+  int64_t descriptors; /* D: distinct job descriptors (port, port name, protocol) */
+  int64_t max_word_runs; /* most egress-identity runs in one 64-pod word */
 } cyc_probe_shape;
 
 /* context / errors */
@@ -114,14 +120,21 @@ int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
  * [1] egress (synchronises the device). */
 int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
 
-/* Tuning knobs (no effect on results): "emit_variant" 0..5 selects the emit store pattern;
+/* Tuning knobs (no effect on results): "emit_variant" 0..6 selects the emit store pattern ("emit_chunk": rows per XCD chunk of variant 6);
  * "class_variant_in" / "class_variant_eg" 0..3 the class-row kernel shape (bit 0: 4 job slots
  * per thread instead of 8; bit 1: block rows stride over the class representatives);
  * "emit_blocks" the persistent emit grid (0 = one block per row); "graph_branches" (default 1)
- * runs ingress and egress as two concurrent branches of the step graph;
+ * runs ingress and egress as two concurrent branches of the step graph; "graph_stagger"
+ * (default 1) starts the egress class rows after the ingress ones (under the ingress emit);
+ * "pod_words" -1 (default: auto) / 0 / 1 has the class rows read pod-peer words from materialised
+ * peer rows (0) or expand them from per-identity outcomes through each word's identity runs (1);
  * "graphs" (default 1) replays the pipeline as one captured hipGraph when the inputs cannot
  * panic (then cyc_last_timings reports only the whole-pipeline time). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
+
+/* The setting in effect for a tuning knob of cyc_set_option; for "pod_words" the mode the
+ * prepared probe actually uses (0 or 1, auto resolved; needs cyc_probe_prepare). */
+int cyc_get_option(cyc_ctx* ctx, const char* name, int64_t* value);
 
 /* Single-cell API (policy.go:131-174): traffic_json is a JSON array of matcher.Traffic objects;
  * out[i] = ingress | egress << 1 (allowed bits).  Needs only a loaded policy. */

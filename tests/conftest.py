@@ -6,6 +6,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+# a native crash inside libcyclonus_hip prints its frames (module + offset) before dying
+os.environ.setdefault("CYC_SEGV_TRACE", "1")
 
 
 def pytest_configure(config):

@@ -229,7 +229,9 @@ def test_graph_and_eager_paths_agree(gpu):
         # single-branch graph, tiny persistent emit grid, one block per row, other store variants
         for graphs, branches, blocks, variant, cls in ((0, 1, 1024, 0, 0), (1, 1, 1024, 0, 0), (1, 1, 1024, 0, 0),
                                                        (1, 0, 1024, 0, 1), (1, 1, 8, 0, 2), (0, 1, 0, 0, 3),
-                                                       (0, 1, 16, 3, 1), (1, 1, 0, 5, 2)):
+                                                       (0, 1, 16, 3, 1), (1, 1, 0, 5, 2), (1, 1, 0, 6, 3), (0, 0, 0, 6, 0)):
+            eng.set_option("emit_chunk", 1 + seed % 3)
+            eng.set_option("emit_merged", int(variant != 5))
             eng.set_option("graphs", graphs)
             eng.set_option("graph_branches", branches)
             eng.set_option("emit_blocks", blocks)
@@ -305,3 +307,42 @@ def test_ip_interval_words(gpu, seed):
     pols, res, probes = _ip_interval_problem(seed)
     o, g = run_both(pols, res, probes)
     assert_same(o, g, f"ip intervals seed {seed}")
+
+
+def _deployment_problem(seed, min_run=22):
+    """Random policies over deployment-style pods: each random pod template is replicated into a
+    contiguous run of >= min_run pods (same namespace, labels and containers; own name and IP),
+    so every 64-pod word holds at most 4 identity runs and the class rows can expand pod-peer
+    words from per-identity outcomes (cyc_set_option pod_words = 1)."""
+    import random
+
+    r = random.Random(seed)
+    pols, res, probes = random_problem(40_000 + seed, n_pods=int(r.randint(3, 12)))
+    pods = []
+    for t, tpl in enumerate(res["Pods"]):
+        for j in range(r.randint(min_run, min_run + 40)):
+            q = dict(tpl)
+            q["Name"] = f"{tpl['Name']}-{j}"
+            q["IP"] = f"10.1.{len(pods) // 250}.{len(pods) % 250}" if r.random() < 0.9 else tpl["IP"]
+            pods.append(q)
+    res = dict(res, Pods=pods)
+    return pols, res, probes
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_pod_words_from_identity_runs(gpu, seed):
+    """Class rows with pod-peer words expanded from identity outcomes (IDO) and from
+    materialised peer rows (PM) both equal the oracle, on the graph and the eager path."""
+    pols, res, probes = _deployment_problem(seed)
+    want = Oracle(pols, res).probe(probes)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    eng.prepare(probes)
+    # (pod_words, graphs, class_variant): 4 or 8 job slots per thread, graph and eager paths, and
+    # the PM path
+    for mode, graphs, cv in ((1, 1, 3), (1, 0, 0), (1, 1, 1), (0, 1, 3), (0, 0, 0)):
+        eng.set_option("pod_words", mode)
+        eng.set_option("graphs", graphs)
+        eng.set_option("class_variant_in", cv)
+        eng.set_option("class_variant_eg", cv)
+        assert eng.get_option("pod_words") == mode, "deployment-style words must allow the IDO path"
+        assert_same(want, eng.run_host(), f"seed {seed} pod_words {mode} graphs {graphs} variant {cv}")
