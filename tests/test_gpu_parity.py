@@ -346,3 +346,20 @@ def test_pod_words_from_identity_runs(gpu, seed):
         eng.set_option("class_variant_eg", cv)
         assert eng.get_option("pod_words") == mode, "deployment-style words must allow the IDO path"
         assert_same(want, eng.run_host(), f"seed {seed} pod_words {mode} graphs {graphs} variant {cv}")
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_edge_shapes(gpu, seed):
+    """Empty and ragged inputs, as the reference's tables allow them: no pods, one pod, pod counts
+    on and around 64-pod word boundaries, no policies, no probes, and pods without containers
+    (AllAvailable yields no job for them, resources.go:336-364)."""
+    pols, res, probes = random_problem(60_000 + seed, n_pods=200)
+    eng = Engine(0)
+    for n in (0, 1, 2, 63, 64, 65, 127, 128, 129, 200):
+        r = dict(res, Pods=res["Pods"][:n])
+        assert_same(*run_both(pols, r, probes, engine=eng), f"seed {seed} pods {n}")
+    assert_same(*run_both([], res, probes, engine=eng), f"seed {seed} no policies")
+    assert_same(*run_both(pols, res, [], engine=eng), f"seed {seed} no probes")
+    bare = [dict(p, Containers=[]) if i % 3 == 0 else p for i, p in enumerate(res["Pods"][:70])]
+    assert_same(*run_both(pols, dict(res, Pods=bare), probes + [{"AllAvailable": True}], engine=eng),
+                f"seed {seed} pods without containers")
