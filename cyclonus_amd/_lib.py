@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(_PKG, "libcyclonus_hip.so")
+# CYC_HIP_LIB: another build of the same library (A/B timing of two builds in one GPU session)
+SO_PATH = os.environ.get("CYC_HIP_LIB") or os.path.join(_PKG, "libcyclonus_hip.so")
 
 # cyc_status
 OK, ERR_ARG, ERR_JSON, ERR_INVALID_POLICY, ERR_PANIC_IP, ERR_PANIC_CIDR, ERR_PANIC_SELECTOR = 0, 1, 2, 3, 4, 5, 6

@@ -246,6 +246,37 @@ __global__ __launch_bounds__(256) void k_pod_rows(uint32_t Rp, uint32_t E, uint3
   if (ERR) ER[j * W + w] = e;
 }
 
+// Pod-peer rows straight from each pod's egress identity: one wave per (pod peer, 64-pod word),
+// lane = pod, one ballot per word.  Used when identities are about as many as pods (every pod
+// labelled apart, e.g. a `pod: <name>` label): then the identity-space outcomes cost as much as
+// this and the run expansion above loops over up to 64 runs per word.
+template <bool ERR>
+__global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P, uint32_t W,
+                                                         const uint32_t* __restrict__ pod_peers,
+                                                         const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres,
+                                                         uint32_t L, const uint32_t* __restrict__ pod_eid,
+                                                         const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
+                                                         const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
+                                                         uint64_t* __restrict__ ER) {
+  const uint32_t lane = threadIdx.x & 63, gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t p = gw / W, w = gw - p * W;
+  if (p >= Rp) return;
+  const uint32_t j = pod_peers[p];
+  const DPeer pr = peers[j];
+  const uint32_t q = w * 64 + lane;
+  uint32_t o = 0;
+  if (q < P) {
+    const uint32_t e = pod_eid[q];
+    o = pod_peer_outcome(pr, selres, L, id_ns[e], id_nsls[e], id_ls[e]);
+  }
+  const uint64_t m = __ballot(o == 1);
+  const uint64_t er = ERR ? __ballot(o == 2) : 0ull;
+  if (lane == 0) {
+    PM[uint64_t(j) * W + w] = m;
+    if (ERR) ER[uint64_t(j) * W + w] = er;
+  }
+}
+
 // IP peers depend on each pod's own address: one wave per 64-pod word (one lane per pod).  A
 // block owns IPB_BATCH IP peers: their CIDR and except records (host-flattened, in evaluation
 // order) are staged once into LDS, then every wave tests its lane's IP (loaded once) against
@@ -1045,6 +1076,98 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   for (; r < r_end; r += r_step) emit_row<VEC, UNROLL, NT>(a, r);
 }
 
+// Variant 7 / 8: one block per G consecutive rows of an XCD's segment (rows are clustered by
+// class, so they mostly share one class row): each 16-byte chunk of the class row is loaded once
+// and stored to every row of the group using that class row (rows with another class row load
+// their own).  G x fewer loads per store than one block per row.
+template <int G, int UNROLL>
+__global__ __launch_bounds__(256) void k_emit_group(EmitArgs a) {
+  const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
+  const uint32_t r0 = x * a.per_xcd + (b >> 3) * G, r_end = min(n, (x + 1) * a.per_xcd);
+  if (r0 >= r_end) return;
+  const u64x2* src[G];
+  u64x2* dst[G];
+  bool same[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    const uint32_t r = r0 + g;
+    src[g] = nullptr;
+    dst[g] = nullptr;
+    if (r < r_end) {
+      const uint32_t pl = r >= a.n_rows ? 1u : 0u;
+      const uint32_t p = a.order[pl][r - pl * a.n_rows];
+      src[g] = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
+      dst[g] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
+    }
+    same[g] = src[g] == src[0];
+  }
+  const uint64_t n2 = a.row_words / 2, step = uint64_t(blockDim.x) * UNROLL;
+  for (uint64_t x0 = threadIdx.x; x0 < n2; x0 += step) {
+    u64x2 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      const uint64_t i = x0 + uint64_t(u) * blockDim.x;
+      if (i < n2) v[u] = src[0][i];
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      if (!dst[g]) continue;
+      if (same[g]) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) {
+          const uint64_t i = x0 + uint64_t(u) * blockDim.x;
+          if (i < n2) __builtin_nontemporal_store(v[u], &dst[g][i]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) {
+          const uint64_t i = x0 + uint64_t(u) * blockDim.x;
+          if (i < n2) __builtin_nontemporal_store(src[g][i], &dst[g][i]);
+        }
+      }
+    }
+  }
+}
+
+// Variant 9 (auto for short rows): one block per a.chunk consecutive rows of an XCD's segment,
+// the threads sweeping the rows' 16-byte chunks as one flat range (row = index / chunks per row),
+// so rows shorter than a block's 4 KB-per-pass still keep every lane storing.  The rows' source
+// and destination addresses are staged in LDS first.
+constexpr uint32_t EMIT_FLAT_MAX_ROWS = 256;
+template <int UNROLL>
+__global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
+  __shared__ const u64x2* s_src[EMIT_FLAT_MAX_ROWS];
+  __shared__ u64x2* s_dst[EMIT_FLAT_MAX_ROWS];
+  const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
+  const uint32_t r0 = x * a.per_xcd + (b >> 3) * a.chunk;
+  const uint32_t r_end = min(n, (x + 1) * a.per_xcd);
+  if (r0 >= r_end) return;
+  const uint32_t nr = min(a.chunk, r_end - r0);
+  if (threadIdx.x < nr) {
+    const uint32_t r = r0 + threadIdx.x;
+    const uint32_t pl = r >= a.n_rows ? 1u : 0u;
+    const uint32_t p = a.order[pl][r - pl * a.n_rows];
+    s_src[threadIdx.x] = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
+    s_dst[threadIdx.x] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
+  }
+  __syncthreads();
+  const uint32_t n2 = uint32_t(a.row_words / 2), tot = nr * n2;
+  for (uint32_t i0 = threadIdx.x; i0 < tot; i0 += 256 * UNROLL) {
+    u64x2 v[UNROLL];
+    uint32_t row[UNROLL], col[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      const uint32_t i = i0 + u * 256;
+      row[u] = i / n2;
+      col[u] = i - row[u] * n2;
+      if (i < tot) v[u] = s_src[row[u]][col[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++)
+      if (i0 + u * 256 < tot) __builtin_nontemporal_store(v[u], &s_dst[row[u]][col[u]]);
+  }
+}
+
 // ---------------------------------------------------------------- panic path (rare)
 struct ErrArgs {
   uint32_t P, K, W, n_cfg;
@@ -1297,12 +1420,14 @@ struct cyc_ctx {
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
   DevBuf act[2], sel_list;
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
-  int emit_variant = 0;  // tuning knob (cyc_set_option "emit_variant")
+  int emit_variant = -1;  // tuning knob (cyc_set_option "emit_variant"; -1 = auto by row length)
   int64_t emit_chunk = 64;  // cyc_set_option "emit_chunk": rows per XCD chunk (emit_variant 6)
   int64_t emit_blocks = 0;  // cyc_set_option "emit_blocks": persistent emit grid (0 = a block per row)
   int class_variant[2] = {3, 3};  // cyc_set_option "class_variant_in" / "_eg" (enq_class_rows;
                                   // defaults measured best on configs #3/#4: profiles/r01_class_sweep.txt)
   bool use_graphs = true;  // cyc_set_option "graphs"
+  int pod_rows = -1;   // cyc_set_option "pod_rows": pod-peer PM rows per pod directly (1), through
+                       // identity outcomes and word runs (0), or -1 = direct when identities >= pods / 2
   int pod_words = -1;  // cyc_set_option "pod_words": pod-peer words in the class rows from IDO (1), from
                        // materialised PM rows (0), or IDO when every word has <= IDO_MAX_RUNS runs (-1)
   int graph_stagger = 1;  // cyc_set_option "graph_stagger": 1 = egress class rows wait for the ingress
@@ -1708,12 +1833,12 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
 // Pipeline pieces.  Steps 1, 3, 4 are shared; steps 2 and 5-7 run per direction (ingress peers,
 // targets, class rows and plane are disjoint from egress ones), so the two directions can run
 // as two independent branches: one direction's front hides under the other's HBM-bound emit.
-enum { COMMON_SELECTORS = 1, COMMON_PORTS = 2, COMMON_ALL = 3 };
+enum { COMMON_SELECTORS = 1, COMMON_PORTS = 2, COMMON_FILL = 4, COMMON_ALL = 7 };
 static void enq_common(cyc_ctx* c, hipStream_t st, int parts = COMMON_ALL) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size());
-  if ((parts & COMMON_PORTS) && !pb.may_err && c->Ri)  // IP-peer word spans (k_ip_rows_fast)
+  if ((parts & COMMON_FILL) && !pb.may_err && c->Ri)  // IP-peer word spans (k_ip_rows_fast)
     k_fill_u32<<<grid1(c->ip_rng.bytes / 4, 256), 256, 0, st>>>(c->ip_rng.as<uint32_t>(), c->ip_rng.bytes / 4, 0xFFFFFFFFu);
   if (!(parts & COMMON_SELECTORS)) goto ports;
   // 1. selectors x label sets
@@ -1757,6 +1882,18 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
         Rp, E, EW, c->pod_peers.as<uint32_t>() + r0, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
         c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(),
         c->idob.as<uint64_t>() + uint64_t(r0) * EW);
+  } else if (Rp && E && W && (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= P)) {
+    const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
+    const unsigned g = unsigned((uint64_t(Rp) * W + 3) / 4);
+    const uint32_t* eid = c->dir[1].pod_id.as<uint32_t>();
+    if (pb.may_err)
+      k_pod_rows_direct<true><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
+                                                 c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(),
+                                                 c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
+    else
+      k_pod_rows_direct<false><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
+                                                  c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(),
+                                                  c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
   } else if (Rp && E && W) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
     uint8_t* ido = c->ido.as<uint8_t>() + uint64_t(r0) * E;
@@ -1791,10 +1928,15 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
 }
 
 // 5. membership + classes of direction d
-static void enq_member(cyc_ctx* c, int d, hipStream_t st) {
+static void enq_member_clear(cyc_ctx* c, int d, hipStream_t st) {
+  DirDev& dd = c->dir[d];
+  if (dd.n) HIPCHK(hipMemsetAsync(dd.ht_key.p, 0xFF, dd.ht_key.bytes, st));  // keys and reps: one buffer
+}
+
+static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
   DirDev& dd = c->dir[d];
   if (!dd.n) return;
-  HIPCHK(hipMemsetAsync(dd.ht_key.p, 0xFF, dd.ht_key.bytes, st));  // keys and reps: one buffer
+  if (clear) enq_member_clear(c, d, st);
   MemberArgs ma = member_args(c, d);
   if (!c->n_act[d]) return;
   k_member<<<grid1(c->n_act[d], 128), 128, 0, st>>>(ma);
@@ -1913,9 +2055,20 @@ static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
     const uint32_t n = ea.n_rows * ea.planes, per = 8 * ea.chunk;
     g = (n + per - 1) / per * per;
   }
+  // emit_variant -1 (default) = auto: one block per row (variant 0) for rows of >= 16 KB, else
+  // the flat multi-row sweep (variant 9) over ~32 KB per block
+  const int variant = c->emit_variant >= 0 ? c->emit_variant : (ea.row_words * 8 >= 16384 ? 0 : 9);
+  if (vec && (variant == 7 || variant == 8)) {  // one block per row group of an XCD segment
+    const uint32_t G = variant == 7 ? 2 : 4;
+    g = (ea.per_xcd + G - 1) / G * 8;
+  }
+  if (vec && variant == 9) {
+    ea.chunk = uint32_t(std::min<uint64_t>(EMIT_FLAT_MAX_ROWS, std::max<uint64_t>(1, 32768 / (ea.row_words * 8))));
+    g = (ea.per_xcd + ea.chunk - 1) / ea.chunk * 8;
+  }
 #define CYC_EMIT(V, U, N, X) k_emit<V, U, N, X><<<g, 256, 0, st>>>(ea)
   if (!vec) CYC_EMIT(false, 1, false, true);
-  else switch (c->emit_variant) {  // 0 = default (measured fastest, profiles/r01_emit_sweep.txt:
+  else switch (variant) {  // 0 = default (measured fastest, profiles/r01_emit_sweep.txt:
                                    // UNROLL 16 x 16 B in flight per thread, nt stores, XCD-mapped)
       case 1: CYC_EMIT(true, 1, true, true); break;
       case 2: CYC_EMIT(true, 4, false, true); break;
@@ -1923,6 +2076,9 @@ static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
       case 4: CYC_EMIT(true, 8, true, true); break;
       case 5: CYC_EMIT(true, 16, true, false); break;
       case 6: k_emit<true, 16, true, true, true><<<g, 256, 0, st>>>(ea); break;
+      case 7: k_emit_group<2, 8><<<g, 256, 0, st>>>(ea); break;
+      case 8: k_emit_group<4, 8><<<g, 256, 0, st>>>(ea); break;
+      case 9: k_emit_flat<8><<<g, 256, 0, st>>>(ea); break;
       default: CYC_EMIT(true, 16, true, true); break;
     }
 #undef CYC_EMIT
@@ -1962,7 +2118,7 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
     // pod-peer sets -> membership / classes -> (wait for st3) class rows; one emit of both planes.
     HIPCHK(hipEventRecord(c->fork_ev, st));
     if (st3 != st) HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
-    enq_common(c, st3, COMMON_PORTS);
+    enq_common(c, st3, COMMON_FILL | COMMON_PORTS);
     for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st3, PEERS_IP);
     HIPCHK(hipEventRecord(c->ports_ev, st3));
     enq_common(c, st, COMMON_SELECTORS);
@@ -2409,6 +2565,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "pod_rows") {
+    if (value < -1 || value > 1) return fail(c, CYC_ERR_ARG, "pod_rows must be -1, 0 or 1");
+    c->pod_rows = int(value);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "emit_merged") {
     c->emit_merged = int(value != 0);
     drop_graph(c);
@@ -2438,6 +2600,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "graph_branches") *value = c->graph_branches;
   else if (n == "graph_stagger") *value = c->graph_stagger;
   else if (n == "emit_merged") *value = c->emit_merged;
+  else if (n == "pod_rows") *value = c->pod_rows;
   else if (n == "graphs") *value = c->use_graphs;
   else if (n == "pod_words") {
     if (!c->prepared) return fail(c, CYC_ERR_ARG, "pod_words: call cyc_probe_prepare first");

@@ -2,7 +2,7 @@
 options) for `rocprofv3 --kernel-trace`, then print the last replay's kernels with start / end
 offsets from the replay's first kernel (shows what overlaps what across the two branches).
 
-    rocprofv3 --kernel-trace -d OUT -o run -- python scripts/graph_timeline.py run [config3] [N]
+    rocprofv3 --kernel-trace -d OUT -o run -- python scripts/graph_timeline.py run [config3] [N] [opt=v ...] [shards=N]
     python scripts/graph_timeline.py show OUT/run_results.db
 """
 import json
@@ -17,11 +17,20 @@ if sys.argv[1] == "show":
     db = sqlite3.connect(sys.argv[2])
     rows = db.execute("select s.kernel_name, d.start, d.end from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s "
                       "on d.kernel_id = s.id order by d.start").fetchall()
-    # last replay = kernels after the last k_selectors launch
-    last = max(i for i, r in enumerate(rows) if "k_selectors" in r[0])
-    rows = rows[last:]
-    t0 = rows[0][1]
-    for name, a, b in rows:
+    # replays end with the emit (and the graph's trailing copy, if any): the last replay = the kernels
+    # after the second-to-last emit ended
+    ends = [i for i, r in enumerate(rows) if "k_emit" in r[0]]
+    spans = []
+    for a, b in zip(ends, ends[1:]):
+        seg = rows[a + 1:b + 1]
+        spans.append((min(r[1] for r in seg), max(r[2] for r in seg), rows[a][2]))
+    if spans:
+        import statistics
+        print(f"replays: first kernel -> emit end {statistics.median(s[1] - s[0] for s in spans) / 1e3:.1f} us median; "
+              f"previous emit end -> first kernel {statistics.median(s[0] - s[2] for s in spans) / 1e3:.1f} us median")
+    rows = rows[ends[-2] + 1:] if len(ends) > 1 else rows
+    t0 = min(r[1] for r in rows)
+    for name, a, b in sorted(rows, key=lambda r: r[1]):
         short = name.split("(")[0].replace("_ZN3cyc", "")[:48]
         print(f"{(a - t0) / 1e3:9.1f} us -> {(b - t0) / 1e3:9.1f} us  ({(b - a) / 1e3:8.1f})  {short}")
     sys.exit(0)
@@ -41,10 +50,16 @@ d_in = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
 d_eg = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
 d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
+lo, hi = 0, P
 for opt in sys.argv[4:]:
     k, v = opt.split("=")
-    eng.set_option(k, int(v))
+    if k == "shards":  # rank 0's rows of an N-way shard (cyclonus_amd.shard.row_range)
+        from cyclonus_amd.shard import row_range
+
+        lo, hi = row_range(P, int(v), 0)
+    else:
+        eng.set_option(k, int(v))
 for _ in range(n):
-    eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), st)
+    eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), st, lo, hi)
 torch.cuda.synchronize()
 print(json.dumps({"config": name, "timings_last": eng.timings()}))

@@ -229,8 +229,11 @@ def test_graph_and_eager_paths_agree(gpu):
         # single-branch graph, tiny persistent emit grid, one block per row, other store variants
         for graphs, branches, blocks, variant, cls in ((0, 1, 1024, 0, 0), (1, 1, 1024, 0, 0), (1, 1, 1024, 0, 0),
                                                        (1, 0, 1024, 0, 1), (1, 1, 8, 0, 2), (0, 1, 0, 0, 3),
-                                                       (0, 1, 16, 3, 1), (1, 1, 0, 5, 2), (1, 1, 0, 6, 3), (0, 0, 0, 6, 0)):
+                                                       (0, 1, 16, 3, 1), (1, 1, 0, 5, 2), (1, 1, 0, 6, 3), (0, 0, 0, 6, 0),
+                                                       (1, 1, 0, 7, 1), (0, 1, 0, 8, 2), (1, 0, 0, 8, 0), (1, 1, 0, 9, 1),
+                                                       (0, 1, 0, 9, 3), (1, 1, 0, -1, 0)):
             eng.set_option("emit_chunk", 1 + seed % 3)
+            eng.set_option("pod_rows", (variant + seed) % 3 - 1)  # direct / word runs / auto
             eng.set_option("emit_merged", int(variant != 5))
             eng.set_option("graphs", graphs)
             eng.set_option("graph_branches", branches)
@@ -363,3 +366,26 @@ def test_edge_shapes(gpu, seed):
     bare = [dict(p, Containers=[]) if i % 3 == 0 else p for i, p in enumerate(res["Pods"][:70])]
     assert_same(*run_both(pols, dict(res, Pods=bare), probes + [{"AllAvailable": True}], engine=eng),
                 f"seed {seed} pods without containers")
+
+
+@pytest.mark.parametrize("bad", [False, True])
+def test_direct_pod_rows_and_flat_emit(gpu, bad):
+    """Pod-peer rows computed per pod (pod_rows = 1) and through identity runs (0), and the flat
+    multi-row emit (emit_variant 9) vs one block per row (0): all equal the oracle, panics too."""
+    eng = Engine(0)
+    for seed in range(40):
+        pols, res, probes = random_problem(70_000 + seed, n_pods=30 + 7 * seed, bad=bad)
+        try:
+            want = Oracle(pols, res).probe(probes)
+        except OraclePanic as e:
+            want = Panicked(str(e))
+        eng.build_policies(pols).load_resources(res)
+        for pod_rows, variant in ((1, 9), (0, 0), (1, 0), (0, 9)):
+            eng.set_option("pod_rows", pod_rows)
+            eng.set_option("emit_variant", variant)
+            try:
+                eng.prepare(probes)
+                got = eng.run_host()
+            except CyclonusPanic as e:
+                got = Panicked(e.msg)
+            assert_same(want, got, f"seed {seed} pod_rows {pod_rows} emit {variant}")
