@@ -120,14 +120,20 @@ int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
  * [1] egress (synchronises the device). */
 int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
 
-/* Tuning knobs (no effect on results): "emit_variant" 0..6 selects the emit store pattern ("emit_chunk": rows per XCD chunk of variant 6);
+/* Tuning knobs (no effect on results): "emit_variant" selects the emit kernel: -1 (default) =
+ * auto (0 for plane rows of >= 16 KB, else 9), 0..5 one block per row with different store
+ * patterns, 6 rows dealt to the XCDs in chunks ("emit_chunk" rows), 7 / 8 one block per 2 / 4
+ * rows, 9 the flat multi-row sweep (~32 KB of rows per block, for short rows);
  * "class_variant_in" / "class_variant_eg" 0..3 the class-row kernel shape (bit 0: 4 job slots
  * per thread instead of 8; bit 1: block rows stride over the class representatives);
- * "emit_blocks" the persistent emit grid (0 = one block per row); "graph_branches" (default 1)
- * runs ingress and egress as two concurrent branches of the step graph; "graph_stagger"
- * (default 1) starts the egress class rows after the ingress ones (under the ingress emit);
+ * "emit_blocks" the persistent emit grid (0 = one block per row); "emit_merged" (default 1) writes
+ * both planes in one emit launch; "graph_branches" (default 1) runs ingress and egress as two
+ * concurrent branches of the step graph; "graph_stagger" (default 1, two-launch emit only) starts
+ * the egress class rows after the ingress ones;
  * "pod_words" -1 (default: auto) / 0 / 1 has the class rows read pod-peer words from materialised
  * peer rows (0) or expand them from per-identity outcomes through each word's identity runs (1);
+ * "pod_rows" -1 (default: auto = 1 when identities >= pods / 2) / 0 / 1 builds materialised
+ * pod-peer rows through identity outcomes and word runs (0) or per pod with one ballot per word (1);
  * "graphs" (default 1) replays the pipeline as one captured hipGraph when the inputs cannot
  * panic (then cyc_last_timings reports only the whole-pipeline time). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
