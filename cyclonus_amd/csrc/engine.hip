@@ -1168,6 +1168,40 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   }
 }
 
+// Variant 10 (auto for rows of >= 64 KB): one block of BS = 512 threads per row (XCD-mapped as
+// variant 0) with UNROLL chosen on the host so one pass of BS x UNROLL 16-byte chunks covers the
+// row (config #3: 100 KB rows, 512 x 13 x 16 B = 104 KB): every lane's loads are in flight before
+// its stores and no second, partly idle pass follows (profiles/r01_emit_wide_sweep.txt: 3-4 %
+// faster than 256 x 16 in two passes; 1024 x 7, 256 x 25, 512 x 7, plain or sc1 stores, and
+// fill-like address-linear 16 / 32 KB segments were all slower).  STORE 0 = non-temporal,
+// 1 = plain, 2 = sc1.
+template <int BS, int UNROLL, int STORE>
+__global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
+  const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
+  const uint32_t r = x * a.per_xcd + (b >> 3);
+  if (r >= min(n, (x + 1) * a.per_xcd)) return;
+  const uint32_t pl = r >= a.n_rows ? 1u : 0u;
+  const uint32_t p = a.order[pl][r - pl * a.n_rows];
+  const u64x2* si = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
+  u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
+  const uint32_t n2 = uint32_t(a.row_words / 2);
+  for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS * UNROLL) {
+    u64x2 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++)
+      if (x0 + u * BS < n2) v[u] = si[x0 + u * BS];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      const uint32_t i = x0 + u * BS;
+      if (i < n2) {
+        if (STORE == 0) __builtin_nontemporal_store(v[u], &di[i]);
+        else if (STORE == 1) di[i] = v[u];
+        else asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(&di[i]), "v"(v[u]) : "memory");
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- panic path (rare)
 struct ErrArgs {
   uint32_t P, K, W, n_cfg;
@@ -2055,9 +2089,11 @@ static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
     const uint32_t n = ea.n_rows * ea.planes, per = 8 * ea.chunk;
     g = (n + per - 1) / per * per;
   }
-  // emit_variant -1 (default) = auto: one block per row (variant 0) for rows of >= 16 KB, else
-  // the flat multi-row sweep (variant 9) over ~32 KB per block
-  const int variant = c->emit_variant >= 0 ? c->emit_variant : (ea.row_words * 8 >= 16384 ? 0 : 9);
+  // emit_variant -1 (default) = auto by plane-row length: >= 64 KB one 512-thread single-pass
+  // block per row (10), >= 16 KB one 256-thread block per row (0), else the flat multi-row
+  // sweep over ~32 KB per block (9)
+  const uint64_t row_bytes = ea.row_words * 8;
+  const int variant = c->emit_variant >= 0 ? c->emit_variant : (row_bytes >= 65536 ? 10 : row_bytes >= 16384 ? 0 : 9);
   if (vec && (variant == 7 || variant == 8)) {  // one block per row group of an XCD segment
     const uint32_t G = variant == 7 ? 2 : 4;
     g = (ea.per_xcd + G - 1) / G * 8;
@@ -2079,6 +2115,18 @@ static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
       case 7: k_emit_group<2, 8><<<g, 256, 0, st>>>(ea); break;
       case 8: k_emit_group<4, 8><<<g, 256, 0, st>>>(ea); break;
       case 9: k_emit_flat<8><<<g, 256, 0, st>>>(ea); break;
+      case 10: {
+        // smallest UNROLL whose single pass covers the row (16 when the row needs more passes)
+        const uint64_t need = (ea.row_words / 2 + 511) / 512;
+        const unsigned gw = ea.per_xcd * 8;
+        if (need <= 8) k_emit_wide<512, 8, 0><<<gw, 512, 0, st>>>(ea);
+        else if (need <= 10) k_emit_wide<512, 10, 0><<<gw, 512, 0, st>>>(ea);
+        else if (need <= 12) k_emit_wide<512, 12, 0><<<gw, 512, 0, st>>>(ea);
+        else if (need <= 13) k_emit_wide<512, 13, 0><<<gw, 512, 0, st>>>(ea);
+        else if (need <= 14) k_emit_wide<512, 14, 0><<<gw, 512, 0, st>>>(ea);
+        else k_emit_wide<512, 16, 0><<<gw, 512, 0, st>>>(ea);
+        break;
+      }
       default: CYC_EMIT(true, 16, true, true); break;
     }
 #undef CYC_EMIT

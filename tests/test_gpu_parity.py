@@ -231,7 +231,7 @@ def test_graph_and_eager_paths_agree(gpu):
                                                        (1, 0, 1024, 0, 1), (1, 1, 8, 0, 2), (0, 1, 0, 0, 3),
                                                        (0, 1, 16, 3, 1), (1, 1, 0, 5, 2), (1, 1, 0, 6, 3), (0, 0, 0, 6, 0),
                                                        (1, 1, 0, 7, 1), (0, 1, 0, 8, 2), (1, 0, 0, 8, 0), (1, 1, 0, 9, 1),
-                                                       (0, 1, 0, 9, 3), (1, 1, 0, -1, 0)):
+                                                       (0, 1, 0, 9, 3), (1, 1, 0, -1, 0), (1, 1, 0, 10, 2), (0, 1, 0, 10, 1)):
             eng.set_option("emit_chunk", 1 + seed % 3)
             eng.set_option("pod_rows", (variant + seed) % 3 - 1)  # direct / word runs / auto
             eng.set_option("emit_merged", int(variant != 5))
@@ -371,7 +371,8 @@ def test_edge_shapes(gpu, seed):
 @pytest.mark.parametrize("bad", [False, True])
 def test_direct_pod_rows_and_flat_emit(gpu, bad):
     """Pod-peer rows computed per pod (pod_rows = 1) and through identity runs (0), and the flat
-    multi-row emit (emit_variant 9) vs one block per row (0): all equal the oracle, panics too."""
+    multi-row emit (emit_variant 9), one 256-thread block per row (0) and the single-pass 512-thread
+    block per row (10): all equal the oracle, panics too."""
     eng = Engine(0)
     for seed in range(40):
         pols, res, probes = random_problem(70_000 + seed, n_pods=30 + 7 * seed, bad=bad)
@@ -380,7 +381,7 @@ def test_direct_pod_rows_and_flat_emit(gpu, bad):
         except OraclePanic as e:
             want = Panicked(str(e))
         eng.build_policies(pols).load_resources(res)
-        for pod_rows, variant in ((1, 9), (0, 0), (1, 0), (0, 9)):
+        for pod_rows, variant in ((1, 9), (0, 0), (1, 0), (0, 9), (1, 10)):
             eng.set_option("pod_rows", pod_rows)
             eng.set_option("emit_variant", variant)
             try:
