@@ -793,6 +793,21 @@ __global__ __launch_bounds__(256) void k_class_ident(RowArgs a) {
   }
 }
 
+// Port check of one peer's port matcher row `pok` for job slot k of pod word w: all 64 pods
+// (descriptor du >= 0), none (invalid slot), or per destination (egress word whose
+// destinations have mixed job descriptors, through DM; rare).
+template <bool EGRESS>
+__device__ __forceinline__ uint64_t port_mask(const RowArgs& a, const uint8_t* pok, int32_t du, uint32_t k, uint32_t w) {
+  if (du >= 0) return pok[du] ? ~0ull : 0ull;
+  if (!EGRESS || du == -2) return 0ull;
+  uint64_t okm = 0;
+  const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
+  for (uint32_t d = 0; d < a.D; d++)
+    if (pok[d]) okm |= dm[uint64_t(d) * a.W];
+  return okm;
+}
+constexpr uint32_t PEER_BATCH = 4;
+
 template <bool EGRESS, bool ERR, int KC>
 __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uint32_t kc, uint32_t w) {
   const uint32_t k0 = kc * KC;
@@ -825,6 +840,45 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
   if (n == 0) {
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) allow[kk] = ~0ull;  // no target applies: allowed (policy.go:158-160)
+  } else if (!ERR) {
+    // No panic is possible: a cell's verdict is the OR over every peer of every matching target
+    // (target.go:29-36 short-circuits only to save work), so the walk loads the PM words of
+    // PEER_BATCH peers at once instead of one dependent load per peer, and drops the early exit.
+    const uint32_t* lst = a.list + a.list_off[i];
+    bool all = false;
+    for (uint32_t tj = 0; tj < n && !all; tj++) {
+      const DTarget tg = a.tgt[lst[tj]];
+      const uint32_t pend = tg.poff + tg.pcnt;
+      for (uint32_t j0 = tg.poff; j0 < pend; j0 += PEER_BATCH) {
+        uint64_t pm[PEER_BATCH];
+        uint32_t port[PEER_BATCH];
+#pragma unroll
+        for (uint32_t u = 0; u < PEER_BATCH; u++) {
+          const uint32_t j = j0 + u;
+          pm[u] = 0;
+          port[u] = 0;
+          if (j < pend) {
+            const DPeer pr = a.peers[j];
+            port[u] = pr.port;
+            if (pr.kind == 0) all = true;  // AllPeersMatcher: every valid cell allowed
+            else if (pr.kind == 1) pm[u] = ~0ull;  // PortsForAllPeers
+            else if (pr.kind == 2 || (w >= a.ip_rng[2 * j] && w <= ~a.ip_rng[2 * j + 1]))
+              pm[u] = a.PM[uint64_t(j) * a.W + w];
+          }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PEER_BATCH; u++) {
+          if (!pm[u]) continue;
+          const uint8_t* pok = a.portok + uint64_t(port[u]) * a.D;
+#pragma unroll
+          for (int kk = 0; kk < KC; kk++) allow[kk] |= pm[u] & port_mask<EGRESS>(a, pok, du[kk], k0 + kk, w);
+        }
+      }
+    }
+    if (all) {
+#pragma unroll
+      for (int kk = 0; kk < KC; kk++) allow[kk] = ~0ull;
+    }
   } else if (n != 0xFFFFFFFFu) {
     const uint32_t* lst = a.list + a.list_off[i];
     for (uint32_t tj = 0; tj < n; tj++) {
@@ -959,26 +1013,30 @@ __global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) {
       }
     }
   }
-  // IP peers (ippeermatcher.go:43-50): per pod word through the PM rows
+  // IP peers (ippeermatcher.go:43-50): per pod word through the PM rows, PEER_BATCH peers' words
+  // loaded at once (no panic in IDO builds: the OR is order-free; the undecided check only ends
+  // the walk early, once per batch)
   const uint32_t m = a.cnt[i] ? a.ip_cnt[i] : 0u;
   const uint4* il = a.ip_list + a.ip_off[i];
-  for (uint32_t x = 0; x < m; x++) {
-    const uint4 jp = il[x];
-    if (w < jp.z || w > jp.w) continue;  // outside the peer's nonzero words
-    const uint64_t pm = a.PM[uint64_t(jp.x) * a.W + w];
-    const uint8_t* pok = a.portok + uint64_t(jp.y) * a.D;
+  for (uint32_t x0 = 0; x0 < m; x0 += PEER_BATCH) {
+    uint64_t pm[PEER_BATCH];
+    uint32_t port[PEER_BATCH];
+#pragma unroll
+    for (uint32_t u = 0; u < PEER_BATCH; u++) {
+      pm[u] = 0;
+      port[u] = 0;
+      if (x0 + u < m) {
+        const uint4 jp = il[x0 + u];
+        port[u] = jp.y;
+        if (w >= jp.z && w <= jp.w) pm[u] = a.PM[uint64_t(jp.x) * a.W + w];  // inside the peer's nonzero words
+      }
+    }
     uint64_t undecided = 0;
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
-      uint64_t okm = 0;
-      if (du[kk] >= 0) {
-        okm = pok[du[kk]] ? ~0ull : 0ull;
-      } else if (EGRESS && du[kk] == -1) {
-        const uint64_t* dm = a.DM + uint64_t(k0 + kk) * a.D * a.W + w;
-        for (uint32_t d = 0; d < a.D; d++)
-          if (pok[d]) okm |= dm[uint64_t(d) * a.W];
-      }
-      allow[kk] |= pm & okm;
+#pragma unroll
+      for (uint32_t u = 0; u < PEER_BATCH; u++)
+        if (pm[u]) allow[kk] |= pm[u] & port_mask<EGRESS>(a, a.portok + uint64_t(port[u]) * a.D, du[kk], k0 + kk, w);
       undecided |= valid[kk] & ~allow[kk];
     }
     if (!undecided) break;
