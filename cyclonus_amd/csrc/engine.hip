@@ -382,22 +382,12 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
 // rng[2 * peer + 1] (~last word), both atomicMin'd from 0xFFFFFFFF: CIDRs are address ranges and
 // pods of a namespace have neighbouring addresses, so a peer's row is mostly zero words the
 // class rows can skip without loading them.
-__global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
-                                                      const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
-                                                      const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint32_t chunks = (W + 63) / 64;
-  const uint32_t r = gw / chunks;
-  if (r >= Ri) return;
-  const DIPTest t = tests[r];
-  const uint32_t w = (gw % chunks) * 64 + lane;
-  const bool valid = w < W;
+__device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
+                                            const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
+                                            uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng) {
   bool uniform = true;
   uint64_t res = 0;
   if (valid) {
-    const DWordIP wd = words[w];
     const bool v4 = t.cidr.fam == 4;
     const uint64_t fm = v4 ? wd.m4 : wd.m6;  // pods of the network's family; the others never match
     if (fm) {
@@ -419,14 +409,14 @@ __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, u
   }
   if (valid && uniform) PM[uint64_t(t.peer) * W + w] = res;
   const uint64_t nz = __ballot(valid && uniform && res != 0);
-  const uint32_t w0 = (gw % chunks) * 64;
+  const uint32_t w0 = chunk * 64;
   uint32_t lo = nz ? w0 + __ffsll((unsigned long long)nz) - 1 : 0xFFFFFFFFu;
   uint32_t hi = nz ? w0 + 63 - __clzll((long long)nz) : 0u;
   uint64_t mixed = __ballot(valid && !uniform);
   while (mixed) {
     const uint32_t wl = __ffsll((unsigned long long)mixed) - 1;
     mixed &= mixed - 1;
-    const uint32_t ww = (gw % chunks) * 64 + wl;
+    const uint32_t ww = chunk * 64 + wl;
     const uint32_t q = ww * 64 + lane;
     uint32_t o = 0;
     if (q < P) {
@@ -451,6 +441,24 @@ __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, u
     atomicMin(&rng[2 * t.peer], lo);
     atomicMin(&rng[2 * t.peer + 1], ~hi);
   }
+}
+
+// A wave handles IP_GROUP peers over its 64 words: the words' [min, max] records are loaded once.
+constexpr uint32_t IP_GROUP = 8;
+__global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
+                                                      const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
+                                                      const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
+                                                      uint32_t* __restrict__ rng) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t chunks = (W + 63) / 64;
+  const uint32_t r0 = (gw / chunks) * IP_GROUP;
+  if (r0 >= Ri) return;
+  const uint32_t w = (gw % chunks) * 64 + lane;
+  const bool valid = w < W;
+  DWordIP wd{};
+  if (valid) wd = words[w];
+  for (uint32_t r = r0; r < min(Ri, r0 + IP_GROUP); r++) ip_row_word(tests[r], ip_ex, pod_ip, wd, valid, w, gw % chunks, P, W, lane, PM, rng);
 }
 
 // PortMatcher.Allows(ResolvedPort, ResolvedPortName, Protocol) — portmatcher.go:10-92, 190-199.
@@ -2012,7 +2020,7 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
       k_ip_rows<true><<<g, 256, 0, st>>>(Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->PM.as<uint64_t>(),
                                          c->ER.as<uint64_t>(), bat);
     } else {
-      k_ip_rows_fast<<<unsigned((uint64_t((W + 63) / 64) * Ri + 3) / 4), 256, 0, st>>>(
+      k_ip_rows_fast<<<unsigned((uint64_t((W + 63) / 64) * ((Ri + IP_GROUP - 1) / IP_GROUP) + 3) / 4), 256, 0, st>>>(
           Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>(),
           c->ip_rng.as<uint32_t>());
     }
