@@ -1512,6 +1512,7 @@ struct cyc_ctx {
   DevBuf ls_off, ls_key, ls_val, sel_off, reqs, req_vals, pod_ns, pod_ls, pod_nsls, pod_ip, cidrs, ipbs, ipb_ex, pms,
       pents, peers, descs, slot_desc, slot_status, slot_cfg, slot_idx;
   DevBuf selres, PM, ER, portok, VALID, DESCW, DM, first_err, order[2];
+  DevBuf status_sink;  // status plane target of graph runs given no status pointer (see capture_pipeline)
   // peer-row stage: pod peers in identity space + per-word identity runs; IP peers per pod
   DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
   bool dense_sel = false;  // k_selectors_dense (LVT fits)
@@ -1540,6 +1541,12 @@ struct cyc_ctx {
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
   hipEvent_t fork_ev = nullptr, join_ev = nullptr, sel_ev = nullptr, ports_ev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
+  hipGraph_t graph = nullptr;  // kept alive with its exec
+  // Execs replaced by a re-capture (new output pointers, row range or tuning knob) are retired, not
+  // destroyed, until the context is destroyed: re-capturing while destroying the previous execs
+  // crashed inside hipGraphLaunch on ROCm 7 (scripts/debug_variants.py; a launch indexed a stream
+  // list past its end).
+  std::vector<std::pair<hipGraphExec_t, hipGraph_t>> retired;
   const void* graph_key[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   bool timed_graph = false;
   DirDev dir[2];
@@ -1765,6 +1772,7 @@ static void prepare_device(cyc_ctx* c) {
   c->DESCW.alloc(std::max<uint64_t>(K * W * 4, 16));
   c->DM.alloc(std::max<uint64_t>(K * D * W * 8, 16));
   c->first_err.alloc(16);
+  c->status_sink.alloc(std::max<uint64_t>(uint64_t(pb.P) * K, 16));
   for (int d = 0; d < 2; d++) {
     Identities& I = c->ids[d];
     DirDev& dd = c->dir[d];
@@ -2267,13 +2275,25 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
     HIPCHK(hipEventRecord(c->join_ev, st2));
     HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
   }
-  if (d_status && uint64_t(pb.P) * pb.K)
-    HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
+  // The step always ends with the status-plane copy (into a sink buffer when the caller passed no
+  // status pointer), so every captured graph has the same shape: one node after the join.
+  const uint64_t nst = uint64_t(pb.P) * pb.K;
+  uint8_t* dst = d_status && nst ? d_status : c->status_sink.as<uint8_t>();  // sink: >= 16 B (prepare_device)
+  HIPCHK(hipMemcpyAsync(dst, c->slot_status.p, std::max<uint64_t>(nst, 1), hipMemcpyDeviceToDevice, st));
 }
 
 static void drop_graph(cyc_ctx* c) {
-  if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+  if (c->graph_exec) c->retired.emplace_back(c->graph_exec, c->graph);
   c->graph_exec = nullptr;
+  c->graph = nullptr;
+  if (c->retired.size() >= 64) {  // bound the retired list: drained with the device idle
+    (void)hipDeviceSynchronize();
+    for (auto& r : c->retired) {
+      (void)hipGraphExecDestroy(r.first);
+      if (r.second) (void)hipGraphDestroy(r.second);
+    }
+    c->retired.clear();
+  }
 }
 
 static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
@@ -2303,9 +2323,8 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
       HIPCHK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
       capture_pipeline(c, c->cap_stream, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status, lo, hi);
       HIPCHK(hipStreamEndCapture(c->cap_stream, &g));
-      hipError_t ie = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(g);
-      HIPCHK(ie);
+      c->graph = g;  // destroyed with the exec (drop_graph)
+      HIPCHK(hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
       memcpy(c->graph_key, key, sizeof(key));
     }
     HIPCHK(hipEventRecord(c->ev[0], st));
@@ -2484,6 +2503,12 @@ void cyc_ctx_destroy(cyc_ctx* c) {
   if (c->stream) {
     (void)hipSetDevice(c->device);
     drop_graph(c);
+    (void)hipDeviceSynchronize();
+    for (auto& r : c->retired) {
+      (void)hipGraphExecDestroy(r.first);
+      if (r.second) (void)hipGraphDestroy(r.second);
+    }
+    c->retired.clear();
     destroy_events(c);
     if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
     if (c->cap_stream2) (void)hipStreamDestroy(c->cap_stream2);

@@ -390,3 +390,26 @@ def test_direct_pod_rows_and_flat_emit(gpu, bad):
             except CyclonusPanic as e:
                 got = Panicked(e.msg)
             assert_same(want, got, f"seed {seed} pod_rows {pod_rows} emit {variant}")
+
+
+def test_graph_joins_without_status_or_rows(gpu):
+    """Captured graphs for steps without a status plane (null pointer) or without rows (an empty
+    row range), with one or two emit launches, replayed and re-captured: results unchanged."""
+    import torch
+
+    pols, res, probes = random_problem(90_001, n_pods=120)
+    want = Oracle(pols, res).probe(probes)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    sh = eng.prepare(probes)
+    P, K, W = sh["pods"], sh["slots"], sh["words"]
+    st = torch.cuda.current_stream().cuda_stream
+    for merged in (1, 0):
+        eng.set_option("emit_merged", merged)
+        for _ in range(3):  # replays of the same graph
+            d_in = torch.zeros((P, K, W), dtype=torch.int64, device="cuda")
+            d_eg = torch.zeros((P, K, W), dtype=torch.int64, device="cuda")
+            eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), 0, st)
+            eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), 0, st, 7, 7)
+            torch.cuda.synchronize()
+            assert np.array_equal(d_in.cpu().numpy().view(np.uint64), want[1]), f"merged {merged}"
+            assert np.array_equal(d_eg.cpu().numpy().view(np.uint64), want[2]), f"merged {merged}"
