@@ -1073,7 +1073,18 @@ struct EmitArgs {
   uint64_t row_words;         // K * W
   uint32_t blocks_per_xcd;    // persistent launch: blocks of one XCD stride over its row segment
   uint32_t chunk;             // CHUNK variant: rows per XCD chunk
+  const uint8_t* st_src;      // job status plane [P][K] (the run's third output), copied by the
+  uint8_t* st_dst;            // emit's blocks in slices: no separate copy node ends the step
+  uint64_t st_bytes;
 };
+
+// Block b's slice of the status plane copy (every emit kernel calls this first).
+__device__ __forceinline__ void emit_status(const EmitArgs& a) {
+  if (!a.st_bytes) return;
+  const uint64_t per = (a.st_bytes + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
+  const uint64_t hi = lo + per < a.st_bytes ? lo + per : a.st_bytes;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.st_dst[i] = a.st_src[i];
+}
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
@@ -1121,6 +1132,7 @@ __device__ __forceinline__ void emit_row(const EmitArgs& a, uint32_t r) {
 // a whole plane apart, while consecutive (same-class) rows still share one XCD's L2.
 template <bool VEC, int UNROLL, bool NT, bool XCD = true, bool CHUNK = false>
 __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
+  emit_status(a);
   const uint32_t b = blockIdx.x, n = a.n_rows * a.planes;
   uint32_t r, r_end, r_step;
   if (CHUNK) {
@@ -1148,6 +1160,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
 // their own).  G x fewer loads per store than one block per row.
 template <int G, int UNROLL>
 __global__ __launch_bounds__(256) void k_emit_group(EmitArgs a) {
+  emit_status(a);
   const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
   const uint32_t r0 = x * a.per_xcd + (b >> 3) * G, r_end = min(n, (x + 1) * a.per_xcd);
   if (r0 >= r_end) return;
@@ -1202,6 +1215,7 @@ __global__ __launch_bounds__(256) void k_emit_group(EmitArgs a) {
 constexpr uint32_t EMIT_FLAT_MAX_ROWS = 256;
 template <int UNROLL>
 __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
+  emit_status(a);
   __shared__ const u64x2* s_src[EMIT_FLAT_MAX_ROWS];
   __shared__ u64x2* s_dst[EMIT_FLAT_MAX_ROWS];
   const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
@@ -1243,6 +1257,7 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
 // 1 = plain, 2 = sc1.
 template <int BS, int UNROLL, int STORE>
 __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
+  emit_status(a);
   const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
   const uint32_t r = x * a.per_xcd + (b >> 3);
   if (r >= min(n, (x + 1) * a.per_xcd)) return;
@@ -2134,11 +2149,17 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 }
 
 // 7. emit of direction d's plane (d = 2: both planes in one launch, out = ingress, out2 = egress)
-static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t lo, int64_t hi, uint64_t* out2 = nullptr) {
+// d_status (may be null): the status plane, copied by the emit's blocks.  Returns false if no
+// emit was launched (no rows in the range; the caller then copies the status plane itself).
+static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t lo, int64_t hi, uint64_t* out2 = nullptr,
+                     uint8_t* d_status = nullptr) {
   Problem& pb = c->pb;
   const uint32_t K = pb.K, W = pb.W;
-  if (hi <= lo || !K || !W) return;
+  if (hi <= lo || !K || !W) return false;
   EmitArgs ea{};
+  ea.st_src = c->slot_status.as<uint8_t>();
+  ea.st_dst = d_status;
+  ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
   ea.n_rows = uint32_t(hi - lo);
   ea.planes = d == 2 ? 2 : 1;
   ea.row_lo = uint32_t(lo);
@@ -2204,6 +2225,7 @@ static void enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
       default: CYC_EMIT(true, 16, true, true); break;
     }
 #undef CYC_EMIT
+  return true;
 }
 
 // Eager launch, in phase order with the timing events: [0] start, [1] after the front (peer
@@ -2218,14 +2240,15 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
   HIPCHK(hipEventRecord(c->ev[1], st));
   for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
   HIPCHK(hipEventRecord(c->ev[2], st));
+  bool status_done;
   if (c->emit_merged) {
-    enq_emit(c, 2, st, d_in, lo, hi, d_eg);
+    status_done = enq_emit(c, 2, st, d_in, lo, hi, d_eg, d_status);
   } else {
-    enq_emit(c, 0, st, d_in, lo, hi);
+    status_done = enq_emit(c, 0, st, d_in, lo, hi, nullptr, d_status);
     enq_emit(c, 1, st, d_eg, lo, hi);
   }
   HIPCHK(hipEventRecord(c->ev[3], st));
-  if (d_status && uint64_t(pb.P) * pb.K)
+  if (!status_done && d_status && uint64_t(pb.P) * pb.K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
 }
 
@@ -2255,7 +2278,8 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
     }
     HIPCHK(hipEventRecord(c->join_ev, st2));
     HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
-    enq_emit(c, 2, st, d_in, lo, hi, d_eg);
+    // the emit also writes the status plane; the copy node below only ends steps without rows
+    if (enq_emit(c, 2, st, d_in, lo, hi, d_eg, d_status)) return;
   } else {
     // one branch per direction, each ending with its own plane's emit
     enq_common(c, st);
