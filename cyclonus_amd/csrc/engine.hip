@@ -614,6 +614,47 @@ __global__ void k_member(MemberArgs a) {
   }
 }
 
+// The same membership with one wave per identity (lanes over its namespace's targets, one ballot
+// per 64 targets): a run has few identities per namespace but several targets each, so a thread
+// per identity leaves the chip nearly idle behind a chain of dependent loads.  Same list order
+// (ascending target id = primary-key order), same hash, same representative election.
+__global__ __launch_bounds__(256) void k_member_wave(MemberArgs a) {
+  const uint32_t lane = threadIdx.x & 63, ii = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ii >= a.n_act) return;
+  const uint32_t i = a.act[ii];
+  const uint32_t ns = a.id_ns[i], ls = a.id_ls[i];
+  const uint32_t lo = a.tns_lo[ns], hi = a.tns_hi[ns], off = a.list_off[i];
+  uint32_t n = 0;
+  bool e = false;
+  uint64_t h = 0x5bd1e9955bd1e995ull;
+  for (uint32_t t0 = lo; t0 < hi; t0 += 64) {
+    const uint32_t t = t0 + lane;
+    const uint8_t r = t < hi ? a.selres[uint64_t(a.tgt[t].sel) * a.L + ls] : 0;
+    e |= __ballot(r == 2) != 0;
+    const uint64_t m = __ballot(r == 1);
+    if (r == 1) a.list[off + n + __popcll(m & ((1ull << lane) - 1))] = t;
+    for (uint64_t mm = m; mm; mm &= mm - 1) h = mix64(h ^ (uint64_t(t0 + __ffsll((unsigned long long)mm) - 1) + 1));
+    n += __popcll(m);
+  }
+  if (a.id_desc) {
+    for (uint32_t k = 0; k < a.K; k++) {
+      uint64_t st = a.id_status[uint64_t(i) * a.K + k];
+      int32_t d = st == CYC_JOB_VALID ? a.id_desc[uint64_t(i) * a.K + k] : -1;
+      h = mix64(h ^ ((st << 40) | uint32_t(d + 1)) ^ (uint64_t(k) << 48));
+    }
+  }
+  h &= 0x7FFFFFFFFFFFFFFFull;  // never the empty key (~0)
+  if (lane == 0) {
+    a.cnt[i] = n;
+    a.hash[i] = h;
+    a.err[i] = e;
+    if (!e) {
+      const uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
+      atomicMin(&a.ht_rep[s], i);
+    }
+  }
+}
+
 // Also compacts the class representatives: each block appends its representatives, in act[]
 // order (ascending identity), at a base taken with one atomicAdd — consecutive identities (one
 // namespace) stay adjacent, so consecutive class-row blocks share their targets' peer rows in
@@ -1544,6 +1585,8 @@ struct cyc_ctx {
   bool use_graphs = true;  // cyc_set_option "graphs"
   int pod_rows = -1;   // cyc_set_option "pod_rows": pod-peer PM rows per pod directly (1), through
                        // identity outcomes and word runs (0), or -1 = direct when identities >= pods / 2
+  int member_wave = -1;  // cyc_set_option "member_wave": membership with a wave (1) or a thread (0) per
+                         // identity, -1 = auto by identity count
   int pod_words = -1;  // cyc_set_option "pod_words": pod-peer words in the class rows from IDO (1), from
                        // materialised PM rows (0), or IDO when every word has <= IDO_MAX_RUNS runs (-1)
   int graph_stagger = 1;  // cyc_set_option "graph_stagger": 1 = egress class rows wait for the ingress
@@ -2062,7 +2105,11 @@ static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
   if (clear) enq_member_clear(c, d, st);
   MemberArgs ma = member_args(c, d);
   if (!c->n_act[d]) return;
-  k_member<<<grid1(c->n_act[d], 128), 128, 0, st>>>(ma);
+  // auto (-1): a wave per identity while identities are few (<= 4096: config #3, 2000 per run; with
+  // tens of thousands, e.g. configs #2 / #4, the per-wave hash-table atomics of identities sharing
+  // a class cost more than the thread-per-identity latency; profiles/r01_member_wave_ab.txt)
+  if (c->member_wave > 0 || (c->member_wave < 0 && c->n_act[d] <= 4096)) k_member_wave<<<unsigned((uint64_t(c->n_act[d]) + 3) / 4), 256, 0, st>>>(ma);
+  else k_member<<<grid1(c->n_act[d], 128), 128, 0, st>>>(ma);
   k_classify<<<grid1(c->n_act[d], 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
 }
 
@@ -2734,6 +2781,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "member_wave") {
+    if (value < -1 || value > 1) return fail(c, CYC_ERR_ARG, "member_wave must be -1, 0 or 1");
+    c->member_wave = int(value);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "emit_merged") {
     c->emit_merged = int(value != 0);
     drop_graph(c);
@@ -2763,6 +2816,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "graph_branches") *value = c->graph_branches;
   else if (n == "graph_stagger") *value = c->graph_stagger;
   else if (n == "emit_merged") *value = c->emit_merged;
+  else if (n == "member_wave") *value = c->member_wave;
   else if (n == "pod_rows") *value = c->pod_rows;
   else if (n == "graphs") *value = c->use_graphs;
   else if (n == "pod_words") {

@@ -372,7 +372,7 @@ def test_edge_shapes(gpu, seed):
 def test_direct_pod_rows_and_flat_emit(gpu, bad):
     """Pod-peer rows computed per pod (pod_rows = 1) and through identity runs (0), and the flat
     multi-row emit (emit_variant 9), one 256-thread block per row (0) and the single-pass 512-thread
-    block per row (10): all equal the oracle, panics too."""
+    block per row (10), membership by wave or by thread: all equal the oracle, panics too."""
     eng = Engine(0)
     for seed in range(40):
         pols, res, probes = random_problem(70_000 + seed, n_pods=30 + 7 * seed, bad=bad)
@@ -381,9 +381,10 @@ def test_direct_pod_rows_and_flat_emit(gpu, bad):
         except OraclePanic as e:
             want = Panicked(str(e))
         eng.build_policies(pols).load_resources(res)
-        for pod_rows, variant in ((1, 9), (0, 0), (1, 0), (0, 9), (1, 10)):
+        for pod_rows, variant, mw in ((1, 9, 1), (0, 0, 0), (1, 0, 1), (0, 9, 0), (1, 10, 1)):
             eng.set_option("pod_rows", pod_rows)
             eng.set_option("emit_variant", variant)
+            eng.set_option("member_wave", mw)  # membership: a wave (1) or a thread (0) per identity
             try:
                 eng.prepare(probes)
                 got = eng.run_host()
