@@ -112,8 +112,9 @@ int cyc_probe_run_host(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_
                        int64_t row_hi);
 
 /* Average device time (ms) of the last run's kernels, measured with HIP events on the launch
- * stream: [0] whole pipeline, [1] both emit launches (the HBM-roofline kernel, one launch per
- * plane), [2] class rows of both directions. */
+ * stream: [0] whole pipeline, [1] the emit launch(es) (the HBM-roofline kernel; one launch writes
+ * both planes unless "emit_merged" is 0), [2] class rows of both directions.  Graph runs report
+ * only [0] ([1], [2] = -1). */
 int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 
 /* Diagnostic: number of distinct classes (class rows computed) of the last run, [0] ingress,
@@ -134,6 +135,8 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  * peer rows (0) or expand them from per-identity outcomes through each word's identity runs (1);
  * "pod_rows" -1 (default: auto = 1 when identities >= pods / 2) / 0 / 1 builds materialised
  * pod-peer rows through identity outcomes and word runs (0) or per pod with one ballot per word (1);
+ * "member_wave" -1 (default: auto = 1 for <= 4096 identities) / 0 / 1 computes target membership
+ * with a thread (0) or a wave (1) per pod identity;
  * "graphs" (default 1) replays the pipeline as one captured hipGraph when the inputs cannot
  * panic (then cyc_last_timings reports only the whole-pipeline time). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
