@@ -101,6 +101,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-assemble", action="store_true", help="skip the N>1 all-gather timing")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="cyc_set_option tuning knob (diagnostics; results never change)")
     args = ap.parse_args()
 
     import numpy as np
@@ -131,6 +133,9 @@ def main():
 
     data = load_workload(args.config)
     eng = Engine(device)
+    for o in args.opt:
+        k, v = o.split("=")
+        eng.set_option(k, int(v))
     eng.build_policies(json.dumps(data["policies"]))
     eng.load_resources(json.dumps(data["resources"]))
     shape = eng.prepare(data["probes"])

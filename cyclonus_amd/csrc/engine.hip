@@ -568,6 +568,18 @@ __device__ __forceinline__ uint32_t ht_find(const unsigned long long* keys, uint
   return 0xFFFFFFFFu;
 }
 
+// Elect identity i as a candidate representative of key h.  A plain read first: the key is
+// usually present already with a smaller identity (keys never change once set, reps only
+// decrease, so a stale read can only send us to the atomics, never skip them wrongly); only
+// otherwise the CAS insert + atomicMin (identities sharing a class then cost one read each
+// instead of a serialised atomic on one address).
+__device__ __forceinline__ void ht_elect(const MemberArgs& a, uint64_t h, uint32_t i) {
+  const uint32_t s0 = ht_find(a.ht_key, a.ht_cap, h);
+  if (s0 != 0xFFFFFFFFu && a.ht_rep[s0] <= i) return;
+  const uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
+  atomicMin(&a.ht_rep[s], i);
+}
+
 __global__ void k_member(MemberArgs a) {
   uint32_t ii = blockIdx.x * blockDim.x + threadIdx.x;
   if (ii >= a.n_act) return;
@@ -608,10 +620,7 @@ __global__ void k_member(MemberArgs a) {
     const uint64_t hj = __shfl(h, int(j));
     if (j < lane && ((live >> j) & 1) && hj == h) leader = false;
   }
-  if (leader) {
-    uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
-    atomicMin(&a.ht_rep[s], i);
-  }
+  if (leader) ht_elect(a, h, i);
 }
 
 // The same membership with one wave per identity (lanes over its namespace's targets, one ballot
@@ -648,10 +657,7 @@ __global__ __launch_bounds__(256) void k_member_wave(MemberArgs a) {
     a.cnt[i] = n;
     a.hash[i] = h;
     a.err[i] = e;
-    if (!e) {
-      const uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
-      atomicMin(&a.ht_rep[s], i);
-    }
+    if (!e) ht_elect(a, h, i);
   }
 }
 
@@ -1577,6 +1583,7 @@ struct cyc_ctx {
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
   DevBuf act[2], sel_list;
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
+  double act_targets[2] = {0, 0};  // mean namespace targets per active identity (range plan)
   int emit_variant = -1;  // tuning knob (cyc_set_option "emit_variant"; -1 = auto by row length)
   int64_t emit_chunk = 64;  // cyc_set_option "emit_chunk": rows per XCD chunk (emit_variant 6)
   int64_t emit_blocks = 0;  // cyc_set_option "emit_blocks": persistent emit grid (0 = a block per row)
@@ -1939,6 +1946,9 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
       if (ns_needed[t.ns])
         for (uint32_t j = t.poff; j < t.poff + t.pcnt; j++) peer_needed[j] = 1;
     c->n_act[d] = uint32_t(act.size());
+    uint64_t tsum = 0;  // namespace targets each active identity's membership walk visits
+    for (uint32_t i : act) tsum += pb.tns_hi[d][I.ns[i]] - pb.tns_lo[d][I.ns[i]];
+    c->act_targets[d] = act.empty() ? 0.0 : double(tsum) / double(act.size());
     upload(c->act[d], act);
   }
   // selectors the range can reach: its targets' pod selectors and their peers' selectors
@@ -2105,10 +2115,10 @@ static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
   if (clear) enq_member_clear(c, d, st);
   MemberArgs ma = member_args(c, d);
   if (!c->n_act[d]) return;
-  // auto (-1): a wave per identity while identities are few (<= 4096: config #3, 2000 per run; with
-  // tens of thousands, e.g. configs #2 / #4, the per-wave hash-table atomics of identities sharing
-  // a class cost more than the thread-per-identity latency; profiles/r01_member_wave_ab.txt)
-  if (c->member_wave > 0 || (c->member_wave < 0 && c->n_act[d] <= 4096)) k_member_wave<<<unsigned((uint64_t(c->n_act[d]) + 3) / 4), 256, 0, st>>>(ma);
+  // auto (-1): a wave per identity while identities are few (<= 4096) and each walks several
+  // targets (>= 4 on average): config #3 (2000 identities, ~6 targets each) gains, configs #2
+  // (10k identities), #4 (38k) and #5 (~0.3 targets each) lose (profiles/r01_member_wave_ab.txt)
+  if (c->member_wave > 0 || (c->member_wave < 0 && c->n_act[d] <= 4096 && c->act_targets[d] >= 4.0)) k_member_wave<<<unsigned((uint64_t(c->n_act[d]) + 3) / 4), 256, 0, st>>>(ma);
   else k_member<<<grid1(c->n_act[d], 128), 128, 0, st>>>(ma);
   k_classify<<<grid1(c->n_act[d], 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
 }
