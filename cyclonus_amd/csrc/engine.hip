@@ -540,7 +540,7 @@ struct MemberArgs {
   const uint32_t* act;        // identities used by the rows of this run (range plan)
   uint32_t n_act;
   uint32_t* reps;             // class representatives, act[] order within each block (k_classify)
-  uint32_t* rep_cnt;          // starts at ~0 (hash-table memset): ends at count - 1
+  uint32_t* rep_cnt;          // set to ~0 by k_member: ends at count - 1
 };
 
 __device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* keys, uint32_t cap, uint64_t h) {
@@ -581,6 +581,7 @@ __device__ __forceinline__ void ht_elect(const MemberArgs& a, uint64_t h, uint32
 }
 
 __global__ void k_member(MemberArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
   uint32_t ii = blockIdx.x * blockDim.x + threadIdx.x;
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
@@ -628,6 +629,7 @@ __global__ void k_member(MemberArgs a) {
 // per identity leaves the chip nearly idle behind a chain of dependent loads.  Same list order
 // (ascending target id = primary-key order), same hash, same representative election.
 __global__ __launch_bounds__(256) void k_member_wave(MemberArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
   const uint32_t lane = threadIdx.x & 63, ii = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
@@ -739,7 +741,18 @@ struct RowArgs {
   uint4* ip_list;            // (peer, port matcher, first, last nonzero PM word)
   const uint32_t* ip_rng;    // [R][2] first word, ~last word of each IP peer's nonzero PM words (no-panic runs)
   uint32_t E, EW, NB;
+  // the direction's hash table (keys + reps), emptied for the NEXT run by the first class-row
+  // kernel in block slices once k_classify is done with it: no memset node precedes k_member
+  uint32_t* ht_clear;
+  uint64_t ht_clear_words;
 };
+
+__device__ __forceinline__ void ht_clear_slice(const RowArgs& a) {
+  if (!a.ht_clear_words) return;
+  const uint64_t per = (a.ht_clear_words + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
+  const uint64_t hi = lo + per < a.ht_clear_words ? lo + per : a.ht_clear_words;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.ht_clear[i] = 0xFFFFFFFFu;
+}
 
 // Most 64-pod words hold 1-2 identity runs (pods of a deployment are contiguous); IDO builds are
 // used only when no word holds more than IDO_MAX_RUNS runs (host-checked, plan_peers).
@@ -786,6 +799,7 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
 // (representative, NB index), lanes over 64-identity words.
 template <bool EGRESS, int G>
 __global__ __launch_bounds__(256) void k_class_ident(RowArgs a) {
+  ht_clear_slice(a);
   // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
   const uint32_t wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t nbc = (a.NB + G - 1) / G;
@@ -999,6 +1013,7 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
 // needs to stay at 3 waves/SIMD.
 template <bool EGRESS, bool ERR, int KC, bool LOOP>
 __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
+  ht_clear_slice(a);
   const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
   const uint32_t kc = (blockIdx.x / chunks) % nkc;
   const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
@@ -1857,6 +1872,7 @@ static void prepare_device(cyc_ctx* c) {
     dd.hash.alloc(std::max<uint64_t>(dd.n * 8ull, 16));
     dd.err.alloc(std::max<uint64_t>(dd.n, 16));
     dd.ht_key.alloc(uint64_t(dd.ht_cap) * 12 + 16);  // [cap] u64 keys (empty = ~0), [cap] u32 reps, counter
+    HIPCHK(hipMemset(dd.ht_key.p, 0xFF, dd.ht_key.bytes));  // empty; afterwards every run's class rows empty it
     dd.reps.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.class_of.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.A.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
@@ -2109,10 +2125,16 @@ static void enq_member_clear(cyc_ctx* c, int d, hipStream_t st) {
   if (dd.n) HIPCHK(hipMemsetAsync(dd.ht_key.p, 0xFF, dd.ht_key.bytes, st));  // keys and reps: one buffer
 }
 
+// The class rows of a run empty the hash table for the next one (ht_clear_slice); only runs whose
+// class rows do not launch (no slots or no pods) need the memset (prepare_device empties it once).
+static bool class_rows_clear_ht(const cyc_ctx* c, int d) {
+  return c->dir[d].n && c->pb.K && c->pb.W && c->n_act[d];
+}
+
 static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
   DirDev& dd = c->dir[d];
   if (!dd.n) return;
-  if (clear) enq_member_clear(c, d, st);
+  if (clear && !class_rows_clear_ht(c, d)) enq_member_clear(c, d, st);
   MemberArgs ma = member_args(c, d);
   if (!c->n_act[d]) return;
   // auto (-1): a wave per identity while identities are few (<= 4096) and each walks several
@@ -2173,10 +2195,14 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   ra.E = c->dir[1].n;
   ra.EW = (ra.E + 63) / 64;
   ra.NB = d == 0 ? K : D;
+  // the first kernel below empties the hash table for the next run (keys + reps; not the counter)
+  ra.ht_clear = reinterpret_cast<uint32_t*>(dd.ht_key.p);
+  ra.ht_clear_words = uint64_t(dd.ht_cap) * 3;
   if (ido_mode(c)) {  // identity sets first (one wave per representative and 4 slots / descriptors)
     const uint64_t waves = uint64_t(c->n_act[d]) * ((ra.NB + 3) / 4);
     if (d == 0) k_class_ident<false, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
     else k_class_ident<true, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
+    ra.ht_clear_words = 0;
   }
   unsigned g = unsigned(per_rep * ra.rep_blocks);
 #define CYC_ROWS(EG, ERR, KCT, LOOP) k_class_rows<EG, ERR, KCT, LOOP><<<g, 256, 0, st>>>(ra)
