@@ -2067,7 +2067,9 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
   Problem& pb = c->pb;
   const uint32_t P = pb.P, W = pb.W;
   const uint32_t E = c->dir[1].n;
-  const uint32_t r0 = c->rp_off[d], Rp = (which & PEERS_POD) ? c->rp_off[d + 1] - r0 : 0u;
+  // d = 2: both directions in one launch (their peer sub-lists are adjacent)
+  const int dlo = d == 2 ? 0 : d, dhi = d == 2 ? 2 : d + 1;
+  const uint32_t r0 = c->rp_off[dlo], Rp = (which & PEERS_POD) ? c->rp_off[dhi] - r0 : 0u;
   if (Rp && E && W && ido_mode(c)) {
     const uint32_t EW = (E + 63) / 64;
     k_peer_bits<<<unsigned((uint64_t((Rp + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4), 256, 0, st>>>(
@@ -2100,7 +2102,7 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
       k_pod_rows<false><<<g, 256, 0, st>>>(Rp, E, W, plist, ido, c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(),
                                            c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
   }
-  const uint32_t i0 = c->ri_off[d], Ri = (which & PEERS_IP) ? c->ri_off[d + 1] - i0 : 0u;
+  const uint32_t i0 = c->ri_off[dlo], Ri = (which & PEERS_IP) ? c->ri_off[dhi] - i0 : 0u;
   if (Ri && W) {
     const DIPTest* tests = c->ip_tests.as<DIPTest>() + i0;
     if (pb.may_err) {
@@ -2347,7 +2349,7 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
     HIPCHK(hipEventRecord(c->fork_ev, st));
     if (st3 != st) HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
     enq_common(c, st3, COMMON_FILL | COMMON_PORTS);
-    for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st3, PEERS_IP);
+    enq_peer_rows(c, 2, st3, PEERS_IP);  // both directions' IP rows in one launch
     HIPCHK(hipEventRecord(c->ports_ev, st3));
     enq_common(c, st, COMMON_SELECTORS);
     HIPCHK(hipEventRecord(c->sel_ev, st));
