@@ -1604,7 +1604,8 @@ struct cyc_ctx {
   int64_t emit_blocks = 0;  // cyc_set_option "emit_blocks": persistent emit grid (0 = a block per row)
   int class_variant[2] = {3, 3};  // cyc_set_option "class_variant_in" / "_eg" (enq_class_rows;
                                   // defaults measured best on configs #3/#4: profiles/r01_class_sweep.txt)
-  bool use_graphs = true;  // cyc_set_option "graphs"
+  int use_graphs = 1;  // cyc_set_option "graphs": 1 = graph replay, 2 = the same DAG enqueued eagerly
+                      // on three streams with events (no graph launch), 0 = eager on one stream
   int pod_rows = -1;   // cyc_set_option "pod_rows": pod-peer PM rows per pod directly (1), through
                        // identity outcomes and word runs (0), or -1 = direct when identities >= pods / 2
   int member_wave = -1;  // cyc_set_option "member_wave": membership with a wave (1) or a thread (0) per
@@ -2405,6 +2406,18 @@ static void drop_graph(cyc_ctx* c) {
   }
 }
 
+static void ensure_cap_streams(cyc_ctx* c) {
+  if (c->cap_stream) return;
+  HIPCHK(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&c->cap_stream2, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&c->cap_stream3, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&c->sel_ev, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->ports_ev, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->stagger_ev, hipEventDisableTiming));
+}
+
 static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
                         int64_t hi) {
   Problem& pb = c->pb;
@@ -2412,22 +2425,22 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
   if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
   if (c->order_lo != lo || c->order_hi != hi) drop_graph(c);  // range plan buffers are re-made
   ensure_range(c, lo, hi);
-  if (c->use_graphs && !pb.may_err) {
+  if (c->use_graphs == 2 && !pb.may_err) {
+    // the graph's DAG, enqueued directly: the caller's stream forks to two internal streams and
+    // joins them back before the emit (events), without hipGraphLaunch's per-replay latency
+    ensure_cap_streams(c);
+    HIPCHK(hipEventRecord(c->ev[0], st));
+    capture_pipeline(c, st, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status, lo, hi);
+    HIPCHK(hipEventRecord(c->ev[3], st));
+    c->timed = true;
+    c->timed_graph = true;
+  } else if (c->use_graphs && !pb.may_err) {
     // The whole pipeline as one hipGraph (captured once per output buffers / row range):
     // removes the host launch cost of ~16 launches per run (dominant on small problems).
     const void* key[5] = {d_in, d_eg, d_status, reinterpret_cast<void*>(lo), reinterpret_cast<void*>(hi)};
     if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
       drop_graph(c);
-      if (!c->cap_stream) {
-        HIPCHK(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&c->cap_stream2, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&c->cap_stream3, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&c->sel_ev, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&c->ports_ev, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&c->stagger_ev, hipEventDisableTiming));
-      }
+      ensure_cap_streams(c);
       hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
       capture_pipeline(c, c->cap_stream, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status, lo, hi);
@@ -2836,7 +2849,8 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     return (int)CYC_OK;
   }
   if (std::string(name) == "graphs") {
-    c->use_graphs = value != 0;
+    if (value < 0 || value > 2) return fail(c, CYC_ERR_ARG, "graphs must be 0, 1 or 2");
+    c->use_graphs = int(value);
     drop_graph(c);
     return (int)CYC_OK;
   }

@@ -226,12 +226,14 @@ def test_graph_and_eager_paths_agree(gpu):
         P, K, W = sh["pods"], sh["slots"], sh["words"]
         outs = []
         # (graphs, graph_branches, emit_blocks, emit_variant): eager, two-branch graph (replayed),
-        # single-branch graph, tiny persistent emit grid, one block per row, other store variants
+        # single-branch graph, tiny persistent emit grid, one block per row, other store variants,
+        # the graph's DAG enqueued eagerly on three streams (graphs = 2)
         for graphs, branches, blocks, variant, cls in ((0, 1, 1024, 0, 0), (1, 1, 1024, 0, 0), (1, 1, 1024, 0, 0),
                                                        (1, 0, 1024, 0, 1), (1, 1, 8, 0, 2), (0, 1, 0, 0, 3),
                                                        (0, 1, 16, 3, 1), (1, 1, 0, 5, 2), (1, 1, 0, 6, 3), (0, 0, 0, 6, 0),
                                                        (1, 1, 0, 7, 1), (0, 1, 0, 8, 2), (1, 0, 0, 8, 0), (1, 1, 0, 9, 1),
-                                                       (0, 1, 0, 9, 3), (1, 1, 0, -1, 0), (1, 1, 0, 10, 2), (0, 1, 0, 10, 1)):
+                                                       (0, 1, 0, 9, 3), (1, 1, 0, -1, 0), (1, 1, 0, 10, 2), (0, 1, 0, 10, 1),
+                                                       (2, 1, 0, -1, 1), (2, 0, 0, 9, 2), (2, 1, 0, 5, 3)):
             eng.set_option("emit_chunk", 1 + seed % 3)
             eng.set_option("pod_rows", (variant + seed) % 3 - 1)  # direct / word runs / auto
             eng.set_option("emit_merged", int(variant != 5))
