@@ -138,7 +138,8 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  * "member_wave" -1 (default: auto = 1 for <= 4096 identities) / 0 / 1 computes target membership
  * with a thread (0) or a wave (1) per pod identity;
  * "graphs" (default 1) replays the pipeline as one captured hipGraph when the inputs cannot
- * panic (then cyc_last_timings reports only the whole-pipeline time). */
+ * panic (then cyc_last_timings reports only the whole-pipeline time); 2 enqueues the same
+ * three-stream DAG eagerly (no graph), 0 runs every kernel in order on the caller's stream. */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
 
 /* The setting in effect for a tuning knob of cyc_set_option; for "pod_words" the mode the

@@ -157,6 +157,7 @@ def _device_cells(eng, shape, s, d, k):
     ("config3", {"n_ns": 100}, 20000),
     ("config3", {}, 6000),
     ("config4", {"n_pods": 10000, "n_policies": 1000, "n_ns": 100}, 20000),
+    ("config4", {}, 6000),
 ])
 def test_synthetic_sampled_parity(gpu, name, kw, n):
     """Full-size tables vs the oracle on random cells, plus run-to-run determinism."""
