@@ -248,7 +248,8 @@ def main():
     # the emit kernel the library picks by plane-row length (emit_variant -1, engine.hip enq_emit)
     row_bytes = K * W * 8
     emit_kernel = ("k_emit_wide<512,U> (one single-pass block per row)" if row_bytes >= 65536 else
-                   "k_emit (one block per row)" if row_bytes >= 16384 else "k_emit_flat (multi-row blocks)")
+                   "k_emit_wide<256,U> (one single-pass block per row)" if row_bytes >= 16384 else
+                   "k_emit_flat (multi-row blocks)")
 
     # HBM traffic of k_emit from the committed PMC passes for this same workload (rocprofv3
     # --pmc FETCH_SIZE / WRITE_SIZE, corrected per MI355X_MICROARCH.md; scripts/pmc_summary.py)

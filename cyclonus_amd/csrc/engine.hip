@@ -2271,10 +2271,11 @@ static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
     g = (n + per - 1) / per * per;
   }
   // emit_variant -1 (default) = auto by plane-row length: >= 64 KB one 512-thread single-pass
-  // block per row (10), >= 16 KB one 256-thread block per row (0), else the flat multi-row
-  // sweep over ~32 KB per block (9)
+  // block per row (10), >= 16 KB one 256-thread single-pass block per row (11; config #4's 25 KB
+  // rows: 256 x 7 x 16 B, emit -6 % vs two-pass variant 0), else the flat multi-row sweep over
+  // ~32 KB per block (9)
   const uint64_t row_bytes = ea.row_words * 8;
-  const int variant = c->emit_variant >= 0 ? c->emit_variant : (row_bytes >= 65536 ? 10 : row_bytes >= 16384 ? 0 : 9);
+  const int variant = c->emit_variant >= 0 ? c->emit_variant : (row_bytes >= 65536 ? 10 : row_bytes >= 16384 ? 11 : 9);
   if (vec && (variant == 7 || variant == 8)) {  // one block per row group of an XCD segment
     const uint32_t G = variant == 7 ? 2 : 4;
     g = (ea.per_xcd + G - 1) / G * 8;
@@ -2306,6 +2307,18 @@ static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
         else if (need <= 13) k_emit_wide<512, 13, 0><<<gw, 512, 0, st>>>(ea);
         else if (need <= 14) k_emit_wide<512, 14, 0><<<gw, 512, 0, st>>>(ea);
         else k_emit_wide<512, 16, 0><<<gw, 512, 0, st>>>(ea);
+        break;
+      }
+      case 11: {  // 256-thread single pass: smallest UNROLL covering the row (16-64 KB rows)
+        const uint64_t need = (ea.row_words / 2 + 255) / 256;
+        const unsigned gw = ea.per_xcd * 8;
+        if (need <= 4) k_emit_wide<256, 4, 0><<<gw, 256, 0, st>>>(ea);
+        else if (need <= 6) k_emit_wide<256, 6, 0><<<gw, 256, 0, st>>>(ea);
+        else if (need <= 7) k_emit_wide<256, 7, 0><<<gw, 256, 0, st>>>(ea);
+        else if (need <= 8) k_emit_wide<256, 8, 0><<<gw, 256, 0, st>>>(ea);
+        else if (need <= 10) k_emit_wide<256, 10, 0><<<gw, 256, 0, st>>>(ea);
+        else if (need <= 12) k_emit_wide<256, 12, 0><<<gw, 256, 0, st>>>(ea);
+        else k_emit_wide<256, 16, 0><<<gw, 256, 0, st>>>(ea);
         break;
       }
       default: CYC_EMIT(true, 16, true, true); break;

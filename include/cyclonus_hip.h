@@ -122,9 +122,10 @@ int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
 
 /* Tuning knobs (no effect on results): "emit_variant" selects the emit kernel: -1 (default) =
- * auto (0 for plane rows of >= 16 KB, else 9), 0..5 one block per row with different store
- * patterns, 6 rows dealt to the XCDs in chunks ("emit_chunk" rows), 7 / 8 one block per 2 / 4
- * rows, 9 the flat multi-row sweep (~32 KB of rows per block, for short rows);
+ * auto (10 for plane rows of >= 64 KB, 11 for >= 16 KB, else 9), 0..5 one block per row with
+ * different store patterns, 6 rows dealt to the XCDs in chunks ("emit_chunk" rows), 7 / 8 one
+ * block per 2 / 4 rows, 9 the flat multi-row sweep (~32 KB of rows per block, for short rows),
+ * 10 / 11 one 512- / 256-thread block per row covering it in a single pass;
  * "class_variant_in" / "class_variant_eg" 0..3 the class-row kernel shape (bit 0: 4 job slots
  * per thread instead of 8; bit 1: block rows stride over the class representatives);
  * "emit_blocks" the persistent emit grid (0 = one block per row); "emit_merged" (default 1) writes

@@ -234,7 +234,8 @@ def test_graph_and_eager_paths_agree(gpu):
                                                        (0, 1, 16, 3, 1), (1, 1, 0, 5, 2), (1, 1, 0, 6, 3), (0, 0, 0, 6, 0),
                                                        (1, 1, 0, 7, 1), (0, 1, 0, 8, 2), (1, 0, 0, 8, 0), (1, 1, 0, 9, 1),
                                                        (0, 1, 0, 9, 3), (1, 1, 0, -1, 0), (1, 1, 0, 10, 2), (0, 1, 0, 10, 1),
-                                                       (2, 1, 0, -1, 1), (2, 0, 0, 9, 2), (2, 1, 0, 5, 3)):
+                                                       (2, 1, 0, -1, 1), (2, 0, 0, 9, 2), (2, 1, 0, 5, 3), (1, 1, 0, 11, 0),
+                                                       (0, 1, 0, 11, 2)):
             eng.set_option("emit_chunk", 1 + seed % 3)
             eng.set_option("pod_rows", (variant + seed) % 3 - 1)  # direct / word runs / auto
             eng.set_option("emit_merged", int(variant != 5))
@@ -384,7 +385,7 @@ def test_direct_pod_rows_and_flat_emit(gpu, bad):
         except OraclePanic as e:
             want = Panicked(str(e))
         eng.build_policies(pols).load_resources(res)
-        for pod_rows, variant, mw in ((1, 9, 1), (0, 0, 0), (1, 0, 1), (0, 9, 0), (1, 10, 1)):
+        for pod_rows, variant, mw in ((1, 9, 1), (0, 0, 0), (1, 0, 1), (0, 9, 0), (1, 10, 1), (0, 11, 0)):
             eng.set_option("pod_rows", pod_rows)
             eng.set_option("emit_variant", variant)
             eng.set_option("member_wave", mw)  # membership: a wave (1) or a thread (0) per identity
