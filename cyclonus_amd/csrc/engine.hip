@@ -1138,7 +1138,23 @@ struct EmitArgs {
   const uint8_t* st_src;      // job status plane [P][K] (the run's third output), copied by the
   uint8_t* st_dst;            // emit's blocks in slices: no separate copy node ends the step
   uint64_t st_bytes;
+  uint32_t interleave;        // two planes: the row list alternates ingress / egress rows
+  uint32_t deal;              // k_emit_wide: rows dealt to the XCDs in chunks of `chunk` (else segments)
 };
+
+// Row r of a launch's row list -> (plane, pod).  The list is the planes' class-clustered row
+// orders, one after the other, or (interleave, two planes) alternating ingress / egress rows, so
+// every XCD's segment of the list writes into both planes.
+__device__ __forceinline__ void emit_row_of(const EmitArgs& a, uint32_t r, uint32_t& pl, uint32_t& p) {
+  if (a.interleave) {
+    pl = r & 1u;
+    const uint32_t idx = r >> 1;
+    p = a.order[pl][idx];
+  } else {
+    pl = r >= a.n_rows ? 1u : 0u;
+    p = a.order[pl][r - pl * a.n_rows];
+  }
+}
 
 // Block b's slice of the status plane copy (every emit kernel calls this first).
 __device__ __forceinline__ void emit_status(const EmitArgs& a) {
@@ -1152,8 +1168,8 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 template <bool VEC, int UNROLL, bool NT>
 __device__ __forceinline__ void emit_row(const EmitArgs& a, uint32_t r) {
-  const uint32_t pl = r >= a.n_rows ? 1u : 0u;
-  const uint32_t p = a.order[pl][r - pl * a.n_rows];
+  uint32_t pl, p;
+  emit_row_of(a, r, pl, p);
   const uint64_t* src = a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words;
   uint64_t* dst = a.out[pl] + uint64_t(p - a.row_lo) * a.row_words;
   if (VEC) {
@@ -1235,8 +1251,8 @@ __global__ __launch_bounds__(256) void k_emit_group(EmitArgs a) {
     src[g] = nullptr;
     dst[g] = nullptr;
     if (r < r_end) {
-      const uint32_t pl = r >= a.n_rows ? 1u : 0u;
-      const uint32_t p = a.order[pl][r - pl * a.n_rows];
+      uint32_t pl, p;
+      emit_row_of(a, r, pl, p);
       src[g] = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
       dst[g] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
     }
@@ -1287,8 +1303,8 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   const uint32_t nr = min(a.chunk, r_end - r0);
   if (threadIdx.x < nr) {
     const uint32_t r = r0 + threadIdx.x;
-    const uint32_t pl = r >= a.n_rows ? 1u : 0u;
-    const uint32_t p = a.order[pl][r - pl * a.n_rows];
+    uint32_t pl, p;
+    emit_row_of(a, r, pl, p);
     s_src[threadIdx.x] = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
     s_dst[threadIdx.x] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
   }
@@ -1321,10 +1337,17 @@ template <int BS, int UNROLL, int STORE>
 __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   emit_status(a);
   const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
-  const uint32_t r = x * a.per_xcd + (b >> 3);
-  if (r >= min(n, (x + 1) * a.per_xcd)) return;
-  const uint32_t pl = r >= a.n_rows ? 1u : 0u;
-  const uint32_t p = a.order[pl][r - pl * a.n_rows];
+  uint32_t r;
+  if (a.deal) {  // rows dealt to the XCDs in chunks of a.chunk: the 8 XCDs write neighbouring chunks
+    const uint32_t j = b >> 3;
+    r = ((j / a.chunk) * 8 + x) * a.chunk + j % a.chunk;
+    if (r >= n) return;
+  } else {  // XCD x writes its own contiguous segment of the row list
+    r = x * a.per_xcd + (b >> 3);
+    if (r >= min(n, (x + 1) * a.per_xcd)) return;
+  }
+  uint32_t pl, p;
+  emit_row_of(a, r, pl, p);
   const u64x2* si = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
   u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
   const uint32_t n2 = uint32_t(a.row_words / 2);
@@ -1615,6 +1638,9 @@ struct cyc_ctx {
   int graph_stagger = 1;  // cyc_set_option "graph_stagger": 1 = egress class rows wait for the ingress
                           // ones (they run under the ingress emit), 0 = branches unordered
   hipEvent_t stagger_ev = nullptr;
+  int emit_deal = 0;  // cyc_set_option "emit_deal": k_emit_wide rows dealt in chunks of "emit_chunk"
+  int emit_interleave = -1;  // cyc_set_option "emit_interleave": the merged emit alternates plane rows
+                            // (1), keeps them one plane after the other (0), -1 = auto by plane size
   int emit_merged = 1;  // cyc_set_option "emit_merged": both planes in ONE emit launch after both
                         // directions' class rows.  A plane's emit grid fills every CU, so a second
                         // branch's front queued behind it would only run once that emit drains.
@@ -2235,6 +2261,13 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 }
 
 // 7. emit of direction d's plane (d = 2: both planes in one launch, out = ingress, out2 = egress)
+// k_emit_wide grid: one block per row slot of the XCD segments, or of the chunked deal.
+static unsigned wide_grid(const EmitArgs& ea) {
+  if (!ea.deal) return ea.per_xcd * 8;
+  const uint64_t n = uint64_t(ea.n_rows) * ea.planes, per = 8ull * ea.chunk;
+  return unsigned((n + per - 1) / per * per);
+}
+
 // d_status (may be null): the status plane, copied by the emit's blocks.  Returns false if no
 // emit was launched (no rows in the range; the caller then copies the status plane itself).
 static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t lo, int64_t hi, uint64_t* out2 = nullptr,
@@ -2249,6 +2282,12 @@ static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
   ea.n_rows = uint32_t(hi - lo);
   ea.planes = d == 2 ? 2 : 1;
   ea.row_lo = uint32_t(lo);
+  // auto (-1): alternate the planes' rows when each plane is >= 8 GB (config #3 on one GPU: the
+  // merged emit 3.42 -> 3.11 ms on two of three boxes, 1 % on the third; with 5 GB or less per
+  // plane — 2, 4, 8 shards — interleaving cost 1-4 %; profiles/r01_emit_interleave_sweep.txt)
+  const bool big = uint64_t(ea.n_rows) * K * W * 8 >= (8ull << 30);
+  ea.interleave = ea.planes == 2 && (c->emit_interleave > 0 || (c->emit_interleave < 0 && big)) ? 1u : 0u;
+  ea.deal = c->emit_deal ? 1u : 0u;
   for (uint32_t pl = 0; pl < ea.planes; pl++) {
     const int dd = d == 2 ? int(pl) : d;
     ea.order[pl] = c->order[dd].as<uint32_t>();
@@ -2300,7 +2339,7 @@ static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
       case 10: {
         // smallest UNROLL whose single pass covers the row (16 when the row needs more passes)
         const uint64_t need = (ea.row_words / 2 + 511) / 512;
-        const unsigned gw = ea.per_xcd * 8;
+        const unsigned gw = wide_grid(ea);
         if (need <= 8) k_emit_wide<512, 8, 0><<<gw, 512, 0, st>>>(ea);
         else if (need <= 10) k_emit_wide<512, 10, 0><<<gw, 512, 0, st>>>(ea);
         else if (need <= 12) k_emit_wide<512, 12, 0><<<gw, 512, 0, st>>>(ea);
@@ -2311,7 +2350,7 @@ static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
       }
       case 11: {  // 256-thread single pass: smallest UNROLL covering the row (16-64 KB rows)
         const uint64_t need = (ea.row_words / 2 + 255) / 256;
-        const unsigned gw = ea.per_xcd * 8;
+        const unsigned gw = wide_grid(ea);
         if (need <= 4) k_emit_wide<256, 4, 0><<<gw, 256, 0, st>>>(ea);
         else if (need <= 6) k_emit_wide<256, 6, 0><<<gw, 256, 0, st>>>(ea);
         else if (need <= 7) k_emit_wide<256, 7, 0><<<gw, 256, 0, st>>>(ea);
@@ -2851,6 +2890,17 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "emit_deal") {
+    c->emit_deal = int(value != 0);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
+  if (std::string(name) == "emit_interleave") {
+    if (value < -1 || value > 1) return fail(c, CYC_ERR_ARG, "emit_interleave must be -1, 0 or 1");
+    c->emit_interleave = int(value);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "emit_merged") {
     c->emit_merged = int(value != 0);
     drop_graph(c);
@@ -2881,6 +2931,8 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "graph_branches") *value = c->graph_branches;
   else if (n == "graph_stagger") *value = c->graph_stagger;
   else if (n == "emit_merged") *value = c->emit_merged;
+  else if (n == "emit_interleave") *value = c->emit_interleave;
+  else if (n == "emit_deal") *value = c->emit_deal;
   else if (n == "member_wave") *value = c->member_wave;
   else if (n == "pod_rows") *value = c->pod_rows;
   else if (n == "graphs") *value = c->use_graphs;

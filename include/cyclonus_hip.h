@@ -129,7 +129,9 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  * "class_variant_in" / "class_variant_eg" 0..3 the class-row kernel shape (bit 0: 4 job slots
  * per thread instead of 8; bit 1: block rows stride over the class representatives);
  * "emit_blocks" the persistent emit grid (0 = one block per row); "emit_merged" (default 1) writes
- * both planes in one emit launch; "graph_branches" (default 1) runs ingress and egress as two
+ * both planes in one emit launch; "emit_interleave" -1 (default: auto = 1 for planes of >= 8 GB)
+ * / 0 / 1 alternates the two planes' rows in that launch's row list; "emit_deal" (default 0) deals
+ * the rows of emit variants 10 / 11 to the XCDs in chunks of "emit_chunk" rows; "graph_branches" (default 1) runs ingress and egress as two
  * concurrent branches of the step graph; "graph_stagger" (default 1, two-launch emit only) starts
  * the egress class rows after the ingress ones;
  * "pod_words" -1 (default: auto) / 0 / 1 has the class rows read pod-peer words from materialised

@@ -238,6 +238,8 @@ def test_graph_and_eager_paths_agree(gpu):
                                                        (0, 1, 0, 11, 2)):
             eng.set_option("emit_chunk", 1 + seed % 3)
             eng.set_option("pod_rows", (variant + seed) % 3 - 1)  # direct / word runs / auto
+            eng.set_option("emit_interleave", (variant + seed) % 2)  # merged emit: planes alternate
+            eng.set_option("emit_deal", int(variant in (10, 11) and seed % 2 == 0))  # wide emit: chunked XCD deal
             eng.set_option("emit_merged", int(variant != 5))
             eng.set_option("graphs", graphs)
             eng.set_option("graph_branches", branches)
