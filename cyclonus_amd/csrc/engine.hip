@@ -1614,10 +1614,13 @@ struct cyc_ctx {
   DevBuf selres, PM, ER, portok, VALID, DESCW, DM, first_err, order[2];
   DevBuf status_sink;  // status plane target of graph runs given no status pointer (see capture_pipeline)
   // peer-row stage: pod peers in identity space + per-word identity runs; IP peers per pod
+  DevBuf pod_peers_u;  // identity-set (IDOB) rows: the needed pod peers, one per distinct
+                       // (namespace matcher, pod selector) of a direction (peer_ido maps every peer)
   DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
   bool dense_sel = false;  // k_selectors_dense (LVT fits)
   uint32_t Rp = 0, Ri = 0;
   uint32_t rp_off[3] = {0, 0, 0}, ri_off[3] = {0, 0, 0};  // per-direction sub-lists (ingress, egress)
+  uint32_t rpu_off[3] = {0, 0, 0};  // sub-lists of pod_peers_u: one pod peer per distinct matcher
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
   DevBuf act[2], sel_list;
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
@@ -2038,8 +2041,22 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   c->Ri = uint32_t(ip.size());
   upload(c->pod_peers, pp);
   {
-    std::vector<uint32_t> pi(std::max<size_t>(pb.peers.size(), 1), 0);
-    for (size_t x = 0; x < pp.size(); x++) pi[pp[x]] = uint32_t(x);
+    // IDOB rows depend on a pod peer only through (namespace matcher, pod selector)
+    // (podpeermatcher.go:21-28; the port is checked per peer by the class rows), so peers sharing
+    // them share one row: config #3 has 17k pod peers over 7.8k distinct matchers
+    std::vector<uint32_t> pi(std::max<size_t>(pb.peers.size(), 1), 0), ppu;
+    for (int d = 0; d < 2; d++) {
+      c->rpu_off[d] = uint32_t(ppu.size());
+      std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> row;
+      for (uint32_t x = c->rp_off[d]; x < c->rp_off[d + 1]; x++) {
+        const DPeer& pr = pb.peers[pp[x]];
+        auto it = row.emplace(std::make_tuple(pr.nskind, pr.nsval, pr.podsel), uint32_t(ppu.size())).first;
+        if (it->second == ppu.size()) ppu.push_back(pp[x]);
+        pi[pp[x]] = it->second;
+      }
+    }
+    c->rpu_off[2] = uint32_t(ppu.size());
+    upload(c->pod_peers_u, ppu);
     upload(c->peer_ido, pi);
   }
   upload(c->ip_peers, ip);
@@ -2099,10 +2116,11 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
   const uint32_t r0 = c->rp_off[dlo], Rp = (which & PEERS_POD) ? c->rp_off[dhi] - r0 : 0u;
   if (Rp && E && W && ido_mode(c)) {
     const uint32_t EW = (E + 63) / 64;
-    k_peer_bits<<<unsigned((uint64_t((Rp + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4), 256, 0, st>>>(
-        Rp, E, EW, c->pod_peers.as<uint32_t>() + r0, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
+    const uint32_t u0 = c->rpu_off[dlo], Ru = c->rpu_off[dhi] - u0;  // distinct matchers only
+    k_peer_bits<<<unsigned((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4), 256, 0, st>>>(
+        Ru, E, EW, c->pod_peers_u.as<uint32_t>() + u0, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
         c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(),
-        c->idob.as<uint64_t>() + uint64_t(r0) * EW);
+        c->idob.as<uint64_t>() + uint64_t(u0) * EW);
   } else if (Rp && E && W && (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= P)) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
     const unsigned g = unsigned((uint64_t(Rp) * W + 3) / 4);
