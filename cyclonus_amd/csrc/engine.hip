@@ -109,15 +109,15 @@ __global__ void k_selectors(uint32_t S, uint32_t L, const uint32_t* sel_off, con
 // the key replaced by its dense index.  One coalesced load per requirement instead of a binary
 // search over the label set (a chain of dependent loads).
 constexpr uint32_t SEL_LPT = 4;  // label sets per thread in k_selectors_dense (independent loads in flight)
-__global__ __launch_bounds__(256) void k_selectors_dense(uint32_t S, uint32_t L, const uint32_t* __restrict__ sel_off,
+__device__ __forceinline__ void selectors_dense_blk(uint32_t S, uint32_t L, const uint32_t* __restrict__ sel_off,
                                                          const DReq* __restrict__ dreqs, const uint32_t* __restrict__ req_vals,
                                                          const uint32_t* __restrict__ LVT, uint8_t* __restrict__ selres,
-                                                         const uint32_t* __restrict__ sel_list) {
+                                                         const uint32_t* __restrict__ sel_list, uint32_t bid_, uint32_t nblk_) {
   // block = (selector, 256 * SEL_LPT label sets): the requirement walk is block-uniform (scalar
   // loads); each thread evaluates SEL_LPT label sets with their table loads issued together
   const uint32_t lchunks = (L + 256 * SEL_LPT - 1) / (256 * SEL_LPT);
-  uint32_t s = blockIdx.x / lchunks;
-  const uint32_t l0 = (blockIdx.x % lchunks) * 256 * SEL_LPT + threadIdx.x;
+  uint32_t s = bid_ / lchunks;
+  const uint32_t l0 = (bid_ % lchunks) * 256 * SEL_LPT + threadIdx.x;
   if (s >= S) return;
   if (sel_list) s = sel_list[s];
   uint8_t res[SEL_LPT];
@@ -163,11 +163,16 @@ __global__ __launch_bounds__(256) void k_selectors_dense(uint32_t S, uint32_t L,
     if (l < L) selres[uint64_t(s) * L + l] = res[x];
   }
 }
+__global__ __launch_bounds__(256) void k_selectors_dense(uint32_t S, uint32_t L, const uint32_t* __restrict__ sel_off,
+                                                         const DReq* __restrict__ dreqs, const uint32_t* __restrict__ req_vals,
+                                                         const uint32_t* __restrict__ LVT, uint8_t* __restrict__ selres,
+                                                         const uint32_t* __restrict__ sel_list) { selectors_dense_blk(S, L, sel_off, dreqs, req_vals, LVT, selres, sel_list, blockIdx.x, gridDim.x); }
 
-__global__ void k_fill_u32(uint32_t* p, uint64_t n, uint32_t v) {
-  const uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+__device__ __forceinline__ void fill_u32_blk(uint32_t* p, uint64_t n, uint32_t v, uint32_t bid_, uint32_t nblk_) {
+  const uint64_t i = bid_ * uint64_t(blockDim.x) + threadIdx.x;
   if (i < n) p[i] = v;
 }
+__global__ void k_fill_u32(uint32_t* p, uint64_t n, uint32_t v) { fill_u32_blk(p, n, v, blockIdx.x, gridDim.x); }
 
 // IPNet.Contains after To4 collapse (ipaddress.go:10-20): families must agree.
 __device__ __forceinline__ bool cidr_contains(const DCidr& c, const DIP& ip) {
@@ -445,12 +450,12 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* __res
 
 // A wave handles IP_GROUP peers over its 64 words: the words' [min, max] records are loaded once.
 constexpr uint32_t IP_GROUP = 8;
-__global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
+__device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng) {
+                                                      uint32_t* __restrict__ rng, uint32_t bid_, uint32_t nblk_) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t gw = bid_ * 4 + (threadIdx.x >> 6);
   const uint32_t chunks = (W + 63) / 64;
   const uint32_t r0 = (gw / chunks) * IP_GROUP;
   if (r0 >= Ri) return;
@@ -460,11 +465,15 @@ __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, u
   if (valid) wd = words[w];
   for (uint32_t r = r0; r < min(Ri, r0 + IP_GROUP); r++) ip_row_word(tests[r], ip_ex, pod_ip, wd, valid, w, gw % chunks, P, W, lane, PM, rng);
 }
+__global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
+                                                      const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
+                                                      const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
+                                                      uint32_t* __restrict__ rng) { ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, blockIdx.x, gridDim.x); }
 
 // PortMatcher.Allows(ResolvedPort, ResolvedPortName, Protocol) — portmatcher.go:10-92, 190-199.
-__global__ void k_portok(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents, const DDesc* descs,
-                         uint8_t* __restrict__ portok) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void portok_blk(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents, const DDesc* descs,
+                         uint8_t* __restrict__ portok, uint32_t bid_, uint32_t nblk_) {
+  uint32_t i = bid_ * blockDim.x + threadIdx.x;
   if (i >= M * D) return;
   uint32_t m = i / D, e = i % D;
   DPortM pm = pms[m];
@@ -482,15 +491,17 @@ __global__ void k_portok(uint32_t M, uint32_t D, const DPortM* pms, const DPortE
   }
   portok[i] = ok;
 }
+__global__ void k_portok(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents, const DDesc* descs,
+                         uint8_t* __restrict__ portok) { portok_blk(M, D, pms, pents, descs, portok, blockIdx.x, gridDim.x); }
 
 // Per (slot k, word w over pods-as-destinations): VALID bits, the word's common descriptor
 // (DESCW >= 0), none valid (-2) or mixed (-1), and per-descriptor masks DM for mixed words.
-__global__ __launch_bounds__(256) void k_slot_words(uint32_t P, uint32_t K, uint32_t W, uint32_t D,
+__device__ __forceinline__ void slot_words_blk(uint32_t P, uint32_t K, uint32_t W, uint32_t D,
                                                     const int32_t* __restrict__ slot_desc,
                                                     const uint8_t* __restrict__ slot_status, uint64_t* __restrict__ VALID,
-                                                    int32_t* __restrict__ DESCW, uint64_t* __restrict__ DM) {
+                                                    int32_t* __restrict__ DESCW, uint64_t* __restrict__ DM, uint32_t bid_, uint32_t nblk_) {
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t idx = blockIdx.x * 4 + wave;  // (k, w)
+  uint32_t idx = bid_ * 4 + wave;  // (k, w)
   if (idx >= K * W) return;
   uint32_t k = idx / W, w = idx % W;
   uint32_t q = w * 64 + lane;
@@ -518,6 +529,10 @@ __global__ __launch_bounds__(256) void k_slot_words(uint32_t P, uint32_t K, uint
     }
   }
 }
+__global__ __launch_bounds__(256) void k_slot_words(uint32_t P, uint32_t K, uint32_t W, uint32_t D,
+                                                    const int32_t* __restrict__ slot_desc,
+                                                    const uint8_t* __restrict__ slot_status, uint64_t* __restrict__ VALID,
+                                                    int32_t* __restrict__ DESCW, uint64_t* __restrict__ DM) { slot_words_blk(P, K, W, D, slot_desc, slot_status, VALID, DESCW, DM, blockIdx.x, gridDim.x); }
 
 // Target membership per pod identity (TargetsApplyingToPod policy.go:68-82 over the identity's
 // namespace's targets), class hash, and election of a representative per distinct class.
@@ -580,9 +595,9 @@ __device__ __forceinline__ void ht_elect(const MemberArgs& a, uint64_t h, uint32
   atomicMin(&a.ht_rep[s], i);
 }
 
-__global__ void k_member(MemberArgs a) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
-  uint32_t ii = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t nblk_) {
+  if (bid_ == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
+  uint32_t ii = bid_ * blockDim.x + threadIdx.x;
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
   uint32_t ns = a.id_ns[i], ls = a.id_ls[i];
@@ -623,14 +638,15 @@ __global__ void k_member(MemberArgs a) {
   }
   if (leader) ht_elect(a, h, i);
 }
+__global__ void k_member(MemberArgs a) { member_blk(a, blockIdx.x, gridDim.x); }
 
 // The same membership with one wave per identity (lanes over its namespace's targets, one ballot
 // per 64 targets): a run has few identities per namespace but several targets each, so a thread
 // per identity leaves the chip nearly idle behind a chain of dependent loads.  Same list order
 // (ascending target id = primary-key order), same hash, same representative election.
-__global__ __launch_bounds__(256) void k_member_wave(MemberArgs a) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
-  const uint32_t lane = threadIdx.x & 63, ii = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void member_wave_blk(MemberArgs a, uint32_t bid_, uint32_t nblk_) {
+  if (bid_ == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
+  const uint32_t lane = threadIdx.x & 63, ii = bid_ * 4 + (threadIdx.x >> 6);
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
   const uint32_t ns = a.id_ns[i], ls = a.id_ls[i];
@@ -662,14 +678,15 @@ __global__ __launch_bounds__(256) void k_member_wave(MemberArgs a) {
     if (!e) ht_elect(a, h, i);
   }
 }
+__global__ __launch_bounds__(256) void k_member_wave(MemberArgs a) { member_wave_blk(a, blockIdx.x, gridDim.x); }
 
 // Also compacts the class representatives: each block appends its representatives, in act[]
 // order (ascending identity), at a base taken with one atomicAdd — consecutive identities (one
 // namespace) stay adjacent, so consecutive class-row blocks share their targets' peer rows in
 // L2.  The counter starts at ~0 (hash-table memset), so it ends at count - 1.
-__global__ __launch_bounds__(256) void k_classify(MemberArgs a, uint32_t* __restrict__ class_of) {
+__device__ __forceinline__ void classify_blk(MemberArgs a, uint32_t* __restrict__ class_of, uint32_t bid_, uint32_t nblk_) {
   __shared__ uint32_t wsum[4], base;
-  const uint32_t ii = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t ii = bid_ * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool live = ii < a.n_act;
   const uint32_t i = live ? a.act[ii] : 0;
@@ -700,6 +717,7 @@ __global__ __launch_bounds__(256) void k_classify(MemberArgs a, uint32_t* __rest
   for (uint32_t x = 0; x < wv; x++) off += wsum[x];
   if (f) a.reps[off + __popcll(m & ((1ull << lane) - 1))] = i;
 }
+__global__ __launch_bounds__(256) void k_classify(MemberArgs a, uint32_t* __restrict__ class_of) { classify_blk(a, class_of, blockIdx.x, gridDim.x); }
 
 
 // Class rows.  For a class representative i, a chunk of KC job slots and one 64-pod word w, walk
@@ -714,6 +732,7 @@ struct RowArgs {
   const DPeer* peers;
   const uint64_t *PM, *ER;
   const uint8_t* portok;
+  const uint32_t* portbits;  // fused IDO egress: portok row m as bits over descriptors (D <= 32), else null
   uint32_t D;
   uint32_t n_ident, K, W, P;
   const uint32_t* reps;     // class representatives (k_classify)
@@ -747,9 +766,9 @@ struct RowArgs {
   uint64_t ht_clear_words;
 };
 
-__device__ __forceinline__ void ht_clear_slice(const RowArgs& a) {
+__device__ __forceinline__ void ht_clear_slice(const RowArgs& a, uint32_t bid, uint32_t nblk) {
   if (!a.ht_clear_words) return;
-  const uint64_t per = (a.ht_clear_words + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
+  const uint64_t per = (a.ht_clear_words + nblk - 1) / nblk, lo = uint64_t(bid) * per;
   const uint64_t hi = lo + per < a.ht_clear_words ? lo + per : a.ht_clear_words;
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.ht_clear[i] = 0xFFFFFFFFu;
 }
@@ -768,11 +787,11 @@ constexpr uint32_t IDO_LDS_BYTES = 48 * 1024;  // staged identity sets per class
 // outcomes (podpeermatcher.go:21-28: namespace then pod matcher) are independent selres gathers;
 // one ballot per peer -> IDOB (no-panic runs only).
 constexpr uint32_t PB_GROUP = 8;
-__global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
+__device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
                                                    const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres, uint32_t L,
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
-                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob) {
-  const uint32_t wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t bid_, uint32_t nblk_) {
+  const uint32_t wv = bid_ * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t groups = (Rp + PB_GROUP - 1) / PB_GROUP;
   if (wv >= groups * EW) return;
   const uint32_t g = wv / EW, ew = wv % EW;
@@ -792,16 +811,20 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
   const uint32_t p = g * PB_GROUP + lane;
   if (lane < PB_GROUP && p < Rp) idob[uint64_t(p) * EW + ew] = mine;
 }
+__global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
+                                                   const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres, uint32_t L,
+                                                   const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
+                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob) { peer_bits_blk(Rp, E, EW, pod_peers, peers, selres, L, id_ns, id_nsls, id_ls, idob, blockIdx.x, gridDim.x); }
 
 // Per class representative and NB index (ingress: job slot, egress: job descriptor): the set of
 // egress identities its targets' pod / all / ports-for-all peers allow on that port (target.go:29-36
 // is an OR over peers; without a panic its order only matters for early exit).  One wave per
 // (representative, NB index), lanes over 64-identity words.
 template <bool EGRESS, int G>
-__global__ __launch_bounds__(256) void k_class_ident(RowArgs a) {
-  ht_clear_slice(a);
+__device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
+  ht_clear_slice(a, bid_, nblk_);
   // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
-  const uint32_t wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t wv = bid_ * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t nbc = (a.NB + G - 1) / G;
   const uint32_t r = wv / nbc, nb0 = (wv % nbc) * G;
   if (r >= *a.rep_cnt + 1u) return;
@@ -861,6 +884,8 @@ __global__ __launch_bounds__(256) void k_class_ident(RowArgs a) {
     a.ip_cnt[i] = m;
   }
 }
+template <bool EGRESS, int G>
+__global__ __launch_bounds__(256) void k_class_ident(RowArgs a) { class_ident_blk<EGRESS, G>(a, blockIdx.x, gridDim.x); }
 
 // Port check of one peer's port matcher row `pok` for job slot k of pod word w: all 64 pods
 // (descriptor du >= 0), none (invalid slot), or per destination (egress word whose
@@ -1013,7 +1038,7 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
 // needs to stay at 3 waves/SIMD.
 template <bool EGRESS, bool ERR, int KC, bool LOOP>
 __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
-  ht_clear_slice(a);
+  ht_clear_slice(a, blockIdx.x, gridDim.x);
   const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
   const uint32_t kc = (blockIdx.x / chunks) % nkc;
   const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
@@ -1042,20 +1067,21 @@ __device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const Word
 }
 
 template <bool EGRESS, int KC>
-__global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) {
+__device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   extern __shared__ uint64_t sB[];
   const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
-  const uint32_t kc = (blockIdx.x / chunks) % nkc;
-  const uint32_t r = blockIdx.x / (chunks * nkc);
+  const uint32_t kc = (bid_ / chunks) % nkc;
+  const uint32_t r = bid_ / (chunks * nkc);
   if (r >= *a.rep_cnt + 1u) return;  // whole block
   const uint32_t i = a.reps[r], k0 = kc * KC;
   const uint32_t nrow = EGRESS ? a.NB : min(uint32_t(KC), a.K - k0);
   const uint64_t* src = a.B + (uint64_t(i) * a.NB + (EGRESS ? 0u : k0)) * a.EW;
-  for (uint32_t x = threadIdx.x; x < nrow * a.EW; x += blockDim.x) sB[x] = src[x];
-  __syncthreads();
-  const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
-  if (w >= a.W) return;
-  const WordRuns wr = a.runs[w];
+  // the word's own loads (runs, slot words) are issued before the staging barrier, so their
+  // latency overlaps the staging loads instead of following them
+  const uint32_t w = (bid_ % chunks) * 256 + threadIdx.x;
+  const bool live = w < a.W;
+  WordRuns wr{};
+  if (live) wr = a.runs[w];
   const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
   const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
   uint64_t valid[KC], allow[KC];
@@ -1066,7 +1092,7 @@ __global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) {
     valid[kk] = 0;
     allow[kk] = 0;
     du[kk] = -2;
-    if (k < a.K) {
+    if (k < a.K && live) {
       if (EGRESS) {
         valid[kk] = a.VALID[uint64_t(k) * a.W + w];
         du[kk] = a.DESCW[uint64_t(k) * a.W + w];
@@ -1075,6 +1101,15 @@ __global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) {
         valid[kk] = v ? wmask : 0ull;
         du[kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
       }
+    }
+  }
+  for (uint32_t x = threadIdx.x; x < nrow * a.EW; x += blockDim.x) sB[x] = src[x];
+  __syncthreads();
+  if (!live) return;
+#pragma unroll
+  for (int kk = 0; kk < KC; kk++) {
+    const uint32_t k = k0 + kk;
+    if (k < a.K) {
       if (du[kk] >= 0) {
         allow[kk] = expand_runs(sB + uint64_t(EGRESS ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wr);
       } else if (EGRESS && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
@@ -1090,14 +1125,16 @@ __global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) {
   const uint4* il = a.ip_list + a.ip_off[i];
   for (uint32_t x0 = 0; x0 < m; x0 += PEER_BATCH) {
     uint64_t pm[PEER_BATCH];
-    uint32_t port[PEER_BATCH];
+    uint32_t port[PEER_BATCH], pbits[PEER_BATCH];
 #pragma unroll
     for (uint32_t u = 0; u < PEER_BATCH; u++) {
       pm[u] = 0;
       port[u] = 0;
+      pbits[u] = 0;
       if (x0 + u < m) {
         const uint4 jp = il[x0 + u];
         port[u] = jp.y;
+        if (EGRESS && a.portbits) pbits[u] = a.portbits[jp.y];  // block-uniform: one scalar load per peer
         if (w >= jp.z && w <= jp.w) pm[u] = a.PM[uint64_t(jp.x) * a.W + w];  // inside the peer's nonzero words
       }
     }
@@ -1105,8 +1142,13 @@ __global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) {
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
 #pragma unroll
-      for (uint32_t u = 0; u < PEER_BATCH; u++)
-        if (pm[u]) allow[kk] |= pm[u] & port_mask<EGRESS>(a, a.portok + uint64_t(port[u]) * a.D, du[kk], k0 + kk, w);
+      for (uint32_t u = 0; u < PEER_BATCH; u++) {
+        if (!pm[u]) continue;
+        // egress: the descriptor varies per destination word, so the byte table would cost a
+        // vector load per (slot, peer); the bit row is a shift
+        if (EGRESS && a.portbits && du[kk] >= 0) allow[kk] |= ((pbits[u] >> du[kk]) & 1u) ? pm[u] : 0ull;
+        else allow[kk] |= pm[u] & port_mask<EGRESS>(a, a.portok + uint64_t(port[u]) * a.D, du[kk], k0 + kk, w);
+      }
       undecided |= valid[kk] & ~allow[kk];
     }
     if (!undecided) break;
@@ -1116,6 +1158,120 @@ __global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) {
     const uint32_t k = k0 + kk;
     if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
   }
+}
+template <bool EGRESS, int KC>
+__global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) { class_rows_ido_blk<EGRESS, KC>(a, blockIdx.x, gridDim.x); }
+
+// Fused front (cyc_set_option "front_fused", IDO builds): the front's ~15 kernels of two graph
+// branches become 5 launches on ONE stream, each launch a concatenation of independent block
+// ranges (every range calls the same per-block body as its stand-alone kernel, with its own
+// block index and count).  A launch depends on the previous one only, so the graph needs no
+// cross-stream edges (each cost ~10 us of join latency on the critical path) and both
+// directions' blocks share every launch.
+//   A: IP word spans reset | port table | slot words | selectors        (independent)
+//   B: IP rows (both directions) | pod-peer identity sets (both) | membership in | membership eg
+//   C: class election in | eg           D: identity sets in | eg         E: class rows in | eg
+struct FrontA {
+  uint32_t nb[4];
+  uint32_t* fill_p;
+  uint64_t fill_n;
+  uint32_t M, D, P, K, W, S, L;
+  const DPortM* pms;
+  const DPortEntry* pents;
+  const DDesc* descs;
+  uint8_t* portok;
+  const int32_t* slot_desc;
+  const uint8_t* slot_status;
+  uint64_t* VALID;
+  int32_t* DESCW;
+  uint64_t* DM;
+  const uint32_t *sel_off, *req_vals, *LVT, *sel_list;
+  const DReq* dreqs;
+  uint8_t* selres;
+};
+__global__ __launch_bounds__(256) void k_front_a(FrontA f) {
+  uint32_t b = blockIdx.x;
+  if (b < f.nb[0]) return fill_u32_blk(f.fill_p, f.fill_n, 0xFFFFFFFFu, b, f.nb[0]);
+  b -= f.nb[0];
+  if (b < f.nb[1]) return portok_blk(f.M, f.D, f.pms, f.pents, f.descs, f.portok, b, f.nb[1]);
+  b -= f.nb[1];
+  if (b < f.nb[2]) return slot_words_blk(f.P, f.K, f.W, f.D, f.slot_desc, f.slot_status, f.VALID, f.DESCW, f.DM, b, f.nb[2]);
+  b -= f.nb[2];
+  if (b < f.nb[3]) selectors_dense_blk(f.S, f.L, f.sel_off, f.dreqs, f.req_vals, f.LVT, f.selres, f.sel_list, b, f.nb[3]);
+}
+
+struct FrontB {
+  uint32_t nb[5];
+  uint32_t M, D;
+  const uint8_t* portok;
+  uint32_t* portbits;
+  uint32_t Ri, P, W;
+  const DIPTest* tests;
+  const DCidr* ip_ex;
+  const DIP* pod_ip;
+  const DWordIP* words;
+  uint64_t* PM;
+  uint32_t* rng;
+  uint32_t Ru, E, EW, L;
+  const uint32_t* pod_peers_u;
+  const DPeer* peers;
+  const uint8_t* selres;
+  const uint32_t *id_ns, *id_nsls, *id_ls;
+  uint64_t* idob;
+  MemberArgs ma[2];
+  uint32_t member_wave[2];  // 1: a wave per identity (k_member_wave), 0: a thread per identity
+};
+__global__ __launch_bounds__(256) void k_front_b(FrontB f) {
+  uint32_t b = blockIdx.x;
+  if (b < f.nb[0]) return ip_rows_fast_blk(f.Ri, f.P, f.W, f.tests, f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, b, f.nb[0]);
+  b -= f.nb[0];
+  if (b < f.nb[1])
+    return peer_bits_blk(f.Ru, f.E, f.EW, f.pod_peers_u, f.peers, f.selres, f.L, f.id_ns, f.id_nsls, f.id_ls, f.idob, b, f.nb[1]);
+  b -= f.nb[1];
+#pragma unroll
+  for (int d = 0; d < 2; d++) {
+    if (b < f.nb[2 + d]) {
+      if (f.member_wave[d]) member_wave_blk(f.ma[d], b, f.nb[2 + d]);
+      else member_blk(f.ma[d], b, f.nb[2 + d]);
+      return;
+    }
+    b -= f.nb[2 + d];
+  }
+  // port table rows as descriptor bit masks (D <= 32), for the egress class rows
+  const uint32_t m = b * 256 + threadIdx.x;
+  if (b < f.nb[4] && m < f.M) {
+    uint32_t bits = 0;
+    for (uint32_t e = 0; e < f.D; e++) bits |= f.portok[uint64_t(m) * f.D + e] ? (1u << e) : 0u;
+    f.portbits[m] = bits;
+  }
+}
+
+struct FrontC {
+  uint32_t nb[2];
+  MemberArgs ma[2];
+  uint32_t* class_of[2];
+};
+__global__ __launch_bounds__(256) void k_front_c(FrontC f) {
+  const uint32_t b = blockIdx.x;
+  if (b < f.nb[0]) classify_blk(f.ma[0], f.class_of[0], b, f.nb[0]);
+  else classify_blk(f.ma[1], f.class_of[1], b - f.nb[0], f.nb[1]);
+}
+
+struct FrontRows {
+  uint32_t nb[2];
+  RowArgs ra[2];
+};
+__global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
+  const uint32_t b = blockIdx.x;
+  if (b < f.nb[0]) class_ident_blk<false, 4>(f.ra[0], b, f.nb[0]);
+  else class_ident_blk<true, 4>(f.ra[1], b - f.nb[0], f.nb[1]);
+}
+// egress blocks first: they are the slower ones (per-destination port masks), so the launch's
+// tail is made of the shorter ingress blocks
+__global__ __launch_bounds__(256) void k_front_e(FrontRows f) {
+  const uint32_t b = blockIdx.x;
+  if (b < f.nb[1]) class_rows_ido_blk<true, 4>(f.ra[1], b, f.nb[1]);
+  else class_rows_ido_blk<false, 4>(f.ra[0], b - f.nb[1], f.nb[0]);
 }
 
 // The HBM-bound kernel: every target pod's plane rows are a copy of its class rows.
@@ -1611,7 +1767,7 @@ struct cyc_ctx {
   // device tables
   DevBuf ls_off, ls_key, ls_val, sel_off, reqs, req_vals, pod_ns, pod_ls, pod_nsls, pod_ip, cidrs, ipbs, ipb_ex, pms,
       pents, peers, descs, slot_desc, slot_status, slot_cfg, slot_idx;
-  DevBuf selres, PM, ER, portok, VALID, DESCW, DM, first_err, order[2];
+  DevBuf selres, PM, ER, portok, portbits, VALID, DESCW, DM, first_err, order[2];
   DevBuf status_sink;  // status plane target of graph runs given no status pointer (see capture_pipeline)
   // peer-row stage: pod peers in identity space + per-word identity runs; IP peers per pod
   DevBuf pod_peers_u;  // identity-set (IDOB) rows: the needed pod peers, one per distinct
@@ -1648,6 +1804,8 @@ struct cyc_ctx {
                         // directions' class rows.  A plane's emit grid fills every CU, so a second
                         // branch's front queued behind it would only run once that emit drains.
   bool graph_branches = true;  // cyc_set_option "graph_branches": ingress / egress as two graph branches
+  int front_fused = 1;  // cyc_set_option "front_fused": the graphed front as 5 block-range-fused launches
+                       // on one stream (enq_front_fused; IDO builds), 0 = the two-branch DAG
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
   hipEvent_t fork_ev = nullptr, join_ev = nullptr, sel_ev = nullptr, ports_ev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
@@ -1878,6 +2036,7 @@ static void prepare_device(cyc_ctx* c) {
     c->idob.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * ((c->ids[1].ns.size() + 63) / 64) * 8, 16));
   }
   c->portok.alloc(std::max<uint64_t>(pb.pms.size() * D, 16));
+  c->portbits.alloc(std::max<uint64_t>(pb.pms.size() * 4, 16));
   c->VALID.alloc(std::max<uint64_t>(K * W * 8, 16));
   c->DESCW.alloc(std::max<uint64_t>(K * W * 4, 16));
   c->DM.alloc(std::max<uint64_t>(K * D * W * 8, 16));
@@ -2193,11 +2352,10 @@ static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
 }
 
 // 6. class rows of direction d
-static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
+static RowArgs row_args(cyc_ctx* c, int d) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   DirDev& dd = c->dir[d];
-  if (!dd.n || !K || !W || !c->n_act[d]) return;
   RowArgs ra{};
   ra.tgt = dd.tgt.as<DTarget>();
   ra.peers = c->peers.as<DPeer>();
@@ -2245,6 +2403,19 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   // the first kernel below empties the hash table for the next run (keys + reps; not the counter)
   ra.ht_clear = reinterpret_cast<uint32_t*>(dd.ht_key.p);
   ra.ht_clear_words = uint64_t(dd.ht_cap) * 3;
+  return ra;
+}
+
+static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
+  Problem& pb = c->pb;
+  const uint32_t K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
+  DirDev& dd = c->dir[d];
+  if (!dd.n || !K || !W || !c->n_act[d]) return;
+  RowArgs ra = row_args(c, d);
+  const int var = d == 0 ? c->class_variant[0] : c->class_variant[1];
+  const uint32_t kct = (var & 1) ? 4 : 8;
+  const bool loop = (var & 2) != 0;
+  const uint64_t per_rep = uint64_t((W + 255) / 256) * ((K + kct - 1) / kct);
   if (ido_mode(c)) {  // identity sets first (one wave per representative and 4 slots / descriptors)
     const uint64_t waves = uint64_t(c->n_act[d]) * ((ra.NB + 3) / 4);
     if (d == 0) k_class_ident<false, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
@@ -2384,18 +2555,136 @@ static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
   return true;
 }
 
+// The fused front (k_front_a..e, one stream): the same block ranges the two-branch DAG launches
+// as ~15 kernels (enq_common, enq_peer_rows, enq_member, enq_class_rows), grouped by dependency
+// level.  Applies to IDO builds with dense selectors and 4 job slots per class-row thread (the
+// defaults on configs #2-#4); returns false (nothing enqueued) otherwise.
+static bool front_fused_ok(const cyc_ctx* c) {
+  const Problem& pb = c->pb;
+  if (!c->front_fused || !c->emit_merged || pb.may_err || !ido_mode(c)) return false;
+  if (!pb.P || !pb.K || !pb.W) return false;
+  if (uint64_t(c->n_sel) * pb.L && !c->dense_sel) return false;
+  return (c->class_variant[0] & 1) && (c->class_variant[1] & 1);  // KC = 4 both directions
+}
+
+static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nullptr, hipEvent_t ev_rows = nullptr) {
+  Problem& pb = c->pb;
+  const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
+  const uint32_t M = uint32_t(pb.pms.size()), E = c->dir[1].n, EW = (E + 63) / 64;
+  bool fits = true;  // every launch's block count below 2^31 (else the DAG path runs)
+  auto blocks = [&fits](uint64_t n) {
+    fits = fits && n < (1ull << 30);
+    return uint32_t(n);
+  };
+  // A: IP word spans | port table | slot words | selectors
+  FrontA fa{};
+  fa.fill_p = c->ip_rng.as<uint32_t>();
+  fa.fill_n = c->Ri ? c->ip_rng.bytes / 4 : 0;
+  fa.nb[0] = blocks((fa.fill_n + 255) / 256);
+  fa.M = M;
+  fa.D = D;
+  fa.P = P;
+  fa.K = K;
+  fa.W = W;
+  fa.pms = c->pms.as<DPortM>();
+  fa.pents = c->pents.as<DPortEntry>();
+  fa.descs = c->descs.as<DDesc>();
+  fa.portok = c->portok.as<uint8_t>();
+  fa.nb[1] = (M && pb.descs.size()) ? blocks((uint64_t(M) * D + 255) / 256) : 0u;
+  fa.slot_desc = c->slot_desc.as<int32_t>();
+  fa.slot_status = c->slot_status.as<uint8_t>();
+  fa.VALID = c->VALID.as<uint64_t>();
+  fa.DESCW = c->DESCW.as<int32_t>();
+  fa.DM = c->DM.as<uint64_t>();
+  fa.nb[2] = blocks((uint64_t(K) * W + 3) / 4);
+  fa.S = c->n_sel;
+  fa.L = pb.L;
+  fa.sel_off = c->sel_off.as<uint32_t>();
+  fa.dreqs = c->dreqs.as<DReq>();
+  fa.req_vals = c->req_vals.as<uint32_t>();
+  fa.LVT = c->lvt.as<uint32_t>();
+  fa.selres = c->selres.as<uint8_t>();
+  fa.sel_list = c->sel_list.as<uint32_t>();
+  fa.nb[3] = uint64_t(c->n_sel) * pb.L ? blocks(uint64_t(c->n_sel) * ((pb.L + 256 * SEL_LPT - 1) / (256 * SEL_LPT))) : 0u;
+  // B: IP rows | pod-peer identity sets (both directions' adjacent sub-lists) | membership x 2
+  FrontB fb{};
+  const uint32_t i0 = c->ri_off[0], Ri = c->ri_off[2] - i0;
+  fb.Ri = Ri;
+  fb.P = P;
+  fb.W = W;
+  fb.tests = c->ip_tests.as<DIPTest>() + i0;
+  fb.ip_ex = c->ip_ex.as<DCidr>();
+  fb.pod_ip = c->pod_ip.as<DIP>();
+  fb.words = c->ip_words.as<DWordIP>();
+  fb.PM = c->PM.as<uint64_t>();
+  fb.rng = c->ip_rng.as<uint32_t>();
+  fb.nb[0] = Ri ? blocks((uint64_t((W + 63) / 64) * ((Ri + IP_GROUP - 1) / IP_GROUP) + 3) / 4) : 0u;
+  const uint32_t Rp = c->rp_off[2] - c->rp_off[0], u0 = c->rpu_off[0], Ru = c->rpu_off[2] - u0;
+  fb.Ru = Ru;
+  fb.E = E;
+  fb.EW = EW;
+  fb.L = pb.L;
+  fb.pod_peers_u = c->pod_peers_u.as<uint32_t>() + u0;
+  fb.peers = c->peers.as<DPeer>();
+  fb.selres = c->selres.as<uint8_t>();
+  fb.id_ns = c->dir[1].id_ns.as<uint32_t>();
+  fb.id_nsls = c->id_nsls.as<uint32_t>();
+  fb.id_ls = c->dir[1].id_ls.as<uint32_t>();
+  fb.idob = c->idob.as<uint64_t>() + uint64_t(u0) * EW;
+  fb.nb[1] = (Rp && E) ? blocks((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4) : 0u;
+  FrontC fc{};
+  FrontRows fd{}, fe{};
+  size_t lds = 0;
+  for (int d = 0; d < 2; d++) {
+    const uint32_t na = c->dir[d].n ? c->n_act[d] : 0u;
+    fb.ma[d] = member_args(c, d);
+    fc.ma[d] = fb.ma[d];
+    fc.class_of[d] = c->dir[d].class_of.as<uint32_t>();
+    fb.member_wave[d] = c->member_wave > 0 || (c->member_wave < 0 && na <= 4096 && c->act_targets[d] >= 4.0);
+    fb.nb[2 + d] = na ? blocks(fb.member_wave[d] ? (uint64_t(na) + 3) / 4 : (uint64_t(na) + 255) / 256) : 0u;
+    fc.nb[d] = na ? blocks((uint64_t(na) + 255) / 256) : 0u;
+    if (!na) continue;
+    fd.ra[d] = row_args(c, d);  // its blocks empty the direction's hash table for the next run
+    fe.ra[d] = fd.ra[d];
+    fe.ra[d].ht_clear_words = 0;
+    fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + 3) / 4) + 3) / 4);
+    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + 3) / 4) * na);
+    lds = std::max<size_t>(lds, size_t(d == 0 ? std::min<uint32_t>(4, K) : D) * fd.ra[d].EW * 8);
+  }
+  const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
+  const bool bits = fa.nb[1] && D <= 32;
+  fb.M = M;
+  fb.D = D;
+  fb.portok = c->portok.as<uint8_t>();
+  fb.portbits = c->portbits.as<uint32_t>();
+  fb.nb[4] = bits ? blocks((uint64_t(M) + 255) / 256) : 0u;
+  fe.ra[1].portbits = bits && fe.nb[1] ? c->portbits.as<uint32_t>() : nullptr;
+  const uint64_t gb = uint64_t(fb.nb[0]) + fb.nb[1] + fb.nb[2] + fb.nb[3] + fb.nb[4];
+  if (!fits) return false;
+  if (ga) k_front_a<<<unsigned(ga), 256, 0, st>>>(fa);
+  if (gb) k_front_b<<<unsigned(gb), 256, 0, st>>>(fb);
+  if (fc.nb[0] + fc.nb[1]) k_front_c<<<fc.nb[0] + fc.nb[1], 256, 0, st>>>(fc);
+  if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
+  if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
+  if (fe.nb[0] + fe.nb[1]) k_front_e<<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
+  if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
+  return true;
+}
+
 // Eager launch, in phase order with the timing events: [0] start, [1] after the front (peer
 // rows, classes), [2] after the class rows, [3] after both emits.
 static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
                              int64_t hi) {
   Problem& pb = c->pb;
   HIPCHK(hipEventRecord(c->ev[0], st));
-  enq_common(c, st);
-  for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st);
-  for (int d = 0; d < 2; d++) enq_member(c, d, st);
-  HIPCHK(hipEventRecord(c->ev[1], st));
-  for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
-  HIPCHK(hipEventRecord(c->ev[2], st));
+  if (!(front_fused_ok(c) && enq_front_fused(c, st, c->ev[1], c->ev[2]))) {
+    enq_common(c, st);
+    for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st);
+    for (int d = 0; d < 2; d++) enq_member(c, d, st);
+    HIPCHK(hipEventRecord(c->ev[1], st));
+    for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
+    HIPCHK(hipEventRecord(c->ev[2], st));
+  }
   bool status_done;
   if (c->emit_merged) {
     status_done = enq_emit(c, 2, st, d_in, lo, hi, d_eg, d_status);
@@ -2414,7 +2703,9 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
                              uint8_t* d_status, int64_t lo, int64_t hi) {
   Problem& pb = c->pb;
   if (!c->graph_branches) st2 = st3 = st;
-  if (c->emit_merged) {
+  if (front_fused_ok(c) && enq_front_fused(c, st)) {
+    if (enq_emit(c, 2, st, d_in, lo, hi, d_eg, d_status)) return;
+  } else if (c->emit_merged) {
     // DAG: [st3] IP rows of both directions + port tables || [st] selectors, then per direction
     // pod-peer sets -> membership / classes -> (wait for st3) class rows; one emit of both planes.
     HIPCHK(hipEventRecord(c->fork_ev, st));
@@ -2924,6 +3215,11 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "front_fused") {
+    c->front_fused = int(value != 0);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "graph_stagger") {
     c->graph_stagger = int(value != 0);
     drop_graph(c);
@@ -2948,6 +3244,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "class_variant_eg") *value = c->class_variant[1];
   else if (n == "graph_branches") *value = c->graph_branches;
   else if (n == "graph_stagger") *value = c->graph_stagger;
+  else if (n == "front_fused") *value = c->front_fused;
   else if (n == "emit_merged") *value = c->emit_merged;
   else if (n == "emit_interleave") *value = c->emit_interleave;
   else if (n == "emit_deal") *value = c->emit_deal;
