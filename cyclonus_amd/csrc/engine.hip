@@ -760,6 +760,7 @@ struct RowArgs {
   uint4* ip_list;            // (peer, port matcher, first, last nonzero PM word)
   const uint32_t* ip_rng;    // [R][2] first word, ~last word of each IP peer's nonzero PM words (no-panic runs)
   uint32_t E, EW, NB;
+  uint32_t rpb;              // IDO class rows: representatives per block (class_rows_ido_blk)
   // the direction's hash table (keys + reps), emptied for the NEXT run by the first class-row
   // kernel in block slices once k_classify is done with it: no memset node precedes k_member
   uint32_t* ht_clear;
@@ -1069,13 +1070,14 @@ __device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const Word
 template <bool EGRESS, int KC>
 __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   extern __shared__ uint64_t sB[];
+  // block = (a.rpb consecutive class representatives, KC job slots, 256 pod words): the word's
+  // runs and slot words are loaded once for all its representatives
   const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
   const uint32_t kc = (bid_ / chunks) % nkc;
-  const uint32_t r = bid_ / (chunks * nkc);
-  if (r >= *a.rep_cnt + 1u) return;  // whole block
-  const uint32_t i = a.reps[r], k0 = kc * KC;
-  const uint32_t nrow = EGRESS ? a.NB : min(uint32_t(KC), a.K - k0);
-  const uint64_t* src = a.B + (uint64_t(i) * a.NB + (EGRESS ? 0u : k0)) * a.EW;
+  const uint32_t r0 = (bid_ / (chunks * nkc)) * a.rpb, n_reps = *a.rep_cnt + 1u;
+  if (r0 >= n_reps) return;  // whole block
+  const uint32_t nr = min(a.rpb, n_reps - r0), k0 = kc * KC;
+  const uint32_t nrow = EGRESS ? a.NB : min(uint32_t(KC), a.K - k0), rowsz = nrow * a.EW;
   // the word's own loads (runs, slot words) are issued before the staging barrier, so their
   // latency overlaps the staging loads instead of following them
   const uint32_t w = (bid_ % chunks) * 256 + threadIdx.x;
@@ -1084,79 +1086,86 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   if (live) wr = a.runs[w];
   const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
   const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
-  uint64_t valid[KC], allow[KC];
+  uint64_t valid[KC];
   int32_t du[KC];
 #pragma unroll
   for (int kk = 0; kk < KC; kk++) {
     const uint32_t k = k0 + kk;
     valid[kk] = 0;
-    allow[kk] = 0;
     du[kk] = -2;
-    if (k < a.K && live) {
-      if (EGRESS) {
-        valid[kk] = a.VALID[uint64_t(k) * a.W + w];
-        du[kk] = a.DESCW[uint64_t(k) * a.W + w];
-      } else {
-        const bool v = a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID;
-        valid[kk] = v ? wmask : 0ull;
-        du[kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
-      }
+    if (EGRESS && k < a.K && live) {
+      valid[kk] = a.VALID[uint64_t(k) * a.W + w];
+      du[kk] = a.DESCW[uint64_t(k) * a.W + w];
     }
   }
-  for (uint32_t x = threadIdx.x; x < nrow * a.EW; x += blockDim.x) sB[x] = src[x];
+  for (uint32_t q = 0; q < nr; q++) {
+    const uint64_t* src = a.B + (uint64_t(a.reps[r0 + q]) * a.NB + (EGRESS ? 0u : k0)) * a.EW;
+    for (uint32_t x = threadIdx.x; x < rowsz; x += blockDim.x) sB[q * rowsz + x] = src[x];
+  }
   __syncthreads();
   if (!live) return;
-#pragma unroll
-  for (int kk = 0; kk < KC; kk++) {
-    const uint32_t k = k0 + kk;
-    if (k < a.K) {
-      if (du[kk] >= 0) {
-        allow[kk] = expand_runs(sB + uint64_t(EGRESS ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wr);
-      } else if (EGRESS && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
-        const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
-        for (uint32_t d = 0; d < a.D; d++) allow[kk] |= expand_runs(sB + uint64_t(d) * a.EW, wr) & dm[uint64_t(d) * a.W];
-      }
-    }
-  }
-  // IP peers (ippeermatcher.go:43-50): per pod word through the PM rows, PEER_BATCH peers' words
-  // loaded at once (no panic in IDO builds: the OR is order-free; the undecided check only ends
-  // the walk early, once per batch)
-  const uint32_t m = a.cnt[i] ? a.ip_cnt[i] : 0u;
-  const uint4* il = a.ip_list + a.ip_off[i];
-  for (uint32_t x0 = 0; x0 < m; x0 += PEER_BATCH) {
-    uint64_t pm[PEER_BATCH];
-    uint32_t port[PEER_BATCH], pbits[PEER_BATCH];
-#pragma unroll
-    for (uint32_t u = 0; u < PEER_BATCH; u++) {
-      pm[u] = 0;
-      port[u] = 0;
-      pbits[u] = 0;
-      if (x0 + u < m) {
-        const uint4 jp = il[x0 + u];
-        port[u] = jp.y;
-        if (EGRESS && a.portbits) pbits[u] = a.portbits[jp.y];  // block-uniform: one scalar load per peer
-        if (w >= jp.z && w <= jp.w) pm[u] = a.PM[uint64_t(jp.x) * a.W + w];  // inside the peer's nonzero words
-      }
-    }
-    uint64_t undecided = 0;
+  for (uint32_t q = 0; q < nr; q++) {
+    const uint32_t i = a.reps[r0 + q];
+    const uint64_t* sb = sB + q * rowsz;
+    uint64_t allow[KC];
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
+      const uint32_t k = k0 + kk;
+      allow[kk] = 0;
+      if (k < a.K) {
+        if (!EGRESS) {  // the destination's slot: per representative (block-uniform)
+          const bool v = a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID;
+          valid[kk] = v ? wmask : 0ull;
+          du[kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
+        }
+        if (du[kk] >= 0) {
+          allow[kk] = expand_runs(sb + uint64_t(EGRESS ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wr);
+        } else if (EGRESS && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
+          const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
+          for (uint32_t d = 0; d < a.D; d++) allow[kk] |= expand_runs(sb + uint64_t(d) * a.EW, wr) & dm[uint64_t(d) * a.W];
+        }
+      }
+    }
+    // IP peers (ippeermatcher.go:43-50): per pod word through the PM rows, PEER_BATCH peers' words
+    // loaded at once (no panic in IDO builds: the OR is order-free; the undecided check only ends
+    // the walk early, once per batch)
+    const uint32_t m = a.cnt[i] ? a.ip_cnt[i] : 0u;
+    const uint4* il = a.ip_list + a.ip_off[i];
+    for (uint32_t x0 = 0; x0 < m; x0 += PEER_BATCH) {
+      uint64_t pm[PEER_BATCH];
+      uint32_t port[PEER_BATCH], pbits[PEER_BATCH];
 #pragma unroll
       for (uint32_t u = 0; u < PEER_BATCH; u++) {
-        if (!pm[u]) continue;
-        // egress: the descriptor varies per destination word, so the byte table would cost a
-        // vector load per (slot, peer); the bit row is a shift
-        if (EGRESS && a.portbits && du[kk] >= 0) allow[kk] |= ((pbits[u] >> du[kk]) & 1u) ? pm[u] : 0ull;
-        else allow[kk] |= pm[u] & port_mask<EGRESS>(a, a.portok + uint64_t(port[u]) * a.D, du[kk], k0 + kk, w);
+        pm[u] = 0;
+        port[u] = 0;
+        pbits[u] = 0;
+        if (x0 + u < m) {
+          const uint4 jp = il[x0 + u];
+          port[u] = jp.y;
+          if (EGRESS && a.portbits) pbits[u] = a.portbits[jp.y];  // block-uniform: one scalar load per peer
+          if (w >= jp.z && w <= jp.w) pm[u] = a.PM[uint64_t(jp.x) * a.W + w];  // inside the peer's nonzero words
+        }
       }
-      undecided |= valid[kk] & ~allow[kk];
-    }
-    if (!undecided) break;
-  }
+      uint64_t undecided = 0;
 #pragma unroll
-  for (int kk = 0; kk < KC; kk++) {
-    const uint32_t k = k0 + kk;
-    if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
+      for (int kk = 0; kk < KC; kk++) {
+#pragma unroll
+        for (uint32_t u = 0; u < PEER_BATCH; u++) {
+          if (!pm[u]) continue;
+          // egress: the descriptor varies per destination word, so the byte table would cost a
+          // vector load per (slot, peer); the bit row is a shift
+          if (EGRESS && a.portbits && du[kk] >= 0) allow[kk] |= ((pbits[u] >> du[kk]) & 1u) ? pm[u] : 0ull;
+          else allow[kk] |= pm[u] & port_mask<EGRESS>(a, a.portok + uint64_t(port[u]) * a.D, du[kk], k0 + kk, w);
+        }
+        undecided |= valid[kk] & ~allow[kk];
+      }
+      if (!undecided) break;
+    }
+#pragma unroll
+    for (int kk = 0; kk < KC; kk++) {
+      const uint32_t k = k0 + kk;
+      if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
+    }
   }
 }
 template <bool EGRESS, int KC>
@@ -1804,6 +1813,8 @@ struct cyc_ctx {
                         // directions' class rows.  A plane's emit grid fills every CU, so a second
                         // branch's front queued behind it would only run once that emit drains.
   bool graph_branches = true;  // cyc_set_option "graph_branches": ingress / egress as two graph branches
+  int64_t class_rpb_opt = 4;  // cyc_set_option "class_rpb": IDO class-row representatives per block
+                              // (config3 N=1 -1%: profiles/r01_class_rpb_ab.txt)
   int front_fused = 1;  // cyc_set_option "front_fused": the graphed front as 5 block-range-fused launches
                        // on one stream (enq_front_fused; IDO builds), 0 = the two-branch DAG
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
@@ -2352,6 +2363,13 @@ static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
 }
 
 // 6. class rows of direction d
+// IDO class rows: representatives per block (cyc_set_option "class_rpb"), as many as fit the
+// staged identity-set budget
+static uint32_t class_rpb(const cyc_ctx* c, size_t per_rep_lds) {
+  const uint64_t fit = std::max<uint64_t>(1, IDO_LDS_BYTES / std::max<size_t>(per_rep_lds, 1));
+  return uint32_t(std::max<int64_t>(1, std::min<int64_t>(c->class_rpb_opt, int64_t(fit))));
+}
+
 static RowArgs row_args(cyc_ctx* c, int d) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
@@ -2403,6 +2421,7 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   // the first kernel below empties the hash table for the next run (keys + reps; not the counter)
   ra.ht_clear = reinterpret_cast<uint32_t*>(dd.ht_key.p);
   ra.ht_clear_words = uint64_t(dd.ht_cap) * 3;
+  ra.rpb = 1;
   return ra;
 }
 
@@ -2430,8 +2449,10 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   } else if (ido_mode(c)) {
     // KC = kct job slots per thread (class_variant bit 0: 4, else 8)
     const uint32_t rows = d == 0 ? std::min<uint32_t>(kct, K) : D;
-    const unsigned gi = unsigned(uint64_t((W + 255) / 256) * ((K + kct - 1) / kct) * c->n_act[d]);
-    const size_t lds = size_t(rows) * ra.EW * 8;
+    const size_t per = size_t(rows) * ra.EW * 8;
+    ra.rpb = class_rpb(c, per);
+    const unsigned gi = unsigned(uint64_t((W + 255) / 256) * ((K + kct - 1) / kct) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
+    const size_t lds = per * ra.rpb;
     if (kct == 4) {
       if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, lds, st>>>(ra);
       else k_class_rows_ido<true, 4><<<gi, 256, lds, st>>>(ra);
@@ -2648,8 +2669,10 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fe.ra[d] = fd.ra[d];
     fe.ra[d].ht_clear_words = 0;
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + 3) / 4) + 3) / 4);
-    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + 3) / 4) * na);
-    lds = std::max<size_t>(lds, size_t(d == 0 ? std::min<uint32_t>(4, K) : D) * fd.ra[d].EW * 8);
+    const size_t per = size_t(d == 0 ? std::min<uint32_t>(4, K) : D) * fd.ra[d].EW * 8;
+    fe.ra[d].rpb = class_rpb(c, per);
+    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + 3) / 4) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
+    lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
   const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
   const bool bits = fa.nb[1] && D <= 32;
@@ -3215,6 +3238,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "class_rpb") {
+    if (value < 1 || value > 64) return fail(c, CYC_ERR_ARG, "class_rpb must be 1..64");
+    c->class_rpb_opt = value;
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "front_fused") {
     c->front_fused = int(value != 0);
     drop_graph(c);
@@ -3245,6 +3274,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "graph_branches") *value = c->graph_branches;
   else if (n == "graph_stagger") *value = c->graph_stagger;
   else if (n == "front_fused") *value = c->front_fused;
+  else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "emit_merged") *value = c->emit_merged;
   else if (n == "emit_interleave") *value = c->emit_interleave;
   else if (n == "emit_deal") *value = c->emit_deal;

@@ -349,19 +349,22 @@ def test_pod_words_from_identity_runs(gpu, seed):
     # (pod_words, graphs, class_variant, front_fused, member_wave): 4 or 8 job slots per thread,
     # graph and eager paths, the fused single-stream front and the two-branch DAG (replayed and
     # enqueued eagerly), membership by wave or thread, and the PM path
-    for mode, graphs, cv, fused, mw in ((1, 1, 3, 1, -1), (1, 1, 3, 1, 1), (1, 1, 3, 1, 0), (1, 1, 3, 0, -1),
-                                        (1, 2, 3, 1, 0), (1, 2, 3, 0, 1), (1, 0, 0, 1, -1), (1, 1, 1, 1, -1),
-                                        (0, 1, 3, 1, -1), (0, 0, 0, 1, -1)):
+    # and several class representatives per class-row block (class_rpb)
+    for mode, graphs, cv, fused, mw, rpb in ((1, 1, 3, 1, -1, 1), (1, 1, 3, 1, 1, 3), (1, 1, 3, 1, 0, 4),
+                                             (1, 1, 3, 0, -1, 2), (1, 2, 3, 1, 0, 1), (1, 2, 3, 0, 1, 5),
+                                             (1, 0, 0, 1, -1, 2), (1, 0, 3, 1, -1, 3), (1, 1, 1, 1, -1, 4),
+                                             (0, 1, 3, 1, -1, 1), (0, 0, 0, 1, -1, 1)):
         eng.set_option("pod_words", mode)
         eng.set_option("graphs", graphs)
         eng.set_option("class_variant_in", cv)
         eng.set_option("class_variant_eg", cv)
         eng.set_option("front_fused", fused)
         eng.set_option("member_wave", mw)
+        eng.set_option("class_rpb", rpb)
         assert eng.get_option("pod_words") == mode, "deployment-style words must allow the IDO path"
         for rep in range(2):  # the second run finds the hash tables the first one emptied
             assert_same(want, eng.run_host(), f"seed {seed} pod_words {mode} graphs {graphs} variant {cv} "
-                                              f"fused {fused} member_wave {mw} run {rep}")
+                                              f"fused {fused} member_wave {mw} rpb {rpb} run {rep}")
 
 
 @pytest.mark.parametrize("seed", range(6))
