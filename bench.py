@@ -207,12 +207,20 @@ def main():
             assembled = {"error": f"{type(e).__name__}: {e}"}
 
     # per-kernel device times from HIP events on the launch stream (separate, synchronised runs)
-    eng.set_option("graphs", 0)  # per-kernel events need the non-graph launch path
+    launch_mode, fused = eng.get_option("launch"), eng.get_option("front_fused_active")
+    front = ("fused front: 5 block-range launches on one stream (both directions' blocks in each)" if fused
+             else "front as a two-branch DAG (ingress / egress)")
+    how = ("one captured hipGraph replay" if launch_mode == 1 else "6 kernel launches enqueued eagerly on one stream" if fused
+           else "the step DAG enqueued eagerly on three streams")
+    launch_desc = (f"{how} "
+                   f"per step (cyc_set_option graphs={launch_mode}): {front}, then one emit launch writing both planes")
+    graphs = eng.get_option("graphs")
+    eng.set_option("graphs", 0)  # per-phase events need the eager launch path with events
     tm = []
     for _ in range(5):
         step()
         tm.append(eng.timings())
-    eng.set_option("graphs", 1)
+    eng.set_option("graphs", graphs)
     tm = np.array(tm)
     pipe_ms, emit_ms, rows_ms = (float(x) for x in tm.mean(axis=0))
     classes_in, classes_eg = eng.classes()
@@ -303,7 +311,7 @@ def main():
                 "launches_per_step": launches,
                 "fill_ceiling_GBs": fill_gbs,
             },
-            "launch": "one captured hipGraph per step (cyc_set_option graphs=1): shared front, ingress and egress fronts as two graph branches, then one emit launch writing both planes",
+            "launch": launch_desc,
             "pipeline_ms": {"total": pipe_ms, "emit": emit_ms, "class_rows": rows_ms, "front": pipe_ms - emit_ms - rows_ms},
         }
         if assembled is not None:

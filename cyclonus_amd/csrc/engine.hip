@@ -1795,8 +1795,11 @@ struct cyc_ctx {
   int64_t emit_blocks = 0;  // cyc_set_option "emit_blocks": persistent emit grid (0 = a block per row)
   int class_variant[2] = {3, 3};  // cyc_set_option "class_variant_in" / "_eg" (enq_class_rows;
                                   // defaults measured best on configs #3/#4: profiles/r01_class_sweep.txt)
-  int use_graphs = 1;  // cyc_set_option "graphs": 1 = graph replay, 2 = the same DAG enqueued eagerly
-                      // on three streams with events (no graph launch), 0 = eager on one stream
+  int use_graphs = -1;  // cyc_set_option "graphs": 1 = graph replay, 2 = the same DAG enqueued eagerly
+                       // on three streams with events (no graph launch), 0 = eager on one stream with
+                       // phase events, -1 = auto: 2 when the fused front applies (its 6 launches on
+                       // one stream start ~8 us sooner after the previous step's emit than a graph
+                       // replay: profiles/r01_front_fused_ab.txt), else 1
   int pod_rows = -1;   // cyc_set_option "pod_rows": pod-peer PM rows per pod directly (1), through
                        // identity outcomes and word runs (0), or -1 = direct when identities >= pods / 2
   int member_wave = -1;  // cyc_set_option "member_wave": membership with a wave (1) or a thread (0) per
@@ -2809,7 +2812,8 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
   if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
   if (c->order_lo != lo || c->order_hi != hi) drop_graph(c);  // range plan buffers are re-made
   ensure_range(c, lo, hi);
-  if (c->use_graphs == 2 && !pb.may_err) {
+  const int graphs = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);
+  if (graphs == 2 && !pb.may_err) {
     // the graph's DAG, enqueued directly: the caller's stream forks to two internal streams and
     // joins them back before the emit (events), without hipGraphLaunch's per-replay latency
     ensure_cap_streams(c);
@@ -2818,7 +2822,7 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     HIPCHK(hipEventRecord(c->ev[3], st));
     c->timed = true;
     c->timed_graph = true;
-  } else if (c->use_graphs && !pb.may_err) {
+  } else if (graphs && !pb.may_err) {
     // The whole pipeline as one hipGraph (captured once per output buffers / row range):
     // removes the host launch cost of ~16 launches per run (dominant on small problems).
     const void* key[5] = {d_in, d_eg, d_status, reinterpret_cast<void*>(lo), reinterpret_cast<void*>(hi)};
@@ -3255,7 +3259,7 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     return (int)CYC_OK;
   }
   if (std::string(name) == "graphs") {
-    if (value < 0 || value > 2) return fail(c, CYC_ERR_ARG, "graphs must be 0, 1 or 2");
+    if (value < -1 || value > 2) return fail(c, CYC_ERR_ARG, "graphs must be -1, 0, 1 or 2");
     c->use_graphs = int(value);
     drop_graph(c);
     return (int)CYC_OK;
@@ -3275,6 +3279,8 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "graph_stagger") *value = c->graph_stagger;
   else if (n == "front_fused") *value = c->front_fused;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
+  else if (n == "launch") *value = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);  // in effect
+  else if (n == "front_fused_active") *value = front_fused_ok(c) ? 1 : 0;
   else if (n == "emit_merged") *value = c->emit_merged;
   else if (n == "emit_interleave") *value = c->emit_interleave;
   else if (n == "emit_deal") *value = c->emit_deal;

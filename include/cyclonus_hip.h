@@ -140,9 +140,16 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  * pod-peer rows through identity outcomes and word runs (0) or per pod with one ballot per word (1);
  * "member_wave" -1 (default: auto = 1 for <= 4096 identities) / 0 / 1 computes target membership
  * with a thread (0) or a wave (1) per pod identity;
- * "graphs" (default 1) replays the pipeline as one captured hipGraph when the inputs cannot
- * panic (then cyc_last_timings reports only the whole-pipeline time); 2 enqueues the same
- * three-stream DAG eagerly (no graph), 0 runs every kernel in order on the caller's stream. */
+ * "front_fused" (default 1) runs the front (selectors .. class rows) as 5 launches on one stream,
+ * each a concatenation of independent block ranges of both directions (IDO builds with dense
+ * selectors and class_variant bit 0 set; otherwise the two-branch DAG); "class_rpb" (default 4,
+ * 1..64) class representatives per IDO class-row block;
+ * "graphs" -1 (default: auto = 2 when the fused front applies, else 1); 1 replays the pipeline as
+ * one captured hipGraph when the inputs cannot panic (then cyc_last_timings reports only the
+ * whole-pipeline time); 2 enqueues the same launches eagerly (the fused front on the caller's
+ * stream, or the three-stream DAG), 0 runs every kernel in order on the caller's stream with
+ * per-phase events.  cyc_get_option also reports "launch" (the graphs mode in effect) and
+ * "front_fused_active" (needs cyc_probe_prepare). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
 
 /* The setting in effect for a tuning knob of cyc_set_option; for "pod_words" the mode the
