@@ -95,8 +95,8 @@ def cpu_baseline(data, seconds: float, seed: int = 1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)  # GPU clocks settle after the host-side prepare
     ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4", "config5"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
