@@ -494,6 +494,22 @@ __device__ __forceinline__ void portok_blk(uint32_t M, uint32_t D, const DPortM*
 __global__ void k_portok(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents, const DDesc* descs,
                          uint8_t* __restrict__ portok) { portok_blk(M, D, pms, pents, descs, portok, blockIdx.x, gridDim.x); }
 
+// Port table rows as descriptor bit masks (D <= 32): the egress class rows test a peer's port
+// matcher against a per-word descriptor with a shift of one block-uniform word instead of a
+// vector byte load per (slot, peer).
+__device__ __forceinline__ void portbits_blk(uint32_t M, uint32_t D, const uint8_t* __restrict__ portok,
+                                             uint32_t* __restrict__ portbits, uint32_t bid_) {
+  const uint32_t m = bid_ * 256 + threadIdx.x;
+  if (m >= M) return;
+  uint32_t bits = 0;
+  for (uint32_t e = 0; e < D; e++) bits |= portok[uint64_t(m) * D + e] ? (1u << e) : 0u;
+  portbits[m] = bits;
+}
+__global__ __launch_bounds__(256) void k_portbits(uint32_t M, uint32_t D, const uint8_t* __restrict__ portok,
+                                                  uint32_t* __restrict__ portbits) {
+  portbits_blk(M, D, portok, portbits, blockIdx.x);
+}
+
 // Per (slot k, word w over pods-as-destinations): VALID bits, the word's common descriptor
 // (DESCW >= 0), none valid (-2) or mixed (-1), and per-descriptor masks DM for mixed words.
 __device__ __forceinline__ void slot_words_blk(uint32_t P, uint32_t K, uint32_t W, uint32_t D,
@@ -946,15 +962,17 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
       const uint32_t pend = tg.poff + tg.pcnt;
       for (uint32_t j0 = tg.poff; j0 < pend; j0 += PEER_BATCH) {
         uint64_t pm[PEER_BATCH];
-        uint32_t port[PEER_BATCH];
+        uint32_t port[PEER_BATCH], pbits[PEER_BATCH];
 #pragma unroll
         for (uint32_t u = 0; u < PEER_BATCH; u++) {
           const uint32_t j = j0 + u;
           pm[u] = 0;
           port[u] = 0;
+          pbits[u] = 0;
           if (j < pend) {
             const DPeer pr = a.peers[j];
             port[u] = pr.port;
+            if (EGRESS && a.portbits && pr.kind != 0) pbits[u] = a.portbits[pr.port];  // AllPeers: port = CYC_ALL
             if (pr.kind == 0) all = true;  // AllPeersMatcher: every valid cell allowed
             else if (pr.kind == 1) pm[u] = ~0ull;  // PortsForAllPeers
             else if (pr.kind == 2 || (w >= a.ip_rng[2 * j] && w <= ~a.ip_rng[2 * j + 1]))
@@ -966,7 +984,10 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
           if (!pm[u]) continue;
           const uint8_t* pok = a.portok + uint64_t(port[u]) * a.D;
 #pragma unroll
-          for (int kk = 0; kk < KC; kk++) allow[kk] |= pm[u] & port_mask<EGRESS>(a, pok, du[kk], k0 + kk, w);
+          for (int kk = 0; kk < KC; kk++) {
+            if (EGRESS && a.portbits && du[kk] >= 0) allow[kk] |= ((pbits[u] >> du[kk]) & 1u) ? pm[u] : 0ull;
+            else allow[kk] |= pm[u] & port_mask<EGRESS>(a, pok, du[kk], k0 + kk, w);
+          }
         }
       }
     }
@@ -1246,13 +1267,7 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
     }
     b -= f.nb[2 + d];
   }
-  // port table rows as descriptor bit masks (D <= 32), for the egress class rows
-  const uint32_t m = b * 256 + threadIdx.x;
-  if (b < f.nb[4] && m < f.M) {
-    uint32_t bits = 0;
-    for (uint32_t e = 0; e < f.D; e++) bits |= f.portok[uint64_t(m) * f.D + e] ? (1u << e) : 0u;
-    f.portbits[m] = bits;
-  }
+  if (b < f.nb[4]) portbits_blk(f.M, f.D, f.portok, f.portbits, b);  // for the egress class rows
 }
 
 struct FrontC {
@@ -1818,6 +1833,7 @@ struct cyc_ctx {
   bool graph_branches = true;  // cyc_set_option "graph_branches": ingress / egress as two graph branches
   int64_t class_rpb_opt = 4;  // cyc_set_option "class_rpb": IDO class-row representatives per block
                               // (config3 N=1 -1%: profiles/r01_class_rpb_ab.txt)
+  int port_bits = 1;  // cyc_set_option "port_bits": egress class rows test ports through descriptor bit rows
   int front_fused = 1;  // cyc_set_option "front_fused": the graphed front as 5 block-range-fused launches
                        // on one stream (enq_front_fused; IDO builds), 0 = the two-branch DAG
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
@@ -2243,6 +2259,9 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
 // targets, class rows and plane are disjoint from egress ones), so the two directions can run
 // as two independent branches: one direction's front hides under the other's HBM-bound emit.
 enum { COMMON_SELECTORS = 1, COMMON_PORTS = 2, COMMON_FILL = 4, COMMON_ALL = 7 };
+// Descriptor bit rows of the port table for the egress class rows (cyc_set_option "port_bits")
+static bool port_bits_on(const cyc_ctx* c) { return c->port_bits && std::max<size_t>(c->pb.descs.size(), 1) <= 32; }
+
 static void enq_common(cyc_ctx* c, hipStream_t st, int parts = COMMON_ALL) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
@@ -2265,6 +2284,8 @@ ports:
   if (M && pb.descs.size())
     k_portok<<<grid1(uint64_t(M) * D, 256), 256, 0, st>>>(M, D, c->pms.as<DPortM>(), c->pents.as<DPortEntry>(),
                                                           c->descs.as<DDesc>(), c->portok.as<uint8_t>());
+  if (M && pb.descs.size() && port_bits_on(c))
+    k_portbits<<<(M + 255) / 256, 256, 0, st>>>(M, D, c->portok.as<uint8_t>(), c->portbits.as<uint32_t>());
   // 4. per-slot destination words
   if (uint64_t(K) * W)
     k_slot_words<<<unsigned((uint64_t(K) * W + 3) / 4), 256, 0, st>>>(
@@ -2383,6 +2404,8 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.PM = c->PM.as<uint64_t>();
   ra.ER = c->ER.as<uint64_t>();
   ra.portok = c->portok.as<uint8_t>();
+  // egress: descriptor bit rows (k_portbits in enq_common; the fused front sets its own)
+  ra.portbits = d == 1 && port_bits_on(c) && pb.pms.size() && pb.descs.size() ? c->portbits.as<uint32_t>() : nullptr;
   ra.D = D;
   ra.n_ident = dd.n;
   ra.K = K;
@@ -2678,7 +2701,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
   const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
-  const bool bits = fa.nb[1] && D <= 32;
+  const bool bits = fa.nb[1] && port_bits_on(c);
   fb.M = M;
   fb.D = D;
   fb.portok = c->portok.as<uint8_t>();
@@ -3248,6 +3271,11 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "port_bits") {
+    c->port_bits = int(value != 0);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "front_fused") {
     c->front_fused = int(value != 0);
     drop_graph(c);
@@ -3278,6 +3306,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "graph_branches") *value = c->graph_branches;
   else if (n == "graph_stagger") *value = c->graph_stagger;
   else if (n == "front_fused") *value = c->front_fused;
+  else if (n == "port_bits") *value = c->port_bits;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "launch") *value = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);  // in effect
   else if (n == "front_fused_active") *value = front_fused_ok(c) ? 1 : 0;

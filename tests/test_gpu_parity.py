@@ -241,6 +241,7 @@ def test_graph_and_eager_paths_agree(gpu):
             eng.set_option("emit_interleave", (variant + seed) % 2)  # merged emit: planes alternate
             eng.set_option("emit_deal", int(variant in (10, 11) and seed % 2 == 0))  # wide emit: chunked XCD deal
             eng.set_option("emit_merged", int(variant != 5))
+            eng.set_option("port_bits", (variant + seed + cls) % 2)  # egress port test: bit rows / byte table
             eng.set_option("graphs", graphs)
             eng.set_option("graph_branches", branches)
             eng.set_option("emit_blocks", blocks)
@@ -361,6 +362,7 @@ def test_pod_words_from_identity_runs(gpu, seed):
         eng.set_option("front_fused", fused)
         eng.set_option("member_wave", mw)
         eng.set_option("class_rpb", rpb)
+        eng.set_option("port_bits", (seed + rpb) % 2)
         assert eng.get_option("pod_words") == mode, "deployment-style words must allow the IDO path"
         for rep in range(2):  # the second run finds the hash tables the first one emptied
             assert_same(want, eng.run_host(), f"seed {seed} pod_words {mode} graphs {graphs} variant {cv} "
