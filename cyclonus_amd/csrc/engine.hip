@@ -256,14 +256,14 @@ __global__ __launch_bounds__(256) void k_pod_rows(uint32_t Rp, uint32_t E, uint3
 // labelled apart, e.g. a `pod: <name>` label): then the identity-space outcomes cost as much as
 // this and the run expansion above loops over up to 64 runs per word.
 template <bool ERR>
-__global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P, uint32_t W,
+__device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uint32_t W,
                                                          const uint32_t* __restrict__ pod_peers,
                                                          const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres,
                                                          uint32_t L, const uint32_t* __restrict__ pod_eid,
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                          const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
-                                                         uint64_t* __restrict__ ER) {
-  const uint32_t lane = threadIdx.x & 63, gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                         uint64_t* __restrict__ ER, uint32_t bid_, uint32_t nblk_) {
+  const uint32_t lane = threadIdx.x & 63, gw = bid_ * 4 + (threadIdx.x >> 6);
   const uint32_t p = gw / W, w = gw - p * W;
   if (p >= Rp) return;
   const uint32_t j = pod_peers[p];
@@ -281,6 +281,14 @@ __global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P
     if (ERR) ER[uint64_t(j) * W + w] = er;
   }
 }
+template <bool ERR>
+__global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P, uint32_t W,
+                                                         const uint32_t* __restrict__ pod_peers,
+                                                         const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres,
+                                                         uint32_t L, const uint32_t* __restrict__ pod_eid,
+                                                         const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
+                                                         const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
+                                                         uint64_t* __restrict__ ER) { pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, PM, ER, blockIdx.x, gridDim.x); }
 
 // IP peers depend on each pod's own address: one wave per 64-pod word (one lane per pod).  A
 // block owns IPB_BATCH IP peers: their CIDR and except records (host-flattened, in evaluation
@@ -1059,20 +1067,22 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
 // surplus rows exit at once) — keeps the per-word body loop-free, which the egress variant
 // needs to stay at 3 waves/SIMD.
 template <bool EGRESS, bool ERR, int KC, bool LOOP>
-__global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
-  ht_clear_slice(a, blockIdx.x, gridDim.x);
+__device__ __forceinline__ void class_rows_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
+  ht_clear_slice(a, bid_, nblk_);
   const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
-  const uint32_t kc = (blockIdx.x / chunks) % nkc;
-  const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
+  const uint32_t kc = (bid_ / chunks) % nkc;
+  const uint32_t w = (bid_ % chunks) * 256 + threadIdx.x;
   if (w >= a.W) return;
   const uint32_t n_reps = *a.rep_cnt + 1u;
-  uint32_t r = blockIdx.x / (chunks * nkc);
+  uint32_t r = bid_ / (chunks * nkc);
   if (LOOP) {
     for (; r < n_reps; r += a.rep_blocks) class_row_word<EGRESS, ERR, KC>(a, a.reps[r], kc, w);
   } else if (r < n_reps) {
     class_row_word<EGRESS, ERR, KC>(a, a.reps[r], kc, w);
   }
 }
+template <bool EGRESS, bool ERR, int KC, bool LOOP>
+__global__ __launch_bounds__(256) void k_class_rows(RowArgs a) { class_rows_blk<EGRESS, ERR, KC, LOOP>(a, blockIdx.x, gridDim.x); }
 
 // Class rows from identity sets (IDO builds).  Block = (class representative, KC job slots,
 // 256 pod words); the representative's identity sets for those slots (ingress) or for every job
@@ -1232,6 +1242,9 @@ __global__ __launch_bounds__(256) void k_front_a(FrontA f) {
 
 struct FrontB {
   uint32_t nb[5];
+  uint32_t pod_direct;  // PM builds: segment 1 = pod-peer rows per pod (k_pod_rows_direct), else identity sets
+  uint32_t Rp;
+  const uint32_t *plist, *pod_eid;
   uint32_t M, D;
   const uint8_t* portok;
   uint32_t* portbits;
@@ -1255,8 +1268,12 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   uint32_t b = blockIdx.x;
   if (b < f.nb[0]) return ip_rows_fast_blk(f.Ri, f.P, f.W, f.tests, f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, b, f.nb[0]);
   b -= f.nb[0];
-  if (b < f.nb[1])
+  if (b < f.nb[1]) {
+    if (f.pod_direct)
+      return pod_rows_direct_blk<false>(f.Rp, f.P, f.W, f.plist, f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls, f.id_ls,
+                                        f.PM, nullptr, b, f.nb[1]);
     return peer_bits_blk(f.Ru, f.E, f.EW, f.pod_peers_u, f.peers, f.selres, f.L, f.id_ns, f.id_nsls, f.id_ls, f.idob, b, f.nb[1]);
+  }
   b -= f.nb[1];
 #pragma unroll
   for (int d = 0; d < 2; d++) {
@@ -1290,6 +1307,13 @@ __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   if (b < f.nb[0]) class_ident_blk<false, 4>(f.ra[0], b, f.nb[0]);
   else class_ident_blk<true, 4>(f.ra[1], b - f.nb[0], f.nb[1]);
 }
+// PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
+__global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
+  const uint32_t b = blockIdx.x;
+  if (b < f.nb[1]) class_rows_blk<true, false, 4, true>(f.ra[1], b, f.nb[1]);
+  else class_rows_blk<false, false, 4, true>(f.ra[0], b - f.nb[1], f.nb[0]);
+}
+
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
 // tail is made of the shorter ingress blocks
 __global__ __launch_bounds__(256) void k_front_e(FrontRows f) {
@@ -2608,10 +2632,14 @@ static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
 // defaults on configs #2-#4); returns false (nothing enqueued) otherwise.
 static bool front_fused_ok(const cyc_ctx* c) {
   const Problem& pb = c->pb;
-  if (!c->front_fused || !c->emit_merged || pb.may_err || !ido_mode(c)) return false;
+  if (!c->front_fused || !c->emit_merged || pb.may_err) return false;
   if (!pb.P || !pb.K || !pb.W) return false;
   if (uint64_t(c->n_sel) * pb.L && !c->dense_sel) return false;
-  return (c->class_variant[0] & 1) && (c->class_variant[1] & 1);  // KC = 4 both directions
+  if (ido_mode(c)) return (c->class_variant[0] & 1) && (c->class_variant[1] & 1);  // KC = 4 both directions
+  // PM builds: pod-peer rows per pod (one level) and k_class_rows<…, 4, LOOP> in both directions
+  const uint32_t E = c->dir[1].n, Rp = c->rp_off[2] - c->rp_off[0];
+  const bool direct = !(Rp && E) || (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= pb.P);
+  return direct && c->class_variant[0] == 3 && c->class_variant[1] == 3;
 }
 
 static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nullptr, hipEvent_t ev_rows = nullptr) {
@@ -2679,6 +2707,14 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.id_ls = c->dir[1].id_ls.as<uint32_t>();
   fb.idob = c->idob.as<uint64_t>() + uint64_t(u0) * EW;
   fb.nb[1] = (Rp && E) ? blocks((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4) : 0u;
+  const bool ido = ido_mode(c);
+  if (!ido) {  // PM builds: pod-peer rows per pod, a wave per (pod peer, 64-pod word)
+    fb.pod_direct = 1;
+    fb.Rp = Rp;
+    fb.plist = c->pod_peers.as<uint32_t>() + c->rp_off[0];
+    fb.pod_eid = c->dir[1].pod_id.as<uint32_t>();
+    fb.nb[1] = (Rp && E) ? blocks((uint64_t(Rp) * W + 3) / 4) : 0u;
+  }
   FrontC fc{};
   FrontRows fd{}, fe{};
   size_t lds = 0;
@@ -2692,6 +2728,10 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fc.nb[d] = na ? blocks((uint64_t(na) + 255) / 256) : 0u;
     if (!na) continue;
     fd.ra[d] = row_args(c, d);  // its blocks empty the direction's hash table for the next run
+    if (!ido) {  // PM builds: the class rows are launch D (k_front_d_pm), no identity sets
+      fd.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + 3) / 4) * fd.ra[d].rep_blocks);
+      continue;
+    }
     fe.ra[d] = fd.ra[d];
     fe.ra[d].ht_clear_words = 0;
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + 3) / 4) + 3) / 4);
@@ -2714,6 +2754,11 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (gb) k_front_b<<<unsigned(gb), 256, 0, st>>>(fb);
   if (fc.nb[0] + fc.nb[1]) k_front_c<<<fc.nb[0] + fc.nb[1], 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
+  if (!ido) {
+    if (fd.nb[0] + fd.nb[1]) k_front_d_pm<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
+    if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
+    return true;
+  }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
   if (fe.nb[0] + fe.nb[1]) k_front_e<<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
   if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
