@@ -208,10 +208,10 @@ def main():
 
     # per-kernel device times from HIP events on the launch stream (separate, synchronised runs)
     launch_mode, fused = eng.get_option("launch"), eng.get_option("front_fused_active")
-    front = ("fused front: 5 block-range launches on one stream (both directions' blocks in each)" if fused
+    front = ("fused front: 4-5 block-range launches on one stream, one per dependency level, both directions' blocks in each" if fused
              else "front as a two-branch DAG (ingress / egress)")
-    how = ("one captured hipGraph replay" if launch_mode == 1 else "6 kernel launches enqueued eagerly on one stream" if fused
-           else "the step DAG enqueued eagerly on three streams")
+    how = ("one captured hipGraph replay" if launch_mode == 1 else "the fused front's launches and the emit enqueued eagerly on one stream"
+           if fused else "the step DAG enqueued eagerly on three streams")
     launch_desc = (f"{how} "
                    f"per step (cyc_set_option graphs={launch_mode}): {front}, then one emit launch writing both planes")
     graphs = eng.get_option("graphs")
