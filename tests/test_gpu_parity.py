@@ -432,3 +432,39 @@ def test_graph_joins_without_status_or_rows(gpu):
             torch.cuda.synchronize()
             assert np.array_equal(d_in.cpu().numpy().view(np.uint64), want[1]), f"merged {merged}"
             assert np.array_equal(d_eg.cpu().numpy().view(np.uint64), want[2]), f"merged {merged}"
+
+
+def test_launch_modes_and_knobs(gpu):
+    """The default launch is the fused front enqueued eagerly (graphs auto = 2) when no panic is
+    possible and the graph of the two-branch DAG otherwise; tuning knobs round-trip and reject
+    out-of-range values; the fused front's results equal the oracle's, run after run, also when
+    switched off and on between runs (hash tables and IP spans are left clean for the next run)."""
+    pols, res, probes = random_problem(91_000, n_pods=150)
+    want = Oracle(pols, res).probe(probes)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    eng.prepare(probes)
+    assert eng.get_option("graphs") == -1
+    fused = not eng.shape["may_panic"]  # no-panic build: the fused front applies
+    assert eng.get_option("front_fused_active") == int(fused)
+    assert eng.get_option("launch") == (2 if fused else 1)
+    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("port_bits", 0), ("graphs", 1), ("graphs", -1)):
+        eng.set_option(name, v)
+        assert eng.get_option(name) == v
+        assert_same(want, eng.run_host(), f"{name}={v}")
+    eng.set_option("front_fused", 0)
+    assert eng.get_option("front_fused_active") == 0 and eng.get_option("launch") == 1
+    assert_same(want, eng.run_host(), "DAG graph")
+    eng.set_option("front_fused", 1)
+    assert_same(want, eng.run_host(), "fused again")
+    for name, v in (("class_rpb", 0), ("class_rpb", 65), ("graphs", 3)):
+        with pytest.raises(Exception):
+            eng.set_option(name, v)
+    # a build that may panic keeps the graph path (the panic walk needs the ordered peer rows)
+    pols_b, res_b, probes_b = random_problem(81_003, n_pods=60, bad=True)
+    eng_b = Engine(0).build_policies(pols_b).load_resources(res_b)
+    try:
+        eng_b.prepare(probes_b)
+    except CyclonusPanic:
+        return
+    if eng_b.shape.get("may_panic"):
+        assert eng_b.get_option("front_fused_active") == 0
