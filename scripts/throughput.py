@@ -1,7 +1,7 @@
 """Back-to-back step throughput (what bench.py times) under cyc_set_option settings, interleaved
 repetitions so box drift hits every setting alike.
 
-    python scripts/throughput.py config3 emit_variant=0,9 [steps=20] [reps=3] [shards=N] [init.<option>=v]
+    python scripts/throughput.py config3 emit_variant=0,9 [steps=20] [reps=3] [shards=N] [rank=R] [init.<option>=v]
 """
 import itertools
 import json
@@ -17,7 +17,7 @@ from cyclonus_amd import synth
 from cyclonus_amd.engine import Engine
 
 name = sys.argv[1]
-grid, steps, reps, shards = [], 20, 3, 1
+grid, steps, reps, shards, rank = [], 20, 3, 1, 0
 for a in sys.argv[2:]:
     k, v = a.split("=")
     if k == "steps":
@@ -26,6 +26,8 @@ for a in sys.argv[2:]:
         reps = int(v)
     elif k == "shards":
         shards = int(v)
+    elif k == "rank":  # the shard of this rank (default 0)
+        rank = int(v)
     else:
         grid.append((k, [int(x) for x in v.split(",")]))
 data = synth.CONFIGS[name]()
@@ -40,7 +42,7 @@ lo, hi = 0, P
 if shards > 1:
     from cyclonus_amd.shard import row_range
 
-    lo, hi = row_range(P, shards, 0)
+    lo, hi = row_range(P, shards, rank)
 rows = hi - lo
 d_in = torch.empty((rows, K, W), dtype=torch.int64, device="cuda")
 d_eg = torch.empty((rows, K, W), dtype=torch.int64, device="cuda")
