@@ -461,22 +461,22 @@ constexpr uint32_t IP_GROUP = 8;
 __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng, uint32_t bid_, uint32_t nblk_) {
+                                                      uint32_t* __restrict__ rng, uint32_t bid_, uint32_t nblk_, uint32_t grp = IP_GROUP) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t gw = bid_ * 4 + (threadIdx.x >> 6);
   const uint32_t chunks = (W + 63) / 64;
-  const uint32_t r0 = (gw / chunks) * IP_GROUP;
+  const uint32_t r0 = (gw / chunks) * grp;
   if (r0 >= Ri) return;
   const uint32_t w = (gw % chunks) * 64 + lane;
   const bool valid = w < W;
   DWordIP wd{};
   if (valid) wd = words[w];
-  for (uint32_t r = r0; r < min(Ri, r0 + IP_GROUP); r++) ip_row_word(tests[r], ip_ex, pod_ip, wd, valid, w, gw % chunks, P, W, lane, PM, rng);
+  for (uint32_t r = r0; r < min(Ri, r0 + grp); r++) ip_row_word(tests[r], ip_ex, pod_ip, wd, valid, w, gw % chunks, P, W, lane, PM, rng);
 }
 __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng) { ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, blockIdx.x, gridDim.x); }
+                                                      uint32_t* __restrict__ rng, uint32_t grp) { ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, blockIdx.x, gridDim.x, grp); }
 
 // PortMatcher.Allows(ResolvedPort, ResolvedPortName, Protocol) — portmatcher.go:10-92, 190-199.
 __device__ __forceinline__ void portok_blk(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents, const DDesc* descs,
@@ -1242,6 +1242,7 @@ __global__ __launch_bounds__(256) void k_front_a(FrontA f) {
 
 struct FrontB {
   uint32_t nb[5];
+  uint32_t ip_grp;      // IP rows: peers per wave
   uint32_t pod_direct;  // PM builds: segment 1 = pod-peer rows per pod (k_pod_rows_direct), else identity sets
   uint32_t Rp;
   const uint32_t *plist, *pod_eid;
@@ -1266,7 +1267,7 @@ struct FrontB {
 };
 __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   uint32_t b = blockIdx.x;
-  if (b < f.nb[0]) return ip_rows_fast_blk(f.Ri, f.P, f.W, f.tests, f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, b, f.nb[0]);
+  if (b < f.nb[0]) return ip_rows_fast_blk(f.Ri, f.P, f.W, f.tests, f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, b, f.nb[0], f.ip_grp);
   b -= f.nb[0];
   if (b < f.nb[1]) {
     if (f.pod_direct)
@@ -1857,6 +1858,7 @@ struct cyc_ctx {
   bool graph_branches = true;  // cyc_set_option "graph_branches": ingress / egress as two graph branches
   int64_t class_rpb_opt = 4;  // cyc_set_option "class_rpb": IDO class-row representatives per block
                               // (config3 N=1 -1%: profiles/r01_class_rpb_ab.txt)
+  uint32_t ip_group = IP_GROUP;  // cyc_set_option "ip_group": IP-peer tests per wave in the IP rows
   int port_bits = 1;  // cyc_set_option "port_bits": egress class rows test ports through descriptor bit rows
   int front_fused = 1;  // cyc_set_option "front_fused": the graphed front as 5 block-range-fused launches
                        // on one stream (enq_front_fused; IDO builds), 0 = the two-branch DAG
@@ -2377,9 +2379,10 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
       k_ip_rows<true><<<g, 256, 0, st>>>(Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->PM.as<uint64_t>(),
                                          c->ER.as<uint64_t>(), bat);
     } else {
-      k_ip_rows_fast<<<unsigned((uint64_t((W + 63) / 64) * ((Ri + IP_GROUP - 1) / IP_GROUP) + 3) / 4), 256, 0, st>>>(
+      const uint32_t grp = c->ip_group;
+      k_ip_rows_fast<<<unsigned((uint64_t((W + 63) / 64) * ((Ri + grp - 1) / grp) + 3) / 4), 256, 0, st>>>(
           Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>(),
-          c->ip_rng.as<uint32_t>());
+          c->ip_rng.as<uint32_t>(), grp);
     }
   }
 }
@@ -2693,7 +2696,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.words = c->ip_words.as<DWordIP>();
   fb.PM = c->PM.as<uint64_t>();
   fb.rng = c->ip_rng.as<uint32_t>();
-  fb.nb[0] = Ri ? blocks((uint64_t((W + 63) / 64) * ((Ri + IP_GROUP - 1) / IP_GROUP) + 3) / 4) : 0u;
+  fb.ip_grp = c->ip_group;
+  fb.nb[0] = Ri ? blocks((uint64_t((W + 63) / 64) * ((Ri + fb.ip_grp - 1) / fb.ip_grp) + 3) / 4) : 0u;
   const uint32_t Rp = c->rp_off[2] - c->rp_off[0], u0 = c->rpu_off[0], Ru = c->rpu_off[2] - u0;
   fb.Ru = Ru;
   fb.E = E;
@@ -3316,6 +3320,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     drop_graph(c);
     return (int)CYC_OK;
   }
+  if (std::string(name) == "ip_group") {
+    if (value < 1 || value > 64) return fail(c, CYC_ERR_ARG, "ip_group must be 1..64");
+    c->ip_group = uint32_t(value);
+    drop_graph(c);
+    return (int)CYC_OK;
+  }
   if (std::string(name) == "port_bits") {
     c->port_bits = int(value != 0);
     drop_graph(c);
@@ -3352,6 +3362,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "graph_stagger") *value = c->graph_stagger;
   else if (n == "front_fused") *value = c->front_fused;
   else if (n == "port_bits") *value = c->port_bits;
+  else if (n == "ip_group") *value = c->ip_group;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "launch") *value = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);  // in effect
   else if (n == "front_fused_active") *value = front_fused_ok(c) ? 1 : 0;

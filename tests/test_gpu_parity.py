@@ -242,6 +242,7 @@ def test_graph_and_eager_paths_agree(gpu):
             eng.set_option("emit_deal", int(variant in (10, 11) and seed % 2 == 0))  # wide emit: chunked XCD deal
             eng.set_option("emit_merged", int(variant != 5))
             eng.set_option("port_bits", (variant + seed + cls) % 2)  # egress port test: bit rows / byte table
+            eng.set_option("ip_group", (1, 3, 8)[(variant + seed) % 3])  # IP rows: tests per wave
             eng.set_option("graphs", graphs)
             eng.set_option("graph_branches", branches)
             eng.set_option("emit_blocks", blocks)
