@@ -143,7 +143,9 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  * "front_fused" (default 1) runs the front (selectors .. class rows) as 5 launches on one stream,
  * each a concatenation of independent block ranges of both directions (IDO builds with dense
  * selectors and class_variant bit 0 set; otherwise the two-branch DAG); "class_rpb" (default 4,
- * 1..64) class representatives per IDO class-row block;
+ * 1..64) class representatives per IDO class-row block; "port_bits" (default 1) has the egress
+ * class rows test port matchers through per-matcher descriptor bit rows (<= 32 descriptors);
+ * "ip_group" (default 8, 1..64) IP-peer tests per wave in the IP rows;
  * "graphs" -1 (default: auto = 2 when the fused front applies, else 1); 1 replays the pipeline as
  * one captured hipGraph when the inputs cannot panic (then cyc_last_timings reports only the
  * whole-pipeline time); 2 enqueues the same launches eagerly (the fused front on the caller's
