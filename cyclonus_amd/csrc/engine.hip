@@ -1317,9 +1317,10 @@ __global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
 // tail is made of the shorter ingress blocks
+template <int KCE>  // egress job slots per thread (class_variant_eg bit 0: 4, else 8)
 __global__ __launch_bounds__(256) void k_front_e(FrontRows f) {
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_ido_blk<true, 4>(f.ra[1], b, f.nb[1]);
+  if (b < f.nb[1]) class_rows_ido_blk<true, KCE>(f.ra[1], b, f.nb[1]);
   else class_rows_ido_blk<false, 4>(f.ra[0], b - f.nb[1], f.nb[0]);
 }
 
@@ -2638,7 +2639,7 @@ static bool front_fused_ok(const cyc_ctx* c) {
   if (!c->front_fused || !c->emit_merged || pb.may_err) return false;
   if (!pb.P || !pb.K || !pb.W) return false;
   if (uint64_t(c->n_sel) * pb.L && !c->dense_sel) return false;
-  if (ido_mode(c)) return (c->class_variant[0] & 1) && (c->class_variant[1] & 1);  // KC = 4 both directions
+  if (ido_mode(c)) return (c->class_variant[0] & 1) != 0;  // KC = 4 ingress; egress 4 or 8 (k_front_e<KCE>)
   // PM builds: pod-peer rows per pod (one level) and k_class_rows<…, 4, LOOP> in both directions
   const uint32_t E = c->dir[1].n, Rp = c->rp_off[2] - c->rp_off[0];
   const bool direct = !(Rp && E) || (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= pb.P);
@@ -2741,7 +2742,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + 3) / 4) + 3) / 4);
     const size_t per = size_t(d == 0 ? std::min<uint32_t>(4, K) : D) * fd.ra[d].EW * 8;
     fe.ra[d].rpb = class_rpb(c, per);
-    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + 3) / 4) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
+    const uint32_t kcd = (d == 1 && !(c->class_variant[1] & 1)) ? 8u : 4u;
+    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + kcd - 1) / kcd) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
     lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
   const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
@@ -2764,7 +2766,10 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     return true;
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
-  if (fe.nb[0] + fe.nb[1]) k_front_e<<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
+  if (fe.nb[0] + fe.nb[1]) {
+    if (c->class_variant[1] & 1) k_front_e<4><<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
+    else k_front_e<8><<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
+  }
   if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
   return true;
 }

@@ -359,7 +359,7 @@ def test_pod_words_from_identity_runs(gpu, seed):
         eng.set_option("pod_words", mode)
         eng.set_option("graphs", graphs)
         eng.set_option("class_variant_in", cv)
-        eng.set_option("class_variant_eg", cv)
+        eng.set_option("class_variant_eg", 2 if (fused and rpb == 3) else cv)  # 2: fused egress rows, 8 slots per thread
         eng.set_option("front_fused", fused)
         eng.set_option("member_wave", mw)
         eng.set_option("class_rpb", rpb)
