@@ -20,6 +20,11 @@ PANIC_CODES = (ERR_INVALID_POLICY, ERR_PANIC_IP, ERR_PANIC_CIDR, ERR_PANIC_SELEC
 # cyc_job_status
 JOB_NONE, JOB_VALID, JOB_BAD_NAMED_PORT, JOB_BAD_PORT_PROTOCOL = 0, 1, 2, 3
 
+# cyc_connectivity (probe.Connectivity in AllConnectivity order, connectivity.go:16-23)
+CONN_UNKNOWN, CONN_CHECK_FAILED, CONN_INVALID_NAMED_PORT, CONN_INVALID_PORT_PROTOCOL, CONN_BLOCKED, CONN_ALLOWED = range(6)
+CONN_NO_JOB = 255
+CONNECTIVITY = ("unknown", "checkfailed", "invalidnamedport", "invalidportprotocol", "blocked", "allowed")
+
 EXPORTS = [
     "cyc_ctx_create",
     "cyc_ctx_destroy",
@@ -39,6 +44,12 @@ EXPORTS = [
     "cyc_query_traffic",
     "cyc_query_traffic_targets",
     "cyc_query_targets",
+    "cyc_table_run",
+    "cyc_table_wrap",
+    "cyc_table_cells",
+    "cyc_table_shape",
+    "cyc_table_error",
+    "cyc_table_destroy",
 ]
 
 
@@ -96,6 +107,14 @@ def lib():
         L.cyc_query_traffic.argtypes = [vp, cp, sz, vp, i64]
         L.cyc_query_traffic_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]
         L.cyc_query_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]
+        L.cyc_table_run.argtypes = [vp, i64, i64, ctypes.POINTER(vp)]
+        L.cyc_table_wrap.argtypes = [vp, vp, vp, vp, i64, i64, ctypes.POINTER(vp)]
+        L.cyc_table_cells.argtypes = [vp, i64, i64, i64, i64, i64, i64, vp, vp, vp]
+        L.cyc_table_shape.argtypes = [vp, ctypes.POINTER(i64), i]
+        L.cyc_table_error.argtypes = [vp]
+        L.cyc_table_error.restype = cp
+        L.cyc_table_destroy.argtypes = [vp]
+        L.cyc_table_destroy.restype = None
         _lib = L
     return _lib
 

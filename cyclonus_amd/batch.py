@@ -8,6 +8,13 @@ their primary keys and the exact-namespace peer matchers then never cross blocks
 namespace / pod label selectors and IPBlocks can match pods of other blocks only in cross-block
 cells, which are computed but never read.  The probe configs of all problems become slot ranges
 of the combined problem; each block reads the slots of its own config.
+
+Panics are the exception: the reference panics on the FIRST panicking job of a problem's own table
+(ippeermatcher.go:46-48, labelselector.go:57), but a combined problem also evaluates cross-block
+cells, so one block's unparsable pod IP met by another block's IPBlock peer would panic the whole
+batch although neither problem panics alone.  `run` therefore answers every block from the batched
+pass when that pass does not panic (then no cell panicked, intra-block cells included), and
+otherwise re-runs each problem stand-alone, so each block gets its own table or its own panic.
 """
 from __future__ import annotations
 
@@ -86,3 +93,31 @@ class Batch:
             return np.packbits(pad, axis=2, bitorder="little").view(np.uint64)
 
         return (status[o : o + s, lo:hi].copy(), plane(ingress[o : o + s, lo:hi]), plane(egress[o : o + s, lo:hi]))
+
+    def run(self, engine):
+        """Per block: (status, in, eg) of its own table, or the CyclonusPanic its stand-alone run raises."""
+        from ._lib import CyclonusPanic
+
+        try:
+            engine.build_policies(json.dumps(self.policies)).load_resources(json.dumps(self.resources))
+            engine.prepare(self.probes)
+            st, ing, eg = engine.run_host()
+            out = []
+            for b, p in enumerate(self.problems):
+                t = self.extract(b, st, ing, eg)
+                if p["probe"].get("AllAvailable"):  # the stand-alone table has its own pods' max containers
+                    k = max((len(q.get("Containers") or []) for q in p["resources"].get("Pods") or []), default=0)
+                    t = (t[0][:, :k], t[1][:, :k], t[2][:, :k])
+                out.append(t)
+            return out
+        except CyclonusPanic:
+            pass
+        out = []
+        for p in self.problems:  # a cell of the combined problem panicked: each problem on its own
+            try:
+                engine.build_policies(json.dumps(p["policies"])).load_resources(json.dumps(p["resources"]))
+                engine.prepare([p["probe"]])
+                out.append(engine.run_host())
+            except CyclonusPanic as e:
+                out.append(e)
+        return out

@@ -38,6 +38,55 @@ def _run(cmd):
     subprocess.run(cmd, check=True)
 
 
+DRIVER_SRC = os.path.join(ROOT, "tests", "native", "capi_driver.cpp")
+DRIVER = os.path.join(ROOT, "tests", "native", "capi_driver")
+ASAN_DIR = os.path.join(BUILD, "asan")
+ASAN_LIB = os.path.join(ASAN_DIR, "libcyclonus_hip.so")
+SAN = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
+
+
+def build_driver(force: bool = False) -> str:
+    """The C++ C-ABI driver (tests/native/capi_driver.cpp), linked against the in-tree library."""
+    if force or _newer(DRIVER, [DRIVER_SRC, OUT, os.path.join(INCLUDE, "cyclonus_hip.h")]):
+        _run(["g++", "-O2", "-std=c++17", "-I", INCLUDE, DRIVER_SRC, "-o", DRIVER, "-L", PKG, "-lcyclonus_hip",
+              f"-Wl,-rpath,{PKG}"])
+    return DRIVER
+
+
+def asan_runtime() -> str:
+    """clang's ASan runtime (LD_PRELOAD it to load the sanitized library into an unsanitized python)."""
+    import glob
+
+    hits = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    if not hits:
+        raise FileNotFoundError("libclang_rt.asan-x86_64.so not found under /opt/rocm/lib/llvm")
+    return hits[-1]
+
+
+def build_asan(force: bool = False) -> str:
+    """ASan + UBSan build of the host side (host.cpp, cjson.hpp, the C ABI in engine.hip) for CPU
+    tests in this container: CYC_HIP_LIB=<this> LD_PRELOAD=asan_runtime() python -m pytest ...
+    The sanitizers apply to host code only (-Xarch_host); device code is compiled as usual."""
+    os.makedirs(ASAN_DIR, exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "cyclonus_hip.h")]
+    common = ["-O1", "-g", "-std=c++17", "-fPIC", "-I", CSRC, "-I", INCLUDE]
+    host_san = [f for x in SAN for f in ("-Xarch_host", x)]
+    objs = []
+    for s in SOURCES_CPP:
+        src, obj = os.path.join(CSRC, s), os.path.join(ASAN_DIR, s + ".o")
+        if force or _newer(obj, [src] + hdrs):
+            _run([HIPCC, "-x", "c++", *common, *SAN, "-c", src, "-o", obj])
+        objs.append(obj)
+    for s in SOURCES_HIP:
+        src, obj = os.path.join(CSRC, s), os.path.join(ASAN_DIR, s + ".o")
+        if force or _newer(obj, [src] + hdrs):
+            _run([HIPCC, f"--offload-arch={ARCH}", *common, *host_san, "-munsafe-fp-atomics", "-c", src, "-o", obj])
+        objs.append(obj)
+    if force or _newer(ASAN_LIB, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *host_san, "-shared-libsan", "-o", ASAN_LIB, *objs])
+    return ASAN_LIB
+
+
 def build(verbose: bool = True, force: bool = False) -> str:
     os.makedirs(BUILD, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "cyclonus_hip.h")]
@@ -57,8 +106,11 @@ def build(verbose: bool = True, force: bool = False) -> str:
         objs.append(obj)
     if force or _newer(OUT, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs])
+    build_driver(force)
     return OUT
 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    if "--asan" in sys.argv:
+        build_asan(force="--force" in sys.argv)

@@ -26,11 +26,12 @@ struct Node {
   bool null() const { return t == Null; }
   bool is_arr() const { return t == Arr; }
   bool is_obj() const { return t == Obj; }
-  // encoding/json field lookup: exact key first, then ASCII case-insensitive
+  // encoding/json struct-field lookup: every key equal to the field name exactly or ASCII
+  // case-insensitively decodes into that field, in document order, so the LAST such key wins
+  // ({"Namespace":"a","namespace":"b"} gives "b", as Go's decoder does).
   const Node* find(std::string_view k) const {
     if (t != Obj) return nullptr;
-    for (auto& kv : o)
-      if (kv.first == k) return &kv.second;
+    const Node* hit = nullptr;
     for (auto& kv : o) {
       if (kv.first.size() != k.size()) continue;
       size_t i = 0;
@@ -40,9 +41,9 @@ struct Node {
         if (y >= 'A' && y <= 'Z') y += 32;
         if (x != y) break;
       }
-      if (i == k.size()) return &kv.second;
+      if (i == k.size()) hit = &kv.second;
     }
-    return nullptr;
+    return hit;
   }
   const Node* val(std::string_view k) const {  // non-null member or nullptr
     const Node* n = find(k);
@@ -75,6 +76,10 @@ class Reader {
  private:
   const char* p_;
   size_t n_, i_ = 0;
+  int depth_ = 0;  // nesting of the value being read
+  // encoding/json's scanner refuses documents nested deeper than 10000 (Go 1.15+ maxNestingDepth);
+  // the same bound keeps this recursive reader's stack use finite on hostile input
+  static constexpr int kMaxDepth = 10000;
   [[noreturn]] void fail(const char* m) {
     throw std::runtime_error(std::string("json: ") + m + " at byte " + std::to_string(i_));
   }
@@ -89,10 +94,24 @@ class Reader {
     }
     return false;
   }
+  struct Nest {  // depth guard for one nested object / array
+    int& d;
+    explicit Nest(Reader& r) : d(r.depth_) {
+      if (++d > kMaxDepth) r.fail("exceeded max depth");
+    }
+    ~Nest() { --d; }
+  };
   Node any() {
-    Node v;
     char c = peek();
-    if (c == '{') {
+    if (c == '{' || c == '[') {
+      Nest guard(*this);
+      return c == '{' ? object() : array();
+    }
+    return scalar(c);
+  }
+  Node object() {
+    Node v;
+    {
       v.t = Node::Obj;
       i_++;
       sp();
@@ -121,7 +140,10 @@ class Reader {
         fail("expected ',' or '}'");
       }
     }
-    if (c == '[') {
+  }
+  Node array() {
+    Node v;
+    {
       v.t = Node::Arr;
       i_++;
       sp();
@@ -144,6 +166,9 @@ class Reader {
         fail("expected ',' or ']'");
       }
     }
+  }
+  Node scalar(char c) {
+    Node v;
     if (c == '"') {
       v.t = Node::Str;
       v.s = string();

@@ -395,7 +395,7 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
 // rng[2 * peer + 1] (~last word), both atomicMin'd from 0xFFFFFFFF: CIDRs are address ranges and
 // pods of a namespace have neighbouring addresses, so a peer's row is mostly zero words the
 // class rows can skip without loading them.
-__device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
+__device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
                                             const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
                                             uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng) {
   bool uniform = true;
@@ -409,7 +409,7 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* __res
       else if (pos == 1) {
         res = fm;
         for (uint32_t e = 0; e < t.excnt; e++) {
-          const DCidr x = ip_ex[t.exoff + e];
+          const DCidr x = ex[e];
           if (x.fam != t.cidr.fam) continue;
           uint32_t xp = v4 ? span_vs_cidr4(wd.min4, wd.max4, x) : span_vs_cidr6(wd.min6, wd.max6, x);
           if (xp == 0) continue;
@@ -437,7 +437,7 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* __res
       if (cidr_contains(t.cidr, ip)) {
         o = 1;
         for (uint32_t e = 0; e < t.excnt; e++)
-          if (cidr_contains(ip_ex[t.exoff + e], ip)) {
+          if (cidr_contains(ex[e], ip)) {
             o = 0;
             break;
           }
@@ -456,27 +456,47 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* __res
   }
 }
 
-// A wave handles IP_GROUP peers over its 64 words: the words' [min, max] records are loaded once.
-constexpr uint32_t IP_GROUP = 8;
+// A block handles one group of `grp` IP peers over 4 chunks of 64 words (a wave per chunk, lane =
+// word): the group's tests and their except records are staged into LDS once (one coalesced load
+// per block, instead of a chain of dependent scalar loads per peer and except), and each wave loads
+// its words' [min, max] records once for the whole group.
+constexpr uint32_t IP_GROUP = 8, IP_GROUP_MAX = 64, IP_EX_LDS = 256;
 __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
                                                       uint32_t* __restrict__ rng, uint32_t bid_, uint32_t nblk_, uint32_t grp = IP_GROUP) {
+  __shared__ DIPTest s_t[IP_GROUP_MAX];
+  __shared__ DCidr s_ex[IP_EX_LDS];
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t gw = bid_ * 4 + (threadIdx.x >> 6);
-  const uint32_t chunks = (W + 63) / 64;
-  const uint32_t r0 = (gw / chunks) * grp;
-  if (r0 >= Ri) return;
-  const uint32_t w = (gw % chunks) * 64 + lane;
+  const uint32_t chunks = (W + 63) / 64, cb = (chunks + 3) / 4;
+  const uint32_t r0 = (bid_ / cb) * grp;
+  if (r0 >= Ri) return;  // whole block
+  const uint32_t nr = min(Ri - r0, grp), chunk = (bid_ % cb) * 4 + (threadIdx.x >> 6);
+  const uint32_t ex0 = tests[r0].exoff, nex = tests[r0 + nr - 1].exoff + tests[r0 + nr - 1].excnt - ex0;
+  const bool ex_lds = nex <= IP_EX_LDS;
+  for (uint32_t x = threadIdx.x; x < nr; x += blockDim.x) s_t[x] = tests[r0 + x];
+  if (ex_lds)
+    for (uint32_t x = threadIdx.x; x < nex; x += blockDim.x) s_ex[x] = ip_ex[ex0 + x];
+  __syncthreads();
+  if (chunk >= chunks) return;
+  const uint32_t w = chunk * 64 + lane;
   const bool valid = w < W;
   DWordIP wd{};
   if (valid) wd = words[w];
-  for (uint32_t r = r0; r < min(Ri, r0 + grp); r++) ip_row_word(tests[r], ip_ex, pod_ip, wd, valid, w, gw % chunks, P, W, lane, PM, rng);
+  for (uint32_t r = 0; r < nr; r++) {
+    const DIPTest t = s_t[r];
+    ip_row_word(t, ex_lds ? s_ex + (t.exoff - ex0) : ip_ex + t.exoff, pod_ip, wd, valid, w, chunk, P, W, lane, PM, rng);
+  }
 }
 __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
                                                       uint32_t* __restrict__ rng, uint32_t grp) { ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, blockIdx.x, gridDim.x, grp); }
+
+// Grid of k_ip_rows_fast / the IP-row range of k_front_b: peer groups x blocks of 4 word chunks.
+__host__ __device__ inline uint64_t ip_rows_blocks(uint32_t Ri, uint32_t W, uint32_t grp) {
+  return uint64_t((Ri + grp - 1) / grp) * (((W + 63) / 64 + 3) / 4);
+}
 
 // PortMatcher.Allows(ResolvedPort, ResolvedPortName, Protocol) — portmatcher.go:10-92, 190-199.
 __device__ __forceinline__ void portok_blk(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents, const DDesc* descs,
@@ -1084,6 +1104,173 @@ __device__ __forceinline__ void class_rows_blk(RowArgs a, uint32_t bid_, uint32_
 template <bool EGRESS, bool ERR, int KC, bool LOOP>
 __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) { class_rows_blk<EGRESS, ERR, KC, LOOP>(a, blockIdx.x, gridDim.x); }
 
+// Class rows of PM builds without a panic.  Block = class representative (blocks stride over
+// them).  The block first flattens the class's peers cooperatively into LDS — lanes over its
+// targets, then over their peers: (PM row, nonzero word span, port test pre-resolved as a bit row:
+// ingress = one bit per job slot of this representative, egress = the port matcher's descriptor
+// bits) — so the long chain of dependent loads (membership list -> target -> peer -> word span)
+// runs once per class with every lane's loads in flight, not once per pod word.  Then each
+// (slot chunk, pod word) item ORs its peers' PM words, PL_BATCH loads in flight.  Without a panic
+// the verdict is that OR (target.go:29-36 short-circuits only to save work); an AllPeersMatcher
+// (peermatcher.go:18) allows every valid cell; no matching target allows (policy.go:158-160).
+// Lists longer than the LDS part spill into the identity's ip_list slot (sized for every peer of
+// its namespace's targets).
+constexpr uint32_t PL_LDS = 512, PL_TGT = 128, PL_BATCH = 8;
+constexpr uint32_t PL_SKIP = 0xFFFFFFFEu, PL_ONES = 0xFFFFFFFFu;  // entry rows: zero row / PortsForAllPeers
+struct PlShared {  // one per block, shared by both directions' instantiations of a fused launch
+  uint4 e[PL_LDS];        // (row, port matcher, first word, last word)
+  uint32_t bits[PL_LDS];  // port test bits
+  uint32_t pre[PL_TGT + 1], poff[PL_TGT];
+  uint32_t all;
+};
+
+template <bool EGRESS>
+__device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
+  constexpr int KC = 4;
+  ht_clear_slice(a, bid_, nblk_);
+  const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC, items = nkc * a.W;
+  const bool kbits = EGRESS ? a.portbits != nullptr : a.K <= 32;
+  for (uint32_t r = bid_; r < n_reps; r += nblk_) {
+    const uint32_t i = a.reps[r];
+    const uint32_t nt = a.cnt[i];
+    const uint32_t* lst = a.list + a.list_off[i];
+    uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
+    if (threadIdx.x == 0) sh.all = 0;
+    uint32_t m = 0;
+    for (uint32_t t0 = 0; t0 < nt; t0 += PL_TGT) {  // targets in chunks: offsets, counts, prefix sums
+      const uint32_t ntc = min(PL_TGT, nt - t0);
+      for (uint32_t t = threadIdx.x; t < ntc; t += blockDim.x) {
+        const DTarget tg = a.tgt[lst[t0 + t]];
+        sh.poff[t] = tg.poff;
+        sh.pre[t + 1] = tg.pcnt;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        sh.pre[0] = 0;
+        for (uint32_t t = 0; t < ntc; t++) sh.pre[t + 1] = acc += sh.pre[t + 1];
+      }
+      __syncthreads();
+      const uint32_t mc = sh.pre[ntc];
+      for (uint32_t e = threadIdx.x; e < mc; e += blockDim.x) {  // the peers, one per lane
+        uint32_t lo = 0, hi = ntc;  // target of peer e: pre[lo] <= e < pre[lo + 1]
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sh.pre[mid] <= e) lo = mid;
+          else hi = mid;
+        }
+        const uint32_t j = sh.poff[lo] + (e - sh.pre[lo]);
+        const DPeer pr = a.peers[j];
+        uint4 en = make_uint4(PL_SKIP, 0u, 1u, 0u);
+        uint32_t bits = 0;
+        if (pr.kind == 0) {
+          sh.all = 1;  // AllPeersMatcher
+        } else {
+          en = make_uint4(pr.kind == 1 ? PL_ONES : j, pr.port, 0u, a.W - 1);
+          if (pr.kind == 3) {
+            en.z = a.ip_rng[2 * j];
+            en.w = ~a.ip_rng[2 * j + 1];
+            if (en.z == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
+          }
+          if (EGRESS) {
+            if (a.portbits) bits = a.portbits[pr.port];
+          } else if (a.K <= 32) {
+            for (uint32_t k = 0; k < a.K; k++) {
+              const uint64_t ik = uint64_t(i) * a.K + k;
+              if (a.id_status[ik] == CYC_JOB_VALID && a.portok[uint64_t(pr.port) * a.D + a.id_desc[ik]]) bits |= 1u << k;
+            }
+          }
+          en.y = EGRESS || a.K > 32 ? pr.port : bits;  // spilled entries carry the bits themselves
+        }
+        const uint32_t x = m + e;
+        if (x < PL_LDS) {
+          sh.e[x] = en;
+          sh.bits[x] = bits;
+        } else {
+          spill[x] = en;
+        }
+      }
+      m += mc;
+      __syncthreads();
+    }
+    const bool allow_all = nt == 0 || sh.all;
+    const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
+    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {  // the class's (slot chunk, word) items
+      const uint32_t kc = it / a.W, w = it - kc * a.W, k0 = kc * KC;
+      uint64_t valid[KC], allow[KC];
+      int32_t du[KC];
+      bool fast = kbits;
+#pragma unroll
+      for (int kk = 0; kk < KC; kk++) {
+        const uint32_t k = k0 + kk;
+        valid[kk] = 0;
+        du[kk] = -2;
+        if (k < a.K) {
+          if (EGRESS) {
+            valid[kk] = a.VALID[uint64_t(k) * a.W + w];
+            du[kk] = a.DESCW[uint64_t(k) * a.W + w];
+          } else {
+            const bool v = a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID;
+            valid[kk] = v ? (w == a.W - 1 ? lastmask : ~0ull) : 0ull;
+            du[kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
+          }
+        }
+        fast = fast && du[kk] != -1;  // -1: egress word whose destinations mix descriptors
+        allow[kk] = allow_all ? ~0ull : 0ull;
+      }
+      if (!allow_all && fast) {
+        for (uint32_t x0 = 0; x0 < m; x0 += PL_BATCH) {
+          uint64_t pm[PL_BATCH];
+          uint32_t bits[PL_BATCH];
+#pragma unroll
+          for (uint32_t u = 0; u < PL_BATCH; u++) {
+            const uint32_t x = x0 + u;
+            uint4 e = make_uint4(PL_SKIP, 0u, 1u, 0u);
+            bits[u] = 0;
+            if (x < min(m, PL_LDS)) {
+              e = sh.e[x];
+              bits[u] = sh.bits[x];
+            } else if (x < m) {
+              e = spill[x];
+              bits[u] = EGRESS ? a.portbits[e.y] : e.y;
+            }
+            pm[u] = e.x == PL_ONES ? ~0ull : (e.x != PL_SKIP && w >= e.z && w <= e.w) ? a.PM[uint64_t(e.x) * a.W + w] : 0ull;
+          }
+          uint64_t undecided = 0;
+#pragma unroll
+          for (int kk = 0; kk < KC; kk++) {
+            if (du[kk] < 0) continue;
+            const uint32_t sft = EGRESS ? uint32_t(du[kk]) : k0 + kk;
+#pragma unroll
+            for (uint32_t u = 0; u < PL_BATCH; u++) allow[kk] |= ((bits[u] >> sft) & 1u) ? pm[u] : 0ull;
+            undecided |= valid[kk] & ~allow[kk];
+          }
+          if (!undecided) break;
+        }
+      } else if (!allow_all) {  // mixed descriptors / no bit rows (ingress K > 32): the byte port table
+        for (uint32_t x = 0; x < m; x++) {
+          const uint4 e = x < PL_LDS ? sh.e[x] : spill[x];
+          const uint64_t pm = e.x == PL_ONES ? ~0ull : (e.x != PL_SKIP && w >= e.z && w <= e.w) ? a.PM[uint64_t(e.x) * a.W + w] : 0ull;
+          if (!pm) continue;
+#pragma unroll
+          for (int kk = 0; kk < KC; kk++) allow[kk] |= pm & port_mask<EGRESS>(a, a.portok + uint64_t(e.y) * a.D, du[kk], k0 + kk, w);
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < KC; kk++) {
+        const uint32_t k = k0 + kk;
+        if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
+      }
+    }
+    __syncthreads();  // LDS reused by the next representative
+  }
+}
+template <bool EGRESS>
+__global__ __launch_bounds__(256) void k_class_rows_pl(RowArgs a) {
+  __shared__ PlShared sh;
+  class_rows_pl_blk<EGRESS>(a, sh, blockIdx.x, gridDim.x);
+}
+
 // Class rows from identity sets (IDO builds).  Block = (class representative, KC job slots,
 // 256 pod words); the representative's identity sets for those slots (ingress) or for every job
 // descriptor (egress) are staged in LDS, each thread expands them over its word's identity runs
@@ -1310,9 +1497,10 @@ __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
 }
 // PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
 __global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
+  __shared__ PlShared sh;
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_blk<true, false, 4, true>(f.ra[1], b, f.nb[1]);
-  else class_rows_blk<false, false, 4, true>(f.ra[0], b - f.nb[1], f.nb[0]);
+  if (b < f.nb[1]) class_rows_pl_blk<true>(f.ra[1], sh, b, f.nb[1]);
+  else class_rows_pl_blk<false>(f.ra[0], sh, b - f.nb[1], f.nb[0]);
 }
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
@@ -1583,33 +1771,45 @@ struct ErrArgs {
   const uint32_t *pod_iid, *pod_eid, *class_in, *class_eg;
   const uint8_t *err_in, *err_eg;  // per identity: a target selector panics
   const uint64_t *AE_in, *AE_eg;
-  unsigned long long* first;       // min job-order key
+  unsigned long long* first;       // [n_cfg] min job-order key within each probe config
 };
 
-// key = ((cfg*P + s)*P + d)*65536 + idx_in_cfg : the reference's job order (resources.go:286-333)
+// Per probe config (each config is its own table, built in order: the lowest config with a panic
+// is the one the reference hits first), key = (s*P + d)*65536 + idx_in_cfg = the reference's job
+// order (resources.go:286-333).  The host guarantees P < 2^24 and idx < 65536 on this path, so the
+// key never overflows.  Grid-stride over (s, 256-destination chunk): no grid-size limit on P.
 __global__ __launch_bounds__(256) void k_first_error(ErrArgs a) {
-  uint32_t chunks = (a.P + 255) / 256;
-  uint32_t s = blockIdx.x / chunks;
-  uint32_t d = (blockIdx.x % chunks) * blockDim.x + threadIdx.x;
-  if (d >= a.P) return;
-  // only the directions whose rows this run computes (the whole table when [lo,hi) = [0,P))
-  const bool din = d >= a.row_lo && d < a.row_hi, sin = s >= a.row_lo && s < a.row_hi;
-  if (!din && !sin) return;
-  bool s_err = sin && a.err_eg[a.pod_eid[s]];
-  bool d_err = din && a.err_in[a.pod_iid[d]];
-  uint32_t ci = din ? a.class_in[a.pod_iid[d]] : 0, ce = sin ? a.class_eg[a.pod_eid[s]] : 0;
-  unsigned long long best = ~0ull;
-  for (uint32_t k = 0; k < a.K; k++) {
-    if (a.slot_status[uint64_t(d) * a.K + k] != CYC_JOB_VALID) continue;
-    bool e = d_err || s_err;
-    if (!e && din && a.AE_in) e = (a.AE_in[(uint64_t(ci) * a.K + k) * a.W + s / 64] >> (s % 64)) & 1;
-    if (!e && sin && a.AE_eg) e = (a.AE_eg[(uint64_t(ce) * a.K + k) * a.W + d / 64] >> (d % 64)) & 1;
-    if (e) {
-      unsigned long long key = ((uint64_t(a.slot_cfg[k]) * a.P + s) * a.P + d) * 65536ull + a.slot_idx[k];
-      best = key < best ? key : best;
+  const uint64_t chunks = (a.P + 255) / 256, n = chunks * a.P;
+  for (uint64_t b = blockIdx.x; b < n; b += gridDim.x) {
+    const uint32_t s = uint32_t(b / chunks);
+    const uint32_t d = uint32_t(b % chunks) * blockDim.x + threadIdx.x;
+    if (d >= a.P) continue;
+    // only the directions whose rows this run computes (the whole table when [lo,hi) = [0,P))
+    const bool din = d >= a.row_lo && d < a.row_hi, sin = s >= a.row_lo && s < a.row_hi;
+    if (!din && !sin) continue;
+    const bool s_err = sin && a.err_eg[a.pod_eid[s]];
+    const bool d_err = din && a.err_in[a.pod_iid[d]];
+    const uint32_t ci = din ? a.class_in[a.pod_iid[d]] : 0, ce = sin ? a.class_eg[a.pod_eid[s]] : 0;
+    uint32_t cfg = 0xFFFFFFFFu;
+    unsigned long long best = ~0ull;
+    for (uint32_t k = 0; k < a.K; k++) {
+      if (a.slot_status[uint64_t(d) * a.K + k] != CYC_JOB_VALID) continue;
+      bool e = d_err || s_err;
+      if (!e && din && a.AE_in) e = (a.AE_in[(uint64_t(ci) * a.K + k) * a.W + s / 64] >> (s % 64)) & 1;
+      if (!e && sin && a.AE_eg) e = (a.AE_eg[(uint64_t(ce) * a.K + k) * a.W + d / 64] >> (d % 64)) & 1;
+      if (!e) continue;
+      const uint32_t kc = a.slot_cfg[k];
+      const unsigned long long key = (uint64_t(s) * a.P + d) * 65536ull + a.slot_idx[k];
+      if (kc != cfg) {  // slots of one config are contiguous, configs ascending
+        if (best != ~0ull) atomicMin(&a.first[cfg], best);
+        cfg = kc;
+        best = key;
+      } else {
+        best = key < best ? key : best;
+      }
     }
+    if (best != ~0ull) atomicMin(&a.first[cfg], best);
   }
-  if (best != ~0ull) atomicMin(a.first, best);
 }
 
 // ---------------------------------------------------------------- single-cell queries
@@ -1734,6 +1934,47 @@ __global__ void k_query(QueryArgs a) {
   a.res[i] = uint8_t((in == 1 ? 1 : 0) | (eg == 1 ? 2 : 0));
   a.pan[i] = code;
   a.pid[i] = sid;
+}
+
+
+// ---------------------------------------------------------------- table cells (lazy probe.Table)
+// One (source s, destination d, job slot k) cell per thread, as the reference's Table would hold
+// it after NewTableFromJobResults (table.go:38-48): VALID jobs take Ingress / Egress from the
+// planes and Combined = both allowed (jobrunner.go:85-93); BadPortProtocol and BadNamedPort jobs
+// get the fixed results of jobrunner.go:36-55; slots without a job are CYC_CONN_NO_JOB.
+struct CellArgs {
+  uint32_t K, W, row_lo, row_hi;
+  const uint64_t *in, *eg;   // planes of rows [row_lo, row_hi) (layout: include/cyclonus_hip.h)
+  const uint8_t* status;     // [P][K]
+  uint32_t s_lo, d_lo, k_lo, nd, nk;
+  uint64_t n;                // cells
+  uint8_t *o_in, *o_eg, *o_comb;  // each optional
+};
+__global__ __launch_bounds__(256) void k_table_cells(CellArgs a) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < a.n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t k = a.k_lo + uint32_t(i % a.nk);
+    const uint64_t sd = i / a.nk;
+    const uint32_t d = a.d_lo + uint32_t(sd % a.nd), s = a.s_lo + uint32_t(sd / a.nd);
+    const uint8_t st = a.status[uint64_t(d) * a.K + k];
+    uint8_t ci = CYC_CONN_NO_JOB, ce = CYC_CONN_NO_JOB, cc = CYC_CONN_NO_JOB;
+    if (st == CYC_JOB_VALID) {
+      // the host checked that the requested planes cover these rows
+      const bool ai = a.o_in || a.o_comb ? (a.in[(uint64_t(d - a.row_lo) * a.K + k) * a.W + s / 64] >> (s % 64)) & 1 : false;
+      const bool ae = a.o_eg || a.o_comb ? (a.eg[(uint64_t(s - a.row_lo) * a.K + k) * a.W + d / 64] >> (d % 64)) & 1 : false;
+      ci = ai ? CYC_CONN_ALLOWED : CYC_CONN_BLOCKED;
+      ce = ae ? CYC_CONN_ALLOWED : CYC_CONN_BLOCKED;
+      cc = ai && ae ? CYC_CONN_ALLOWED : CYC_CONN_BLOCKED;
+    } else if (st == CYC_JOB_BAD_PORT_PROTOCOL) {
+      ci = cc = CYC_CONN_INVALID_PORT_PROTOCOL;
+      ce = CYC_CONN_UNKNOWN;
+    } else if (st == CYC_JOB_BAD_NAMED_PORT) {
+      ci = cc = CYC_CONN_INVALID_NAMED_PORT;
+      ce = CYC_CONN_UNKNOWN;
+    }
+    if (a.o_in) a.o_in[i] = ci;
+    if (a.o_eg) a.o_eg[i] = ce;
+    if (a.o_comb) a.o_comb[i] = cc;
+  }
 }
 
 }  // namespace cyc
@@ -1867,11 +2108,18 @@ struct cyc_ctx {
   hipEvent_t fork_ev = nullptr, join_ev = nullptr, sel_ev = nullptr, ports_ev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   hipGraph_t graph = nullptr;  // kept alive with its exec
-  // Execs replaced by a re-capture (new output pointers, row range or tuning knob) are retired, not
-  // destroyed, until the context is destroyed: re-capturing while destroying the previous execs
-  // crashed inside hipGraphLaunch on ROCm 7 (scripts/debug_variants.py; a launch indexed a stream
-  // list past its end).
-  std::vector<std::pair<hipGraphExec_t, hipGraph_t>> retired;
+  hipEvent_t graph_done = nullptr;  // recorded on the caller's stream after each launch of graph_exec
+  // An exec replaced by a re-capture (new output pointers, row range or tuning knob) may still have
+  // a launch queued on the caller's stream: cyc_probe_run returns without synchronising.  It is
+  // retired with the event recorded after its last launch and destroyed only once that event has
+  // completed (reap_graphs).  Destroying it at once freed an exec a queued launch still used — the
+  // intermittent crash inside hipGraphLaunch seen in round 1.
+  struct Retired {
+    hipGraphExec_t exec;
+    hipGraph_t graph;
+    hipEvent_t done;  // null: never launched
+  };
+  std::vector<Retired> retired;
   const void* graph_key[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   bool timed_graph = false;
   DirDev dir[2];
@@ -2097,7 +2345,7 @@ static void prepare_device(cyc_ctx* c) {
   c->VALID.alloc(std::max<uint64_t>(K * W * 8, 16));
   c->DESCW.alloc(std::max<uint64_t>(K * W * 4, 16));
   c->DM.alloc(std::max<uint64_t>(K * D * W * 8, 16));
-  c->first_err.alloc(16);
+  c->first_err.alloc(std::max<uint64_t>(uint64_t(pb.n_cfg) * 8, 16));  // per probe config (k_first_error)
   c->status_sink.alloc(std::max<uint64_t>(uint64_t(pb.P) * K, 16));
   for (int d = 0; d < 2; d++) {
     Identities& I = c->ids[d];
@@ -2126,9 +2374,9 @@ static void prepare_device(cyc_ctx* c) {
     else dd.AE.alloc(0);
     dd.B.alloc(ido_possible(c) ? std::max<uint64_t>(ido_b_bytes(c, d), 16) : 16);
     {  // IP-peer list bounds per identity: the IP peers of its namespace's targets
+      // (upper bound for both list uses: IDO builds list the IP peers, PM builds every peer)
       std::vector<uint32_t> ns_ip(pb.strings.size(), 0), off(dd.n + 1, 0);
-      for (const DTarget& t : pb.tgt[d])
-        for (uint32_t j = t.poff; j < t.poff + t.pcnt; j++) ns_ip[t.ns] += pb.peers[j].kind == PK_IP;
+      for (const DTarget& t : pb.tgt[d]) ns_ip[t.ns] += t.pcnt;
       for (uint32_t i = 0; i < dd.n; i++) off[i + 1] = off[i] + ns_ip[I.ns[i]];
       upload(dd.ip_off, off);
       dd.ip_cnt.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
@@ -2169,6 +2417,9 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   a.rep_cnt = dd.rep_cnt();
   return a;
 }
+
+// PM-build class rows (k_class_rows_pl): blocks per direction; they stride over the representatives
+static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c->n_act[d], 2048u); }
 
 // Range plan for rows [lo,hi): (1) the rows ordered so pods sharing class rows are adjacent
 // (L2 / Infinity-Cache reuse in k_emit); (2) the identities those rows use, per direction —
@@ -2381,7 +2632,7 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
                                          c->ER.as<uint64_t>(), bat);
     } else {
       const uint32_t grp = c->ip_group;
-      k_ip_rows_fast<<<unsigned((uint64_t((W + 63) / 64) * ((Ri + grp - 1) / grp) + 3) / 4), 256, 0, st>>>(
+      k_ip_rows_fast<<<unsigned(ip_rows_blocks(Ri, W, grp)), 256, 0, st>>>(
           Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>(),
           c->ip_rng.as<uint32_t>(), grp);
     }
@@ -2497,7 +2748,10 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   }
   unsigned g = unsigned(per_rep * ra.rep_blocks);
 #define CYC_ROWS(EG, ERR, KCT, LOOP) k_class_rows<EG, ERR, KCT, LOOP><<<g, 256, 0, st>>>(ra)
-  if (pb.may_err) {
+  if (!pb.may_err && !ido_mode(c)) {  // per-class flattened peer lists (the IP word spans are final here)
+    if (d == 0) k_class_rows_pl<false><<<pl_blocks(c, d), 256, 0, st>>>(ra);
+    else k_class_rows_pl<true><<<pl_blocks(c, d), 256, 0, st>>>(ra);
+  } else if (pb.may_err) {
     if (d == 0) CYC_ROWS(false, true, 8, false);
     else CYC_ROWS(true, true, 8, false);
   } else if (ido_mode(c)) {
@@ -2698,7 +2952,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.PM = c->PM.as<uint64_t>();
   fb.rng = c->ip_rng.as<uint32_t>();
   fb.ip_grp = c->ip_group;
-  fb.nb[0] = Ri ? blocks((uint64_t((W + 63) / 64) * ((Ri + fb.ip_grp - 1) / fb.ip_grp) + 3) / 4) : 0u;
+  fb.nb[0] = Ri ? blocks(ip_rows_blocks(Ri, W, fb.ip_grp)) : 0u;
   const uint32_t Rp = c->rp_off[2] - c->rp_off[0], u0 = c->rpu_off[0], Ru = c->rpu_off[2] - u0;
   fb.Ru = Ru;
   fb.E = E;
@@ -2733,8 +2987,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fc.nb[d] = na ? blocks((uint64_t(na) + 255) / 256) : 0u;
     if (!na) continue;
     fd.ra[d] = row_args(c, d);  // its blocks empty the direction's hash table for the next run
-    if (!ido) {  // PM builds: the class rows are launch D (k_front_d_pm), no identity sets
-      fd.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + 3) / 4) * fd.ra[d].rep_blocks);
+    if (!ido) {  // PM builds: launch D (k_front_d_pm) is the class rows from flattened peer lists
+      fd.nb[d] = pl_blocks(c, d);
       continue;
     }
     fe.ra[d] = fd.ra[d];
@@ -2856,18 +3110,30 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
   HIPCHK(hipMemcpyAsync(dst, c->slot_status.p, std::max<uint64_t>(nst, 1), hipMemcpyDeviceToDevice, st));
 }
 
+// Destroy the retired execs whose last launch has completed (all of them when `wait`).
+static void reap_graphs(cyc_ctx* c, bool wait) {
+  size_t keep = 0;
+  for (size_t i = 0; i < c->retired.size(); i++) {
+    cyc_ctx::Retired& r = c->retired[i];
+    if (r.done && wait) (void)hipEventSynchronize(r.done);
+    const bool done = !r.done || wait || hipEventQuery(r.done) != hipErrorNotReady;
+    if (!done) {
+      c->retired[keep++] = r;
+      continue;
+    }
+    (void)hipGraphExecDestroy(r.exec);
+    if (r.graph) (void)hipGraphDestroy(r.graph);
+    if (r.done) (void)hipEventDestroy(r.done);
+  }
+  c->retired.resize(keep);
+}
+
 static void drop_graph(cyc_ctx* c) {
-  if (c->graph_exec) c->retired.emplace_back(c->graph_exec, c->graph);
+  if (c->graph_exec) c->retired.push_back({c->graph_exec, c->graph, c->graph_done});
   c->graph_exec = nullptr;
   c->graph = nullptr;
-  if (c->retired.size() >= 64) {  // bound the retired list: drained with the device idle
-    (void)hipDeviceSynchronize();
-    for (auto& r : c->retired) {
-      (void)hipGraphExecDestroy(r.first);
-      if (r.second) (void)hipGraphDestroy(r.second);
-    }
-    c->retired.clear();
-  }
+  c->graph_done = nullptr;
+  reap_graphs(c, false);
 }
 
 static void ensure_cap_streams(cyc_ctx* c) {
@@ -2910,12 +3176,14 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
       HIPCHK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
       capture_pipeline(c, c->cap_stream, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status, lo, hi);
       HIPCHK(hipStreamEndCapture(c->cap_stream, &g));
-      c->graph = g;  // destroyed with the exec (drop_graph)
+      c->graph = g;  // destroyed with the exec (drop_graph / reap_graphs)
       HIPCHK(hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
+      HIPCHK(hipEventCreateWithFlags(&c->graph_done, hipEventDisableTiming));
       memcpy(c->graph_key, key, sizeof(key));
     }
     HIPCHK(hipEventRecord(c->ev[0], st));
     HIPCHK(hipGraphLaunch(c->graph_exec, st));
+    HIPCHK(hipEventRecord(c->graph_done, st));  // the exec may be retired once this completes
     HIPCHK(hipEventRecord(c->ev[3], st));
     c->timed = true;
     c->timed_graph = true;
@@ -2927,7 +3195,9 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
 
   // 8. panic path: the first panicking job in job order, as the reference would hit it
   if (pb.may_err) {
-    HIPCHK(hipMemsetAsync(c->first_err.p, 0xFF, 8, st));
+    if (P >= (1u << 24) || K > 65536)  // k_first_error's job-order key: (s*P + d)*65536 + idx < 2^64
+      throw Panic{CYC_ERR_ARG, "inputs that can panic are limited to 2^24 pods and 65536 job slots"};
+    HIPCHK(hipMemsetAsync(c->first_err.p, 0xFF, uint64_t(pb.n_cfg) * 8, st));
     ErrArgs e{};
     e.P = P;
     e.K = K;
@@ -2947,14 +3217,16 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     e.AE_in = c->dir[0].n ? c->dir[0].AE.as<uint64_t>() : nullptr;
     e.AE_eg = c->dir[1].n ? c->dir[1].AE.as<uint64_t>() : nullptr;
     e.first = c->first_err.as<unsigned long long>();
-    if (P && K) k_first_error<<<unsigned(uint64_t((P + 255) / 256) * P), 256, 0, st>>>(e);
-    unsigned long long first = ~0ull;
-    HIPCHK(hipMemcpyAsync(&first, c->first_err.p, 8, hipMemcpyDeviceToHost, st));
+    if (P && K) k_first_error<<<grid1(uint64_t((P + 255) / 256) * P, 1), 256, 0, st>>>(e);
+    std::vector<unsigned long long> first(std::max<uint32_t>(pb.n_cfg, 1), ~0ull);
+    HIPCHK(hipMemcpyAsync(first.data(), c->first_err.p, uint64_t(pb.n_cfg) * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (first != ~0ull) {
-      uint32_t idx = uint32_t(first % 65536);
-      uint64_t rest = first / 65536;
-      uint32_t d = uint32_t(rest % P), s = uint32_t((rest / P) % P), cfg = uint32_t(rest / P / P);
+    uint32_t cfg = 0;
+    while (cfg < pb.n_cfg && first[cfg] == ~0ull) cfg++;
+    if (cfg < pb.n_cfg) {
+      const uint32_t idx = uint32_t(first[cfg] % 65536);
+      const uint64_t rest = first[cfg] / 65536;
+      const uint32_t d = uint32_t(rest % P), s = uint32_t(rest / P);
       // duplicate-key fatal of an EARLIER config's table wins (tables are built per config)
       for (uint32_t cc = 0; cc < cfg; cc++)
         if (!pb.dup_key_msg[cc].empty()) return fail(c, CYC_ERR_DUPLICATE_KEY, pb.dup_key_msg[cc]);
@@ -3090,12 +3362,7 @@ void cyc_ctx_destroy(cyc_ctx* c) {
   if (c->stream) {
     (void)hipSetDevice(c->device);
     drop_graph(c);
-    (void)hipDeviceSynchronize();
-    for (auto& r : c->retired) {
-      (void)hipGraphExecDestroy(r.first);
-      if (r.second) (void)hipGraphDestroy(r.second);
-    }
-    c->retired.clear();
+    reap_graphs(c, true);  // waits for each retired exec's last launch only
     destroy_events(c);
     if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
     if (c->cap_stream2) (void)hipStreamDestroy(c->cap_stream2);
@@ -3223,6 +3490,148 @@ int cyc_probe_run_host(cyc_ctx* c, uint64_t* h_in, uint64_t* h_eg, uint8_t* h_st
   });
 }
 
+// ---------------------------------------------------------------- device-resident tables
+struct cyc_table {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  uint32_t P = 0, K = 0, W = 0;
+  int64_t row_lo = 0, row_hi = 0;
+  const uint64_t *in = nullptr, *eg = nullptr;
+  const uint8_t* status = nullptr;
+  DevBuf own_in, own_eg, own_st;  // cyc_table_run: the table owns its planes
+};
+
+static int table_new(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) {
+  if (lo < 0 || hi > int64_t(c->pb.P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
+  auto* t = new cyc_table();
+  t->device = c->device;
+  t->P = c->pb.P;
+  t->K = c->pb.K;
+  t->W = c->pb.W;
+  t->row_lo = lo;
+  t->row_hi = hi;
+  *out = t;
+  return (int)CYC_OK;
+}
+
+int cyc_table_run(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) {
+  if (!c || !out) return CYC_ERR_ARG;
+  *out = nullptr;
+  if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
+  return guarded(c, [&]() -> int {
+    HIPCHK(hipSetDevice(c->device));
+    cyc_table* t = nullptr;
+    int rc = table_new(c, lo, hi, &t);
+    if (rc != CYC_OK) return rc;
+    std::unique_ptr<cyc_table> hold(t);
+    const uint64_t words = uint64_t(hi - lo) * c->pb.K * c->pb.W;
+    t->own_in.alloc(std::max<uint64_t>(words * 8, 16));
+    t->own_eg.alloc(std::max<uint64_t>(words * 8, 16));
+    t->own_st.alloc(std::max<uint64_t>(uint64_t(c->pb.P) * c->pb.K, 16));
+    t->in = t->own_in.as<uint64_t>();
+    t->eg = t->own_eg.as<uint64_t>();
+    t->status = t->own_st.as<uint8_t>();
+    rc = run_pipeline(c, c->stream, t->own_in.as<uint64_t>(), t->own_eg.as<uint64_t>(), t->own_st.as<uint8_t>(), lo, hi);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (rc != CYC_OK) return rc;
+    *out = hold.release();
+    return (int)CYC_OK;
+  });
+}
+
+int cyc_table_wrap(cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg, const uint8_t* d_status, int64_t lo, int64_t hi,
+                   cyc_table** out) {
+  if (!c || !out) return CYC_ERR_ARG;
+  *out = nullptr;
+  if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
+  if (!d_status || ((!d_in || !d_eg) && hi > lo)) return fail(c, CYC_ERR_ARG, "null plane");
+  cyc_table* t = nullptr;
+  int rc = table_new(c, lo, hi, &t);
+  if (rc != CYC_OK) return rc;
+  t->in = d_in;
+  t->eg = d_eg;
+  t->status = d_status;
+  *out = t;
+  return (int)CYC_OK;
+}
+
+const char* cyc_table_error(const cyc_table* t) { return t ? t->err.c_str() : "null table"; }
+
+int cyc_table_shape(const cyc_table* t, int64_t* out, int n) {
+  if (!t || !out) return CYC_ERR_ARG;
+  const int64_t v[5] = {t->P, t->K, t->W, t->row_lo, t->row_hi};
+  for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
+  return (int)CYC_OK;
+}
+
+int cyc_table_cells(cyc_table* t, int64_t s_lo, int64_t s_hi, int64_t d_lo, int64_t d_hi, int64_t k_lo, int64_t k_hi,
+                    uint8_t* ingress, uint8_t* egress, uint8_t* combined) {
+  if (!t) return CYC_ERR_ARG;
+  auto bad = [&](const char* m) {
+    t->err = m;
+    return (int)CYC_ERR_ARG;
+  };
+  if (s_lo < 0 || s_hi > int64_t(t->P) || s_lo > s_hi || d_lo < 0 || d_hi > int64_t(t->P) || d_lo > d_hi || k_lo < 0 ||
+      k_hi > int64_t(t->K) || k_lo > k_hi)
+    return bad("cell range out of bounds");
+  // ingress rows are keyed by destination, egress rows by source (include/cyclonus_hip.h)
+  const bool need_d = ingress || combined, need_s = egress || combined;
+  if (s_hi > s_lo && d_hi > d_lo && k_hi > k_lo) {
+    if (need_d && (d_lo < t->row_lo || d_hi > t->row_hi)) return bad("ingress cells need destinations inside the table's rows");
+    if (need_s && (s_lo < t->row_lo || s_hi > t->row_hi)) return bad("egress cells need sources inside the table's rows");
+  }
+  const uint64_t n = uint64_t(s_hi - s_lo) * uint64_t(d_hi - d_lo) * uint64_t(k_hi - k_lo);
+  if (!n) return (int)CYC_OK;
+  try {
+    HIPCHK(hipSetDevice(t->device));
+    if (!t->stream) HIPCHK(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    DevBuf o[3];
+    uint8_t* host[3] = {ingress, egress, combined};
+    for (int x = 0; x < 3; x++)
+      if (host[x]) o[x].alloc(n);
+    CellArgs a{};
+    a.K = t->K;
+    a.W = t->W;
+    a.row_lo = uint32_t(t->row_lo);
+    a.row_hi = uint32_t(t->row_hi);
+    a.in = t->in;
+    a.eg = t->eg;
+    a.status = t->status;
+    a.s_lo = uint32_t(s_lo);
+    a.d_lo = uint32_t(d_lo);
+    a.k_lo = uint32_t(k_lo);
+    a.nd = uint32_t(d_hi - d_lo);
+    a.nk = uint32_t(k_hi - k_lo);
+    a.n = n;
+    a.o_in = o[0].as<uint8_t>();
+    a.o_eg = o[1].as<uint8_t>();
+    a.o_comb = o[2].as<uint8_t>();
+    k_table_cells<<<grid1(n, 256), 256, 0, t->stream>>>(a);
+    HIPCHK(hipGetLastError());
+    for (int x = 0; x < 3; x++)
+      if (host[x]) HIPCHK(hipMemcpyAsync(host[x], o[x].p, n, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+  } catch (HipErr& h) {
+    t->err = h.msg;
+    return (int)CYC_ERR_HIP;
+  } catch (std::bad_alloc&) {
+    t->err = "host allocation failed";
+    return (int)CYC_ERR_OOM;
+  }
+  return (int)CYC_OK;
+}
+
+void cyc_table_destroy(cyc_table* t) {
+  if (!t) return;
+  (void)hipSetDevice(t->device);
+  if (t->stream) {
+    (void)hipStreamSynchronize(t->stream);
+    (void)hipStreamDestroy(t->stream);
+  }
+  delete t;  // owned planes are freed by their DevBufs
+}
+
 int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
   if (!c || !ms) return CYC_ERR_ARG;
   if (!c->timed) return fail(c, CYC_ERR_ARG, "no run yet");
@@ -3257,6 +3666,7 @@ int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
 
 int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return CYC_ERR_ARG;
+  if (c->stream) (void)hipSetDevice(c->device);  // drop_graph may destroy this context's execs
   if (std::string(name) == "emit_variant") {
     c->emit_variant = int(value);
     drop_graph(c);

@@ -99,6 +99,21 @@ class Engine:
             ),
         )
 
+    def table(self, row_lo: int = 0, row_hi: Optional[int] = None) -> "DeviceTable":
+        """Run the probe into a device-resident table (cyc_table_run) for target rows [row_lo, row_hi)."""
+        hi = self.shape["pods"] if row_hi is None else row_hi
+        t = ctypes.c_void_p()
+        check(self._ctx, lib().cyc_table_run(self._ctx, int(row_lo), int(hi), ctypes.byref(t)))
+        return DeviceTable(t)
+
+    def wrap_table(self, d_ingress: int, d_egress: int, d_status: int, row_lo: int = 0, row_hi=None) -> "DeviceTable":
+        """A table over planes produced by run_device (cyc_table_wrap; the caller keeps them alive)."""
+        hi = self.shape["pods"] if row_hi is None else row_hi
+        t = ctypes.c_void_p()
+        check(self._ctx, lib().cyc_table_wrap(self._ctx, ctypes.c_void_p(d_ingress), ctypes.c_void_p(d_egress),
+                                              ctypes.c_void_p(d_status), int(row_lo), int(hi), ctypes.byref(t)))
+        return DeviceTable(t)
+
     def query_traffic(self, traffics):
         """Policy.IsTrafficAllowed on the GPU for a list of matcher.Traffic dicts -> [(ingress, egress)]."""
         b = _bytes(list(traffics))
@@ -148,3 +163,35 @@ class Engine:
         ms = (ctypes.c_double * 3)()
         check(self._ctx, lib().cyc_last_timings(self._ctx, ms, 3))
         return tuple(ms)
+
+
+class DeviceTable:
+    """A cyc_table: verdict planes resident on the GPU; cells() returns probe.Connectivity codes."""
+
+    def __init__(self, handle: ctypes.c_void_p):
+        self._t = handle
+        v = (ctypes.c_int64 * 5)()
+        lib().cyc_table_shape(self._t, v, 5)
+        self.pods, self.slots, self.words, self.row_lo, self.row_hi = (int(x) for x in v)
+
+    def close(self):
+        if self._t:
+            lib().cyc_table_destroy(self._t)
+            self._t = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def cells(self, s_lo, s_hi, d_lo, d_hi, k_lo=0, k_hi=None, want=("ingress", "egress", "combined")):
+        """{name: u8 array [s, d, k]} of cyc_connectivity codes for the requested block."""
+        k_hi = self.slots if k_hi is None else k_hi
+        shp = (max(s_hi - s_lo, 0), max(d_hi - d_lo, 0), max(k_hi - k_lo, 0))
+        out = {n: np.zeros(shp, np.uint8) for n in want}
+        ptr = [out[n].ctypes.data if n in out else None for n in ("ingress", "egress", "combined")]
+        rc = lib().cyc_table_cells(self._t, int(s_lo), int(s_hi), int(d_lo), int(d_hi), int(k_lo), int(k_hi), *ptr)
+        if rc != _lib.OK:
+            raise _lib.CyclonusError(rc, lib().cyc_table_error(self._t).decode(errors="replace"))
+        return out

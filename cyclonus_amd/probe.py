@@ -130,18 +130,53 @@ class Item:  # table.go:10-23
 
 
 # ----------------------------------------------------------------------------- table view
-class Table:
-    """Lazy probe.Table over one probe config's packed planes (layout: include/cyclonus_hip.h)."""
+_CONN = {_lib.CONN_UNKNOWN: UNKNOWN, _lib.CONN_CHECK_FAILED: CHECK_FAILED, _lib.CONN_INVALID_NAMED_PORT: INVALID_NAMED_PORT,
+         _lib.CONN_INVALID_PORT_PROTOCOL: INVALID_PORT_PROTOCOL, _lib.CONN_BLOCKED: BLOCKED, _lib.CONN_ALLOWED: ALLOWED}
 
-    def __init__(self, resources: Resources, config: ProbeConfig, status, ingress, egress, slot_lo: int, slot_hi: int):
+
+class PlaneCells:
+    """Cells source over packed planes held on the host (status[P,K], ingress[P,K,W], egress[P,K,W]),
+    e.g. the oracle's: the same Connectivity mapping as cyc_table_cells (jobrunner.go:36-55,85-93)."""
+
+    def __init__(self, status, ingress, egress):
+        self.status, self.ingress, self.egress = status, ingress, egress
+
+    def cells(self, s_lo, s_hi, d_lo, d_hi, k_lo, k_hi, want=("ingress", "egress", "combined")):
+        s = np.arange(s_lo, s_hi)[:, None, None]
+        d = np.arange(d_lo, d_hi)[None, :, None]
+        k = np.arange(k_lo, k_hi)[None, None, :]
+        st = self.status[d, k]
+        ai = ((self.ingress[d, k, s // 64] >> (s % 64).astype(np.uint64)) & np.uint64(1)).astype(bool)
+        ae = ((self.egress[s, k, d // 64] >> (d % 64).astype(np.uint64)) & np.uint64(1)).astype(bool)
+        valid, bpp, bnp = st == _lib.JOB_VALID, st == _lib.JOB_BAD_PORT_PROTOCOL, st == _lib.JOB_BAD_NAMED_PORT
+        inv = np.where(bpp, _lib.CONN_INVALID_PORT_PROTOCOL, np.where(bnp, _lib.CONN_INVALID_NAMED_PORT, _lib.CONN_NO_JOB))
+        allowed = lambda b: np.where(b, _lib.CONN_ALLOWED, _lib.CONN_BLOCKED)  # noqa: E731
+        out = {"ingress": np.where(valid, allowed(ai), inv),
+               "egress": np.where(valid, allowed(ae), np.where(bpp | bnp, _lib.CONN_UNKNOWN, _lib.CONN_NO_JOB)),
+               "combined": np.where(valid, allowed(ai & ae), inv)}
+        return {n: np.broadcast_to(out[n], (s_hi - s_lo, d_hi - d_lo, k_hi - k_lo)).astype(np.uint8) for n in want}
+
+
+class Table:
+    """Lazy probe.Table over one probe config's slots of a verdict table (table.go:24-56).
+
+    `cells` is a cells source: the product's DeviceTable (cyc_table: planes resident on the GPU,
+    Connectivity computed on the device per block of cells) or a PlaneCells view.  Items
+    (table.go:10-23) are built on demand; the P^2 Item maps of truthtable.go:28-48 never exist."""
+
+    CACHE_CELLS = 1 << 24  # whole-table Connectivity cache for rendering small tables
+
+    def __init__(self, resources: Resources, config: ProbeConfig, cells, slot_lo: int, slot_hi: int):
         self.resources = resources
         self.config = config
-        self.status, self.ingress, self.egress = status, ingress, egress
+        self.src = cells
         self.slots = range(slot_lo, slot_hi)
         self.items = resources.sorted_pod_names()
         self.index = {p.pod_string(): i for i, p in enumerate(resources.pods)}
+        self._all = None
+        self._rows = {}
 
-    def _job_key(self, d: int, j: int, st: int) -> str:
+    def _job_key(self, d: int, j: int) -> str:
         pod = self.resources.pods[d]
         if self.config.all_available:
             c = pod.containers[j]
@@ -154,23 +189,29 @@ class Table:
             resolved = int(port)
         return f"{self.config.protocol}/{resolved}"
 
+    def _row(self, s: int):
+        """Connectivity codes of source row s: {name: [P, nk]}."""
+        P, lo, hi = len(self.resources.pods), self.slots.start, self.slots.stop
+        if self._all is None and P * P * max(hi - lo, 1) <= self.CACHE_CELLS:
+            self._all = self.src.cells(0, P, 0, P, lo, hi)
+        if self._all is not None:
+            return {n: a[s] for n, a in self._all.items()}
+        if s not in self._rows:
+            if len(self._rows) > 64:
+                self._rows.clear()
+            self._rows[s] = {n: a[0] for n, a in self.src.cells(s, s + 1, 0, P, lo, hi).items()}
+        return self._rows[s]
+
     def get(self, fr: str, to: str) -> Item:
         s, d = self.index[fr], self.index[to]
+        row = self._row(s)
         out = {}
-        for j, k in enumerate(self.slots):
-            st = int(self.status[d, k])
-            if st == _lib.JOB_NONE:
+        for j in range(len(self.slots)):
+            ci = int(row["combined"][d, j])
+            if ci == _lib.CONN_NO_JOB:
                 continue
-            key = self._job_key(d, j, st)
-            if st == _lib.JOB_VALID:
-                ing = ALLOWED if (int(self.ingress[d, k, s // 64]) >> (s % 64)) & 1 else BLOCKED
-                eg = ALLOWED if (int(self.egress[s, k, d // 64]) >> (d % 64)) & 1 else BLOCKED
-                comb = ALLOWED if ing == ALLOWED and eg == ALLOWED else BLOCKED
-            elif st == _lib.JOB_BAD_NAMED_PORT:
-                ing, eg, comb = INVALID_NAMED_PORT, UNKNOWN, INVALID_NAMED_PORT
-            else:
-                ing, eg, comb = INVALID_PORT_PROTOCOL, UNKNOWN, INVALID_PORT_PROTOCOL
-            out[key] = JobResult(key, ing, eg, comb)
+            key = self._job_key(d, j)
+            out[key] = JobResult(key, _CONN[int(row["ingress"][d, j])], _CONN[int(row["egress"][d, j])], _CONN[ci])
         return Item(fr, to, out)
 
     def keys(self):
@@ -242,12 +283,12 @@ class Runner:
         eng: Engine = self.policy.engine
         eng.load_resources(json.dumps(res.to_json()))
         eng.prepare([c.to_json() for c in cfgs])
-        status, ing, eg = eng.run_host()
+        dt = eng.table()  # planes stay on the GPU; Items are built from device-computed cells
         maxc = max((len(p.containers) for p in res.pods), default=0)
         tables, lo = [], 0
         for c in cfgs:
             n = maxc if c.all_available else 1
-            tables.append(Table(res, c, status, ing, eg, lo, lo + n))
+            tables.append(Table(res, c, dt, lo, lo + n))
             lo += n
         return tables
 

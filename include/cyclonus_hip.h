@@ -111,6 +111,44 @@ int cyc_probe_run(cyc_ctx* ctx, void* hip_stream, uint64_t* d_ingress, uint64_t*
 int cyc_probe_run_host(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_t* status, int64_t row_lo,
                        int64_t row_hi);
 
+/* ---- Device-resident verdict tables: the lazy probe.Table (pkg/connectivity/probe/table.go:24-56).
+ * The reference's Runner.RunProbeForConfig returns *Table = NewTableFromJobResults(resources,
+ * runProbe(jobs)) (jobrunner.go:29-58, table.go:38-48): one Item per (from, to) pod pair holding a
+ * JobResult {Ingress, Egress, Combined} per job key.  A cyc_table keeps the packed planes on the GPU
+ * and hands out those Connectivity values for any block of cells, so a binding never builds the
+ * P^2*K Job structs of resources.go:284-364. */
+typedef enum { /* probe.Connectivity, in the order of AllConnectivity (connectivity.go:16-23) */
+  CYC_CONN_UNKNOWN = 0,
+  CYC_CONN_CHECK_FAILED = 1,
+  CYC_CONN_INVALID_NAMED_PORT = 2,
+  CYC_CONN_INVALID_PORT_PROTOCOL = 3,
+  CYC_CONN_BLOCKED = 4,
+  CYC_CONN_ALLOWED = 5,
+  CYC_CONN_NO_JOB = 255 /* no job in this slot: the Item has no JobResult for it */
+} cyc_connectivity;
+
+typedef struct cyc_table cyc_table;
+
+/* Run the probe for target rows [row_lo, row_hi) into planes the table owns (synchronous; panics
+ * are reported as by cyc_probe_run).  A table stays valid after its context is destroyed. */
+int cyc_table_run(cyc_ctx* ctx, int64_t row_lo, int64_t row_hi, cyc_table** out);
+/* A table over planes the caller produced with cyc_probe_run (device pointers, not owned; they
+ * must outlive the table and the run must be complete before cyc_table_cells). */
+int cyc_table_wrap(cyc_ctx* ctx, const uint64_t* d_ingress, const uint64_t* d_egress, const uint8_t* d_status,
+                   int64_t row_lo, int64_t row_hi, cyc_table** out);
+/* Connectivity of every cell (s, d, k) of sources [s_lo,s_hi) x destinations [d_lo,d_hi) x slots
+ * [k_lo,k_hi), computed on the device, into host arrays indexed
+ *   ((s - s_lo) * (d_hi - d_lo) + (d - d_lo)) * (k_hi - k_lo) + (k - k_lo)
+ * ingress / egress / combined are each optional (NULL = not wanted): JobResult.Ingress, .Egress and
+ * .Combined of that job (jobrunner.go:36-55,85-93).  Ingress needs the destinations inside the
+ * table's rows, egress the sources, combined both (a row shard answers its own rows). */
+int cyc_table_cells(cyc_table* t, int64_t s_lo, int64_t s_hi, int64_t d_lo, int64_t d_hi, int64_t k_lo, int64_t k_hi,
+                    uint8_t* ingress, uint8_t* egress, uint8_t* combined);
+/* out[0..4] = pods, slots, words, row_lo, row_hi */
+int cyc_table_shape(const cyc_table* t, int64_t* out, int n);
+const char* cyc_table_error(const cyc_table* t);
+void cyc_table_destroy(cyc_table* t);
+
 /* Average device time (ms) of the last run's kernels, measured with HIP events on the launch
  * stream: [0] whole pipeline, [1] the emit launch(es) (the HBM-roofline kernel; one launch writes
  * both planes unless "emit_merged" is 0), [2] class rows of both directions.  Graph runs report

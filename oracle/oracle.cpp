@@ -709,11 +709,18 @@ struct Policy {
     const TrafficPeer& target = isIngress ? tr.dst : tr.src;
     const TrafficPeer& peer = isIngress ? tr.src : tr.dst;
     if (!target.internal) return true;  // :151-153
+    return allowed_given(targets_applying(target, isIngress), peer, tr);
+  }
+  // TargetsApplyingToPod :68-82 walks EVERY target of the direction
+  std::vector<const Target*> targets_applying(const TrafficPeer& target, bool isIngress) const {
     const auto& dict = isIngress ? ingress : egress;
-    // TargetsApplyingToPod :68-82 walks EVERY target
     std::vector<const Target*> matching;
     for (auto& kv : dict)
       if (kv.second->is_match(target.internal->ns, target.internal->podLabels)) matching.push_back(kv.second.get());
+    return matching;
+  }
+  // :158-171 given the matching targets (every matching target's Allows runs, in order)
+  static bool allowed_given(const std::vector<const Target*>& matching, const TrafficPeer& peer, const Traffic& tr) {
     if (matching.empty()) return true;  // :158-160
     size_t allowers = 0, deniers = 0;
     for (auto* t : matching) {
@@ -1190,6 +1197,69 @@ int orc_probe_cells_mt(void* hv, const char* probes_json, const int32_t* ss, con
 
 // analyze --mode query-traffic (analyze.go:209-225): JSON list of matcher.Traffic.
 // out[i] = ingress | egress<<1 | panic<<2
+// One plane row: dir 0 = ingress row of destination `pod` (bit s over every source), dir 1 = egress
+// row of source `pod` (bit d over every destination), slot k; row[W] as in the planes.  The same
+// per-cell IsIngressOrEgressAllowed walk as orc_probe_run, with the row's fixed target pod's
+// TargetsApplyingToPod list computed once (it depends on that pod alone, policy.go:68-82).  Cells
+// without a VALID job are 0.  `threads` split the row's cells.  Returns 0, 1 on a Go panic.
+int orc_probe_row(void* hv, const char* probes_json, int dir, int pod, int k, uint64_t* row, int threads, char* err,
+                  size_t errcap) {
+  auto* h = static_cast<Handle*>(hv);
+  try {
+    auto cfgs = decode_probes(*ojson::parse(probes_json));
+    int K;
+    auto off = slot_offsets(h->res, cfgs, K);
+    const auto& pods = h->res.pods;
+    const int P = int(pods.size()), W = (P + 63) / 64;
+    if (pod < 0 || pod >= P || k < 0 || k >= K) {
+      set_err(err, errcap, "row out of range");
+      return -1;
+    }
+    size_t c = 0;
+    while (c + 1 < cfgs.size() && off[c + 1] <= k) c++;
+    memset(row, 0, size_t(W) * 8);
+    const bool ingress = dir == 0;
+    // the fixed pod is the target of this direction (ingress: destination, egress: source)
+    TrafficPeer tp;
+    tp.internal = std::make_shared<InternalPeer>(InternalPeer{pods[pod].labels, h->res.ns_labels(pods[pod].ns), pods[pod].ns});
+    tp.ip = pods[pod].ip;
+    const auto matching = h->policy->targets_applying(tp, ingress);
+    const JobDesc jd = ingress ? job_desc(pods[pod], cfgs[c], k - int(off[c])) : JobDesc{};
+    threads = std::max(1, std::min(threads, 64));
+    std::vector<std::thread> pool;
+    std::vector<int> rc(threads, 0);
+    std::vector<std::string> msg(threads);
+    for (int t = 0; t < threads; t++) {
+      // whole 64-pod words per thread: no two threads write one word
+      const int w0 = int(int64_t(W) * t / threads), w1 = int(int64_t(W) * (t + 1) / threads);
+      pool.emplace_back([&, t, w0, w1] {
+        try {
+          for (int q = w0 * 64; q < std::min(P, w1 * 64); q++) {
+            const int s = ingress ? q : pod, d = ingress ? pod : q;
+            const JobDesc j = ingress ? jd : job_desc(pods[d], cfgs[c], k - int(off[c]));
+            if (j.status != ST_VALID) continue;
+            const Traffic tr = job_traffic(h->res, pods[s], pods[d], j);
+            if (Policy::allowed_given(matching, ingress ? tr.src : tr.dst, tr)) row[q / 64] |= 1ull << (q % 64);
+          }
+        } catch (GoPanic& p) {
+          rc[t] = 1;
+          msg[t] = p.msg;
+        }
+      });
+    }
+    for (auto& th : pool) th.join();
+    for (int t = 0; t < threads; t++)
+      if (rc[t]) {
+        set_err(err, errcap, msg[t]);
+        return 1;
+      }
+    return 0;
+  } catch (std::exception& e) {
+    set_err(err, errcap, e.what());
+    return -1;
+  }
+}
+
 static std::vector<Traffic> decode_traffics(const char* traffic_json) {
   VP v = ojson::parse(traffic_json);
   auto peer = [](const Value* p) {

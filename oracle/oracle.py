@@ -48,6 +48,7 @@ def lib():
         L.orc_probe_run.argtypes = [vp, c, vp, vp, vp, ctypes.POINTER(ctypes.c_longlong), c, sz]
         L.orc_probe_cells.argtypes = [vp, c, vp, vp, vp, i, vp, c, sz]
         L.orc_probe_cells_mt.argtypes = [vp, c, vp, vp, vp, i, vp, i, c, sz]
+        L.orc_probe_row.argtypes = [vp, c, i, i, i, vp, i, c, sz]
         L.orc_query_traffic.argtypes = [vp, c, vp, i, c, sz]
         L.orc_query_traffic_targets.argtypes = [vp, c, c, sz, c, sz]
         L.orc_query_targets.argtypes = [vp, c, c, sz, c, sz]
@@ -128,6 +129,20 @@ class Oracle:
         err = ctypes.create_string_buffer(4096)
         rc = lib().orc_probe_cells_mt(self._h, _j(probes), s.ctypes.data, d.ctypes.data, k.ctypes.data, len(s),
                                       out.ctypes.data, int(threads), err, 4096)
+        if rc != 0:
+            raise ValueError(err.value.decode())
+        return out
+
+    def row(self, probes, direction: str, pod: int, k: int, threads: int = 1):
+        """One plane row as u64[W]: "ingress" = row of destination `pod` (bits over sources),
+        "egress" = row of source `pod` (bits over destinations), job slot k."""
+        P, _ = self.shape(probes)
+        out = np.zeros((P + 63) // 64, np.uint64)
+        err = ctypes.create_string_buffer(4096)
+        rc = lib().orc_probe_row(self._h, _j(probes), 0 if direction == "ingress" else 1, int(pod), int(k),
+                                 out.ctypes.data, int(threads), err, 4096)
+        if rc == 1:
+            raise OraclePanic(err.value.decode())
         if rc != 0:
             raise ValueError(err.value.decode())
         return out

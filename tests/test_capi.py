@@ -33,3 +33,85 @@ def test_no_gpu_paths_fail_cleanly():
     rc = _lib.lib().cyc_probe_run(e._ctx, None, None, None, None, 0, 0)
     assert rc == _lib.ERR_ARG
     assert b"prepare" in _lib.lib().cyc_last_error(e._ctx)
+
+
+def test_json_depth_limit_and_last_key_wins():
+    """encoding/json semantics at the boundary: documents nested deeper than 10000 are refused
+    (not a stack overflow), and among keys that name one struct field the last one wins."""
+    from cyclonus_amd.engine import Engine
+
+    e = Engine(0)
+    deep = b"[" * 20000 + b"]" * 20000
+    rc = _lib.lib().cyc_policy_build_json(e._ctx, 1, deep, len(deep))
+    assert rc == _lib.ERR_JSON and b"max depth" in _lib.lib().cyc_last_error(e._ctx)
+    ok = b"[" * 9000 + b"]" * 9000  # within the limit: parses (an empty policy list nested)
+    assert _lib.lib().cyc_resources_load_json(e._ctx, ok, len(ok)) in (_lib.OK, _lib.ERR_JSON)
+    pol = [{"metadata": {"name": "p", "namespace": "a", "Namespace": "b"},
+            "spec": {"podSelector": {}, "policyTypes": ["Ingress"]}}]
+    ir = e.build_policies(pol).policy_ir()
+    ns = [t["Namespace"] for t in ir["Ingress"].values()]
+    assert ns == ["b"], ir
+
+
+def test_malformed_inputs_fail_cleanly():
+    """Random truncations / byte flips of valid documents: every entry point returns a status (the
+    sanitizer run of this file, tests/test_sanitized.py, checks there is no memory error either)."""
+    import json
+    import random
+
+    from cyclonus_amd.engine import Engine
+
+    c = json.load(open(os.path.join(ROOT, "tests", "golden", "config1.json")))
+    docs = [json.dumps(c["policies"]).encode(), json.dumps(c["resources"]).encode()]
+    e = Engine(0)
+    L = _lib.lib()
+    rng = random.Random(5)
+    for i in range(400):
+        d = bytearray(docs[i % 2])
+        op = rng.randrange(3)
+        if op == 0:
+            d = d[: rng.randrange(len(d))]
+        elif op == 1:
+            for _ in range(rng.randrange(1, 6)):
+                d[rng.randrange(len(d))] = rng.choice(b'{}[]",:\\0aZ-9 \x00\xff')
+        else:
+            x = rng.randrange(len(d))
+            d = d[:x] + d[x: x + rng.randrange(1, 40)] * rng.randrange(2, 5) + d[x:]
+        b = bytes(d)
+        for fn in (L.cyc_policy_build_json, L.cyc_policy_load_ir_json, L.cyc_resources_load_json):
+            rc = fn(e._ctx, 1, b, len(b)) if fn is L.cyc_policy_build_json else fn(e._ctx, b, len(b))
+            assert rc in (_lib.OK, _lib.ERR_JSON, _lib.ERR_INVALID_POLICY, _lib.ERR_ARG), (i, rc)
+
+
+def _driver_inputs(tmp_path, pols, res, probes):
+    import json
+
+    paths = []
+    for name, doc in (("pols", pols), ("res", res), ("probes", probes)):
+        p = tmp_path / f"{name}.json"
+        p.write_text(json.dumps(doc))
+        paths.append(str(p))
+    return paths
+
+
+def test_cpp_driver_compile_path(tmp_path):
+    """The C++ client of the C ABI (stand-in for the cgo binding) compiles a policy and exports the
+    same json.Marshal(*Policy) as the Python binding; a panicking build reports the Go panic text."""
+    import json
+    import subprocess
+
+    from cyclonus_amd import build
+    from cyclonus_amd.engine import Engine
+
+    drv = build.build_driver()
+    c = json.load(open(os.path.join(ROOT, "tests", "golden", "config1.json")))
+    args = _driver_inputs(tmp_path, c["policies"], c["resources"], c["probes"])
+    r = subprocess.run([drv, *args, "--no-gpu"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    ir = json.loads(r.stdout.split("ir ", 1)[1])
+    assert ir == Engine(0).build_policies(c["policies"]).policy_ir()
+    bad = [{"metadata": {"name": "p", "namespace": "x"},
+            "spec": {"podSelector": {}, "policyTypes": ["Ingress"], "ingress": [{"ports": [{"port": "x", "endPort": 9}]}]}}]
+    args = _driver_inputs(tmp_path, bad, c["resources"], c["probes"])
+    r = subprocess.run([drv, *args, "--no-gpu"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3 and r.stdout.startswith("error cyc_policy_build_json rc=3"), r.stdout

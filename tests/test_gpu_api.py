@@ -9,7 +9,7 @@ import pytest
 
 from cyclonus_amd._lib import CyclonusPanic
 from cyclonus_amd.matcher import build_network_policies
-from cyclonus_amd.probe import Resources, Table, new_all_available, new_probe_config, new_simulated_runner
+from cyclonus_amd.probe import PlaneCells, Resources, Table, new_all_available, new_probe_config, new_simulated_runner
 from oracle.oracle import Oracle, OraclePanic
 from randgen import KEYS, NS, VALS, random_problem
 
@@ -129,7 +129,7 @@ def test_runner_tables_match_oracle_render(gpu):
     tables = runner.run_probes(c["probes"], res)
     st, inp, egp = Oracle(c["policies"], c["resources"]).probe(c["probes"])
     for i, (t, p) in enumerate(zip(tables, c["probes"])):
-        o = Table(res, new_probe_config(p["Port"], p["Protocol"]), st, inp, egp, i, i + 1)
+        o = Table(res, new_probe_config(p["Port"], p["Protocol"]), PlaneCells(st, inp, egp), i, i + 1)
         for fn in ("render_ingress", "render_egress", "render_table"):
             assert getattr(t, fn)() == getattr(o, fn)()
     assert tables[0].render_table() == c["readme_combined_tcp80"]["text"]
@@ -147,7 +147,7 @@ def test_runner_all_available_and_named(gpu):
     lo = 0
     for t, p in zip(tables, probes):
         n = maxc if p.all_available else 1
-        o = Table(res, p, st, inp, egp, lo, lo + n)
+        o = Table(res, p, PlaneCells(st, inp, egp), lo, lo + n)
         lo += n
         for fr, to in t.keys():
             assert t.get(fr, to) == o.get(fr, to)
@@ -158,3 +158,21 @@ def test_runner_all_available_and_named(gpu):
                 t.render_table()
             continue
         assert t.render_table() == want
+
+
+def test_config1_through_yaml_loader(gpu, tmp_path):
+    """analyze --mode probe's input path: the policy directory (cli/utils.go:14-60, YAML written
+    from the committed fixture with quoted strings, as networkpolicies/simple-example quotes "y")
+    -> BuildNetworkPolicies -> GPU table -> README.md:294-313 byte for byte."""
+    import yaml
+
+    from cyclonus_amd.loader import read_policies_from_path
+
+    c = json.load(open(os.path.join(GOLD, "config1.json")))
+    for p in c["policies"]:
+        (tmp_path / f"{p['metadata']['name']}.yaml").write_text(yaml.safe_dump(p, default_style='"'))
+    pols = read_policies_from_path(str(tmp_path))
+    assert sorted(json.dumps(p, sort_keys=True) for p in pols) == sorted(json.dumps(p, sort_keys=True) for p in c["policies"])
+    runner = new_simulated_runner(build_network_policies(True, pols))
+    table = runner.run_probe_for_config(new_probe_config(80, "TCP"), Resources.from_json(c["resources"]))
+    assert table.render_table() == c["readme_combined_tcp80"]["text"]

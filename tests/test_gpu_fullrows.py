@@ -1,0 +1,71 @@
+"""Whole plane rows at full size (configs #3 and #4): complete ingress rows (one destination, every
+source, every slot) and egress rows (one source, every destination, every slot) from the device
+table equal the oracle's rows bit for bit — rows from the first / last positions, 64-pod word
+edges, the most populous identities (largest classes) and random positions, on the whole table and
+on row shards (row_lo > 0)."""
+import json
+from collections import Counter
+
+import numpy as np
+import pytest
+
+from cyclonus_amd import synth
+from cyclonus_amd.engine import Engine
+from cyclonus_amd.shard import row_range
+from oracle.oracle import Oracle
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("gpu")]
+THREADS = 16
+
+
+def _pick_rows(res, lo, hi, n_random, seed):
+    pods = res["Pods"][lo:hi]
+    ident = [(p["Namespace"], tuple(sorted((p.get("Labels") or {}).items()))) for p in pods]
+    top = [i for i, _ in Counter(ident).most_common(3)]
+    rows = {0, 1, 63, 64, 65, len(pods) // 2, len(pods) - 64, len(pods) - 1}
+    for t in top:  # first and last pod of the largest identities
+        idx = [i for i, x in enumerate(ident) if x == t]
+        rows |= {idx[0], idx[-1]}
+    rng = np.random.default_rng(seed)
+    rows |= set(int(x) for x in rng.integers(0, len(pods), n_random))
+    return sorted(lo + r for r in rows if 0 <= r < len(pods))
+
+
+def _check(name, kw, shards):
+    import torch
+
+    data = synth.CONFIGS[name](**kw)
+    eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
+    sh = eng.prepare(data["probes"])
+    P, K, W = sh["pods"], sh["slots"], sh["words"]
+    orc = Oracle(data["policies"], data["resources"])
+    for world, rank in shards:
+        lo, hi = row_range(P, world, rank)
+        rows = hi - lo
+        d_in = torch.empty((rows, K, W), dtype=torch.int64, device="cuda")
+        d_eg = torch.empty((rows, K, W), dtype=torch.int64, device="cuda")
+        d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
+        eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), torch.cuda.current_stream().cuda_stream, lo, hi)
+        torch.cuda.synchronize()
+        picks = _pick_rows(data["resources"], lo, hi, 6, seed=world * 100 + rank)
+        idx = torch.as_tensor([p - lo for p in picks], device="cuda")
+        g_in = d_in[idx].cpu().numpy().view(np.uint64)
+        g_eg = d_eg[idx].cpu().numpy().view(np.uint64)
+        del d_in, d_eg
+        torch.cuda.empty_cache()
+        for x, pod in enumerate(picks):
+            for k in range(K):
+                want_in = orc.row(data["probes"], "ingress", pod, k, threads=THREADS)
+                want_eg = orc.row(data["probes"], "egress", pod, k, threads=THREADS)
+                for plane, got, want in (("ingress", g_in[x, k], want_in), ("egress", g_eg[x, k], want_eg)):
+                    bad = np.nonzero(got != want)[0]
+                    assert bad.size == 0, (f"{name} shard {rank}/{world} {plane} row {pod} slot {k}: "
+                                           f"{bad.size} words differ, first at word {int(bad[0])}")
+
+
+def test_config3_full_rows():
+    _check("config3", {}, [(1, 0), (8, 3)])
+
+
+def test_config4_full_rows():
+    _check("config4", {}, [(1, 0), (4, 3)])

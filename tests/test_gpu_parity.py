@@ -469,3 +469,35 @@ def test_launch_modes_and_knobs(gpu):
         return
     if eng_b.shape.get("may_panic"):
         assert eng_b.get_option("front_fused_active") == 0
+
+
+def test_batch_cross_block_panic_isolated(gpu):
+    """Block B holds a pod with an unparsable IP and no IPBlock rule; block A has an IPBlock peer.
+    Neither panics alone, the combined problem does (cross-block cells): Batch.run must still give
+    each block its own stand-alone table; a block that panics alone reports its own panic."""
+    from cyclonus_amd.batch import Batch
+
+    def pod(ns, name, ip):
+        return {"Namespace": ns, "Name": name, "Labels": {"app": name}, "IP": ip,
+                "Containers": [{"Name": "c", "Port": 80, "Protocol": "TCP", "PortName": "serve-80-tcp"}]}
+
+    a = {"policies": [{"metadata": {"name": "ipb", "namespace": "x"},
+                       "spec": {"podSelector": {}, "policyTypes": ["Ingress"],
+                                "ingress": [{"from": [{"ipBlock": {"cidr": "10.0.0.0/8"}}]}]}}],
+         "resources": {"Namespaces": {"x": {"ns": "x"}}, "Pods": [pod("x", "a", "10.0.0.1"), pod("x", "b", "10.0.0.2")]},
+         "probe": {"Port": 80, "Protocol": "TCP"}}
+    b = {"policies": [{"metadata": {"name": "deny", "namespace": "y"},
+                       "spec": {"podSelector": {"matchLabels": {"app": "c"}}, "policyTypes": ["Ingress"]}}],
+         "resources": {"Namespaces": {"y": {"ns": "y"}}, "Pods": [pod("y", "c", "not-an-ip"), pod("y", "d", "10.1.0.1")]},
+         "probe": {"Port": 80, "Protocol": "TCP"}}
+    c = {"policies": a["policies"], "resources": {"Namespaces": {"x": {}}, "Pods": [pod("x", "e", "bad"), pod("x", "f", "10.0.0.9")]},
+         "probe": {"AllAvailable": True}}
+    eng = Engine(0)
+    got = Batch([a, b, c]).run(eng)
+    for blk, g in zip((a, b, c), got):
+        try:
+            want = Oracle(blk["policies"], blk["resources"]).probe([blk["probe"]])
+        except OraclePanic as e:
+            want = Panicked(str(e))
+        assert_same(want, Panicked(g.msg) if isinstance(g, CyclonusPanic) else g, blk["resources"]["Pods"][0]["Name"])
+    assert isinstance(got[2], CyclonusPanic) and not isinstance(got[0], CyclonusPanic)

@@ -39,8 +39,45 @@ def test_rejects_missing_policy_types_and_unknown_fields(tmp_path):
         read_policies_from_path(str(tmp_path))
 
 
-def test_yaml11_booleans_like_go_yaml_v2(tmp_path):
-    # an unquoted `namespace: y` is a boolean for go-yaml v2, so the reference cannot load it
-    (tmp_path / "x.yaml").write_text("kind: NetworkPolicy\nmetadata: {name: a, namespace: y}\nspec: {podSelector: {}, policyTypes: [Ingress]}\n")
-    with pytest.raises(PolicyLoadError):
-        read_policies_from_path(str(tmp_path))
+def _one(tmp_path, text):
+    (tmp_path / "x.yaml").write_text(text)
+    return read_policies_from_path(str(tmp_path))
+
+
+POL = "kind: NetworkPolicy\nmetadata: {name: a, namespace: %s}\nspec: {podSelector: {}, policyTypes: [Ingress]}\n"
+
+
+def test_yaml11_scalars_coerced_into_string_fields(tmp_path):
+    """sigs.k8s.io/yaml v1.2.0 convertToJSONableObject: YAML 1.1 bools / ints / floats landing in Go
+    string fields become their text (parity unpinned: no reference fixture has them unquoted)."""
+    for raw, want in (("y", "true"), ("Yes", "true"), ("off", "false"), ("010", "8"), ("0x1F", "31"), ("1_000", "1000"),
+                      ("1.5", "1.5"), ("1e6", "1e+06"), ("100000.0", "100000"), ("0.1", "0.1"), ("2001-12-14", "2001-12-14"),
+                      ("'y'", "y"), ("x-y", "x-y")):
+        got = _one(tmp_path, POL % raw)
+        assert got[0]["metadata"]["namespace"] == want, raw
+    got = _one(tmp_path, "kind: NetworkPolicy\nmetadata: {name: a, labels: {y: on, 7: 2.50}}\n"
+                         "spec: {podSelector: {matchLabels: {n: 3}}, policyTypes: [Ingress],"
+                         " ingress: [{ports: [{port: 80}, {port: '81', protocol: UDP}]}]}\n")
+    assert got[0]["metadata"]["labels"] == {"true": "true", "7": "2.5"}
+    assert got[0]["spec"]["podSelector"]["matchLabels"] == {"false": "3"}
+    assert got[0]["spec"]["ingress"][0]["ports"] == [{"port": 80}, {"port": "81", "protocol": "UDP"}]  # intstr: no coercion
+
+
+def test_first_document_only_and_strictness(tmp_path):
+    two = POL % "one" + "---\n" + POL % "two"
+    assert [p["metadata"]["namespace"] for p in _one(tmp_path, two)] == ["one"]
+    # UnmarshalStrict: unknown fields at any depth and duplicate keys are errors for a single policy...
+    for bad in ("kind: NetworkPolicy\nspec: {podSelectr: {}, policyTypes: [Ingress]}\n",
+                "kind: NetworkPolicy\nstatus: {}\nspec: {policyTypes: [Ingress]}\n",
+                "kind: NetworkPolicy\nkind: NetworkPolicy\nspec: {policyTypes: [Ingress]}\n",
+                "kind: NetworkPolicy\nspec: {policyTypes: Ingress}\n"):
+        with pytest.raises(PolicyLoadError, match="unable to unmarshal single policy"):
+            _one(tmp_path, bad)
+    # ...while the list form (yaml.Unmarshal) drops unknown fields and lets a later key win
+    got = _one(tmp_path, "- kind: NetworkPolicy\n  metadata: {name: a, name: b}\n"
+                         "  spec: {podSelectr: {}, policyTypes: [Egress]}\n")
+    assert got == [{"kind": "NetworkPolicy", "metadata": {"name": "b"}, "spec": {"policyTypes": ["Egress"]}}]
+    # field names match case-insensitively; the last key naming a field wins
+    got = _one(tmp_path, "Kind: NetworkPolicy\nMetadata: {Name: a, namespace: p, Namespace: q}\nSPEC: {policyTypes: [Ingress]}\n")
+    assert got[0]["metadata"] == {"name": "a", "namespace": "q"} and got[0]["kind"] == "NetworkPolicy"
+    assert _one(tmp_path, "") == []  # an empty file is an empty list

@@ -4,7 +4,7 @@ import os
 
 import numpy as np
 
-from cyclonus_amd.probe import Resources, Table, new_probe_config
+from cyclonus_amd.probe import PlaneCells, Resources, Table, new_probe_config
 from cyclonus_amd.tablewriter import render, title
 from oracle import oracle as O
 
@@ -14,7 +14,7 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 def test_readme_table_text_from_oracle_planes():
     c = json.load(open(os.path.join(GOLD, "config1.json")))
     status, inp, egp = O.Oracle(c["policies"], c["resources"]).probe(c["probes"])
-    t = Table(Resources.from_json(c["resources"]), new_probe_config(80, "TCP"), status, inp, egp, 0, 1)
+    t = Table(Resources.from_json(c["resources"]), new_probe_config(80, "TCP"), PlaneCells(status, inp, egp), 0, 1)
     assert t.render_table() == c["readme_combined_tcp80"]["text"]
 
 
