@@ -246,16 +246,16 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = cells / (dt / args.steps)
 
-    # k_emit writes each plane (ingress, egress) of this rank's rows once: rows x K x W x 8 B per
-    # plane = 2 bits per cell.  Merged (default): ONE launch writes both planes; else one launch
-    # per plane.  emit_ms covers every emit launch of the step.
-    launches = 1 if eng.get_option("emit_merged") else 2
-    emit_bytes = rows * K * W * 8 * (2 // launches)
-    emit_launch_ms = emit_ms / launches
+    # the emit writes each plane (ingress, egress) of this rank's rows once, both in ONE launch:
+    # rows x K x W x 8 B per plane = 2 bits per cell
+    launches = 1
+    emit_bytes = rows * K * W * 8 * 2
+    emit_launch_ms = emit_ms
     achieved = emit_bytes / (emit_launch_ms * 1e-3) / 1e9
-    # the emit kernel the library picks by plane-row length (emit_variant -1, engine.hip enq_emit)
+    # the emit kernel the library picks by plane-row length (engine.hip enq_emit)
     row_bytes = K * W * 8
-    emit_kernel = ("k_emit_wide<512,U> (one single-pass block per row)" if row_bytes >= 65536 else
+    emit_kernel = ("k_emit_words (8-byte copies)" if (K * W) % 2 else
+                   "k_emit_wide<512,U> (one single-pass block per row)" if row_bytes >= 65536 else
                    "k_emit_wide<256,U> (one single-pass block per row)" if row_bytes >= 16384 else
                    "k_emit_flat (multi-row blocks)")
 

@@ -14,8 +14,8 @@ SO_PATH = os.environ.get("CYC_HIP_LIB") or os.path.join(_PKG, "libcyclonus_hip.s
 
 # cyc_status
 OK, ERR_ARG, ERR_JSON, ERR_INVALID_POLICY, ERR_PANIC_IP, ERR_PANIC_CIDR, ERR_PANIC_SELECTOR = 0, 1, 2, 3, 4, 5, 6
-ERR_DUPLICATE_KEY, ERR_HIP, ERR_OOM, ERR_RCCL = 7, 8, 9, 10
-PANIC_CODES = (ERR_INVALID_POLICY, ERR_PANIC_IP, ERR_PANIC_CIDR, ERR_PANIC_SELECTOR)
+ERR_DUPLICATE_KEY, ERR_HIP, ERR_OOM, ERR_RCCL, ERR_PANIC_RUNTIME = 7, 8, 9, 10, 11
+PANIC_CODES = (ERR_INVALID_POLICY, ERR_PANIC_IP, ERR_PANIC_CIDR, ERR_PANIC_SELECTOR, ERR_PANIC_RUNTIME)
 
 # cyc_job_status
 JOB_NONE, JOB_VALID, JOB_BAD_NAMED_PORT, JOB_BAD_PORT_PROTOCOL = 0, 1, 2, 3

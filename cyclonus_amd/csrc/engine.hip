@@ -394,10 +394,14 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
 // Also records each IP peer's nonzero word span in rng[2 * peer] (first word) and
 // rng[2 * peer + 1] (~last word), both atomicMin'd from 0xFFFFFFFF: CIDRs are address ranges and
 // pods of a namespace have neighbouring addresses, so a peer's row is mostly zero words the
-// class rows can skip without loading them.
+// class rows can skip without loading them.  Only NONZERO words are stored: cnz[peer][chunk]
+// (one u64 per 64-word chunk, written by the chunk's wave) marks them, and readers AND the PM
+// word with its cnz bit (both loads issued together), so the zero words — most of a row — cost no
+// HBM writes at all.
 __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
                                             const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
-                                            uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng) {
+                                            uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng,
+                                            uint64_t* __restrict__ cnz) {
   bool uniform = true;
   uint64_t res = 0;
   if (valid) {
@@ -420,8 +424,8 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
       }
     }
   }
-  if (valid && uniform) PM[uint64_t(t.peer) * W + w] = res;
-  const uint64_t nz = __ballot(valid && uniform && res != 0);
+  if (valid && uniform && res) PM[uint64_t(t.peer) * W + w] = res;
+  uint64_t nz = __ballot(valid && uniform && res != 0);
   const uint32_t w0 = chunk * 64;
   uint32_t lo = nz ? w0 + __ffsll((unsigned long long)nz) - 1 : 0xFFFFFFFFu;
   uint32_t hi = nz ? w0 + 63 - __clzll((long long)nz) : 0u;
@@ -444,16 +448,25 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
       }
     }
     const uint64_t m = __ballot(o == 1);
-    if (lane == 0) PM[uint64_t(t.peer) * W + ww] = m;
+    if (lane == 0 && m) PM[uint64_t(t.peer) * W + ww] = m;
     if (m) {
+      nz |= 1ull << wl;
       lo = min(lo, ww);
       hi = max(hi, ww);
     }
   }
-  if (lane == 0 && lo != 0xFFFFFFFFu) {
-    atomicMin(&rng[2 * t.peer], lo);
-    atomicMin(&rng[2 * t.peer + 1], ~hi);
+  if (lane == 0) {
+    cnz[uint64_t(t.peer) * ((W + 63) / 64) + chunk] = nz;
+    if (lo != 0xFFFFFFFFu) {
+      atomicMin(&rng[2 * t.peer], lo);
+      atomicMin(&rng[2 * t.peer + 1], ~hi);
+    }
   }
+}
+
+// A nonzero-word mask bit of IP peer j's PM row (see ip_row_word): ~0 if word w was written.
+__device__ __forceinline__ uint64_t cnz_mask(const uint64_t* __restrict__ cnz, uint32_t W, uint32_t j, uint32_t w) {
+  return ((cnz[uint64_t(j) * ((W + 63) / 64) + w / 64] >> (w % 64)) & 1) ? ~0ull : 0ull;
 }
 
 // A block handles one group of `grp` IP peers over 4 chunks of 64 words (a wave per chunk, lane =
@@ -464,7 +477,8 @@ constexpr uint32_t IP_GROUP = 8, IP_GROUP_MAX = 64, IP_EX_LDS = 256;
 __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng, uint32_t bid_, uint32_t nblk_, uint32_t grp = IP_GROUP) {
+                                                      uint32_t* __restrict__ rng, uint64_t* __restrict__ cnz, uint32_t bid_, uint32_t nblk_,
+                                                      uint32_t grp = IP_GROUP) {
   __shared__ DIPTest s_t[IP_GROUP_MAX];
   __shared__ DCidr s_ex[IP_EX_LDS];
   const uint32_t lane = threadIdx.x & 63;
@@ -483,15 +497,26 @@ __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32
   const bool valid = w < W;
   DWordIP wd{};
   if (valid) wd = words[w];
+  // the chunk's own [min, max] per family (records W.. of `words`): a peer whose network misses
+  // the whole chunk leaves all 64 words zero — the wave only clears the chunk's cnz mask
+  const DWordIP ck = words[W + __builtin_amdgcn_readfirstlane(chunk)];
   for (uint32_t r = 0; r < nr; r++) {
     const DIPTest t = s_t[r];
-    ip_row_word(t, ex_lds ? s_ex + (t.exoff - ex0) : ip_ex + t.exoff, pod_ip, wd, valid, w, chunk, P, W, lane, PM, rng);
+    const bool v4 = t.cidr.fam == 4;
+    if (t.cidr.valid && (v4 ? !ck.m4 || span_vs_cidr4(ck.min4, ck.max4, t.cidr) == 0
+                            : !ck.m6 || span_vs_cidr6(ck.min6, ck.max6, t.cidr) == 0)) {
+      if (lane == 0) cnz[uint64_t(t.peer) * ((W + 63) / 64) + chunk] = 0;
+      continue;
+    }
+    ip_row_word(t, ex_lds ? s_ex + (t.exoff - ex0) : ip_ex + t.exoff, pod_ip, wd, valid, w, chunk, P, W, lane, PM, rng, cnz);
   }
 }
 __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng, uint32_t grp) { ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, blockIdx.x, gridDim.x, grp); }
+                                                      uint32_t* __restrict__ rng, uint64_t* __restrict__ cnz, uint32_t grp) {
+  ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, cnz, blockIdx.x, gridDim.x, grp);
+}
 
 // Grid of k_ip_rows_fast / the IP-row range of k_front_b: peer groups x blocks of 4 word chunks.
 __host__ __device__ inline uint64_t ip_rows_blocks(uint32_t Ri, uint32_t W, uint32_t grp) {
@@ -649,12 +674,22 @@ __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t
   uint32_t n = 0, off = a.list_off[i];
   uint8_t e = 0;
   uint64_t h = 0x5bd1e9955bd1e995ull;
-  for (uint32_t t = lo; t < hi; t++) {
-    uint8_t r = a.selres[uint64_t(a.tgt[t].sel) * a.L + ls];
-    if (r == 2) e = 1;
-    if (r == 1) {
-      a.list[off + n++] = t;
-      h = mix64(h ^ (uint64_t(t) + 1));
+  constexpr uint32_t MB = 8;  // targets whose selector results are loaded at once
+  for (uint32_t t0 = lo; t0 < hi; t0 += MB) {
+    uint32_t sel[MB];
+    uint8_t r[MB];
+#pragma unroll
+    for (uint32_t x = 0; x < MB; x++) sel[x] = t0 + x < hi ? a.tgt[t0 + x].sel : 0u;
+#pragma unroll
+    for (uint32_t x = 0; x < MB; x++) r[x] = t0 + x < hi ? a.selres[uint64_t(sel[x]) * a.L + ls] : 0;
+#pragma unroll
+    for (uint32_t x = 0; x < MB; x++) {
+      const uint32_t t = t0 + x;
+      if (r[x] == 2) e = 1;
+      if (r[x] == 1) {  // ascending target id = primary-key order
+        a.list[off + n++] = t;
+        h = mix64(h ^ (uint64_t(t) + 1));
+      }
     }
   }
   if (a.id_desc) {
@@ -803,6 +838,7 @@ struct RowArgs {
   uint32_t* ip_cnt;          // [n_ident] IP peers of the class's targets, listed in ip_list as
   uint4* ip_list;            // (peer, port matcher, first, last nonzero PM word)
   const uint32_t* ip_rng;    // [R][2] first word, ~last word of each IP peer's nonzero PM words (no-panic runs)
+  const uint64_t* ip_cnz;    // [R][W/64] which PM words of an IP peer were written (no-panic runs)
   uint32_t E, EW, NB;
   uint32_t rpb;              // IDO class rows: representatives per block (class_rows_ido_blk)
   // the direction's hash table (keys + reps), emptied for the NEXT run by the first class-row
@@ -979,50 +1015,6 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
   if (n == 0) {
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) allow[kk] = ~0ull;  // no target applies: allowed (policy.go:158-160)
-  } else if (!ERR) {
-    // No panic is possible: a cell's verdict is the OR over every peer of every matching target
-    // (target.go:29-36 short-circuits only to save work), so the walk loads the PM words of
-    // PEER_BATCH peers at once instead of one dependent load per peer, and drops the early exit.
-    const uint32_t* lst = a.list + a.list_off[i];
-    bool all = false;
-    for (uint32_t tj = 0; tj < n && !all; tj++) {
-      const DTarget tg = a.tgt[lst[tj]];
-      const uint32_t pend = tg.poff + tg.pcnt;
-      for (uint32_t j0 = tg.poff; j0 < pend; j0 += PEER_BATCH) {
-        uint64_t pm[PEER_BATCH];
-        uint32_t port[PEER_BATCH], pbits[PEER_BATCH];
-#pragma unroll
-        for (uint32_t u = 0; u < PEER_BATCH; u++) {
-          const uint32_t j = j0 + u;
-          pm[u] = 0;
-          port[u] = 0;
-          pbits[u] = 0;
-          if (j < pend) {
-            const DPeer pr = a.peers[j];
-            port[u] = pr.port;
-            if (EGRESS && a.portbits && pr.kind != 0) pbits[u] = a.portbits[pr.port];  // AllPeers: port = CYC_ALL
-            if (pr.kind == 0) all = true;  // AllPeersMatcher: every valid cell allowed
-            else if (pr.kind == 1) pm[u] = ~0ull;  // PortsForAllPeers
-            else if (pr.kind == 2 || (w >= a.ip_rng[2 * j] && w <= ~a.ip_rng[2 * j + 1]))
-              pm[u] = a.PM[uint64_t(j) * a.W + w];
-          }
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < PEER_BATCH; u++) {
-          if (!pm[u]) continue;
-          const uint8_t* pok = a.portok + uint64_t(port[u]) * a.D;
-#pragma unroll
-          for (int kk = 0; kk < KC; kk++) {
-            if (EGRESS && a.portbits && du[kk] >= 0) allow[kk] |= ((pbits[u] >> du[kk]) & 1u) ? pm[u] : 0ull;
-            else allow[kk] |= pm[u] & port_mask<EGRESS>(a, pok, du[kk], k0 + kk, w);
-          }
-        }
-      }
-    }
-    if (all) {
-#pragma unroll
-      for (int kk = 0; kk < KC; kk++) allow[kk] = ~0ull;
-    }
   } else if (n != 0xFFFFFFFFu) {
     const uint32_t* lst = a.list + a.list_off[i];
     for (uint32_t tj = 0; tj < n; tj++) {
@@ -1080,29 +1072,20 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
   }
 }
 
-// Grid = rep_blocks x slot chunks x 256-word chunks; block rows stride over the compacted class
-// representatives (their number is only known on the device), so no block is spent on the
-// identities that merely share a class.
-// LOOP = false: one block row per representative slot (rep_blocks >= the count of identities;
-// surplus rows exit at once) — keeps the per-word body loop-free, which the egress variant
-// needs to stay at 3 waves/SIMD.
-template <bool EGRESS, bool ERR, int KC, bool LOOP>
-__device__ __forceinline__ void class_rows_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
-  ht_clear_slice(a, bid_, nblk_);
+// Panic-capable builds (ordered walk with panic bits).  Grid = representative slots x slot chunks
+// x 256-word chunks: one block row per representative slot (the count of classes is only known on
+// the device; surplus rows exit at once), 8 job slots per thread.
+template <bool EGRESS>
+__global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
+  constexpr int KC = 8;
+  ht_clear_slice(a, blockIdx.x, gridDim.x);
   const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
-  const uint32_t kc = (bid_ / chunks) % nkc;
-  const uint32_t w = (bid_ % chunks) * 256 + threadIdx.x;
+  const uint32_t kc = (blockIdx.x / chunks) % nkc;
+  const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
   if (w >= a.W) return;
-  const uint32_t n_reps = *a.rep_cnt + 1u;
-  uint32_t r = bid_ / (chunks * nkc);
-  if (LOOP) {
-    for (; r < n_reps; r += a.rep_blocks) class_row_word<EGRESS, ERR, KC>(a, a.reps[r], kc, w);
-  } else if (r < n_reps) {
-    class_row_word<EGRESS, ERR, KC>(a, a.reps[r], kc, w);
-  }
+  const uint32_t r = blockIdx.x / (chunks * nkc);
+  if (r < *a.rep_cnt + 1u) class_row_word<EGRESS, true, KC>(a, a.reps[r], kc, w);
 }
-template <bool EGRESS, bool ERR, int KC, bool LOOP>
-__global__ __launch_bounds__(256) void k_class_rows(RowArgs a) { class_rows_blk<EGRESS, ERR, KC, LOOP>(a, blockIdx.x, gridDim.x); }
 
 // Class rows of PM builds without a panic.  Block = class representative (blocks stride over
 // them).  The block first flattens the class's peers cooperatively into LDS — lanes over its
@@ -1115,14 +1098,135 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) { class_rows_blk<
 // (peermatcher.go:18) allows every valid cell; no matching target allows (policy.go:158-160).
 // Lists longer than the LDS part spill into the identity's ip_list slot (sized for every peer of
 // its namespace's targets).
-constexpr uint32_t PL_LDS = 512, PL_TGT = 128, PL_BATCH = 8;
+#ifndef CYC_PL_BATCH
+#define CYC_PL_BATCH 8  // list entries whose PM words are loaded at once (16: occupancy 6 -> 4)
+#endif
+#ifndef CYC_PL_THREADS
+#define CYC_PL_THREADS 128  // threads per class-row block (one representative per block)
+#endif
+constexpr uint32_t PL_LDS = 256, PL_TGT = 64, PL_BATCH = CYC_PL_BATCH, PL_THREADS = CYC_PL_THREADS;
 constexpr uint32_t PL_SKIP = 0xFFFFFFFEu, PL_ONES = 0xFFFFFFFFu;  // entry rows: zero row / PortsForAllPeers
+constexpr uint32_t PL_IP = 0x80000000u;
+
+// PM word of list entry e for pod word w (0 outside the entry's span)
+__device__ __forceinline__ uint64_t pl_word(const RowArgs& a, const uint4& e, uint32_t w) {
+  if (e.x == PL_ONES) return ~0ull;
+  const uint32_t lo = e.z & ~PL_IP;
+  if (e.x == PL_SKIP || w < lo || w > e.w) return 0ull;
+  const uint64_t v = a.PM[uint64_t(e.x) * a.W + w];
+  return (e.z & PL_IP) ? v & cnz_mask(a.ip_cnz, a.W, e.x, w) : v;
+}
 struct PlShared {  // one per block, shared by both directions' instantiations of a fused launch
   uint4 e[PL_LDS];        // (row, port matcher, first word, last word)
   uint32_t bits[PL_LDS];  // port test bits
   uint32_t pre[PL_TGT + 1], poff[PL_TGT];
   uint32_t all;
 };
+
+#ifndef CYC_PL_ITEMS
+#define CYC_PL_ITEMS 2
+#endif
+constexpr int PL_ITEMS = CYC_PL_ITEMS;
+
+// PL_ITEMS (slot chunk, pod word) items of class representative i: items it0, it0 + blockDim.x, ...
+template <bool EGRESS>
+__device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, const uint4* spill, uint32_t i, uint32_t m,
+                                         bool allow_all, bool kbits, uint32_t it0, uint32_t items, uint64_t lastmask) {
+  constexpr int KC = 4, NI = PL_ITEMS;
+  uint64_t valid[NI][KC], allow[NI][KC];
+  int32_t du[NI][KC];
+  uint32_t w[NI], k0[NI];
+  bool fast = kbits;
+#pragma unroll
+  for (int q = 0; q < NI; q++) {
+    const uint32_t it = it0 + q * blockDim.x;
+    const bool live = it < items;
+    const uint32_t kc = live ? it / a.W : 0u;
+    w[q] = live ? it - kc * a.W : 0u;
+    k0[q] = live ? kc * KC : a.K;  // a dead item has no slot
+#pragma unroll
+    for (int kk = 0; kk < KC; kk++) {
+      const uint32_t k = k0[q] + kk;
+      valid[q][kk] = 0;
+      du[q][kk] = -2;
+      if (k < a.K) {
+        if (EGRESS) {
+          valid[q][kk] = a.VALID[uint64_t(k) * a.W + w[q]];
+          du[q][kk] = a.DESCW[uint64_t(k) * a.W + w[q]];
+        } else {
+          const bool v = a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID;
+          valid[q][kk] = v ? (w[q] == a.W - 1 ? lastmask : ~0ull) : 0ull;
+          du[q][kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
+        }
+      }
+      fast = fast && du[q][kk] != -1;  // -1: egress word whose destinations mix descriptors
+      allow[q][kk] = allow_all ? ~0ull : 0ull;
+    }
+  }
+  if (!allow_all && fast) {
+    // the entries are the same for every thread of the block: their fields are read once per wave
+    // into scalar registers; entries without a passing slot were dropped at build time
+    for (uint32_t x0 = 0; x0 < m; x0 += PL_BATCH) {
+      uint64_t pm[NI][PL_BATCH];
+      uint32_t bits[PL_BATCH];
+#pragma unroll
+      for (uint32_t u = 0; u < PL_BATCH; u++) {
+        const uint32_t x = x0 + u;
+        uint4 e = make_uint4(PL_SKIP, 0u, 1u, 0u);
+        uint32_t b = 0;
+        if (x < min(m, PL_LDS)) {
+          e = sh.e[x];
+          b = sh.bits[x];
+        } else if (x < m) {
+          e = spill[x];
+          b = EGRESS ? a.portbits[e.y] : e.y;
+        }
+        e.x = __builtin_amdgcn_readfirstlane(e.x);
+        e.z = __builtin_amdgcn_readfirstlane(e.z);
+        e.w = __builtin_amdgcn_readfirstlane(e.w);
+        bits[u] = __builtin_amdgcn_readfirstlane(b);
+#pragma unroll
+        for (int q = 0; q < NI; q++) pm[q][u] = pl_word(a, e, w[q]);
+      }
+      uint64_t undecided = 0;
+#pragma unroll
+      for (int q = 0; q < NI; q++)
+#pragma unroll
+        for (int kk = 0; kk < KC; kk++) {
+          if (du[q][kk] < 0) continue;
+          if (EGRESS) {
+#pragma unroll
+            for (uint32_t u = 0; u < PL_BATCH; u++) allow[q][kk] |= ((bits[u] >> uint32_t(du[q][kk])) & 1u) ? pm[q][u] : 0ull;
+          } else {  // ingress: the slot's port test is the same for the whole block
+#pragma unroll
+            for (uint32_t u = 0; u < PL_BATCH; u++)
+              if ((bits[u] >> (k0[q] + kk)) & 1u) allow[q][kk] |= pm[q][u];
+          }
+          undecided |= valid[q][kk] & ~allow[q][kk];
+        }
+      if (!undecided) break;
+    }
+  } else if (!allow_all) {  // mixed descriptors / no bit rows (ingress K > 32): the byte port table
+    for (uint32_t x = 0; x < m; x++) {
+      const uint4 e = x < PL_LDS ? sh.e[x] : spill[x];
+#pragma unroll
+      for (int q = 0; q < NI; q++) {
+        const uint64_t pm = pl_word(a, e, w[q]);
+        if (!pm) continue;
+#pragma unroll
+        for (int kk = 0; kk < KC; kk++)
+          allow[q][kk] |= pm & port_mask<EGRESS>(a, a.portok + uint64_t(e.y) * a.D, du[q][kk], k0[q] + kk, w[q]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NI; q++)
+#pragma unroll
+    for (int kk = 0; kk < KC; kk++) {
+      const uint32_t k = k0[q] + kk;
+      if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w[q]] = allow[q][kk] & valid[q][kk];
+    }
+}
 
 template <bool EGRESS>
 __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
@@ -1167,10 +1271,10 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
           sh.all = 1;  // AllPeersMatcher
         } else {
           en = make_uint4(pr.kind == 1 ? PL_ONES : j, pr.port, 0u, a.W - 1);
-          if (pr.kind == 3) {
-            en.z = a.ip_rng[2 * j];
+          if (pr.kind == 3) {  // bit 31 of z: an IP row (only the cnz-marked words were written)
+            en.z = a.ip_rng[2 * j] | PL_IP;
             en.w = ~a.ip_rng[2 * j + 1];
-            if (en.z == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
+            if (a.ip_rng[2 * j] == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
           }
           if (EGRESS) {
             if (a.portbits) bits = a.portbits[pr.port];
@@ -1181,6 +1285,7 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
             }
           }
           en.y = EGRESS || a.K > 32 ? pr.port : bits;  // spilled entries carry the bits themselves
+          if (kbits && !bits) en.x = PL_SKIP;  // the port matcher passes no slot / descriptor here
         }
         const uint32_t x = m + e;
         if (x < PL_LDS) {
@@ -1195,73 +1300,9 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     }
     const bool allow_all = nt == 0 || sh.all;
     const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
-    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {  // the class's (slot chunk, word) items
-      const uint32_t kc = it / a.W, w = it - kc * a.W, k0 = kc * KC;
-      uint64_t valid[KC], allow[KC];
-      int32_t du[KC];
-      bool fast = kbits;
-#pragma unroll
-      for (int kk = 0; kk < KC; kk++) {
-        const uint32_t k = k0 + kk;
-        valid[kk] = 0;
-        du[kk] = -2;
-        if (k < a.K) {
-          if (EGRESS) {
-            valid[kk] = a.VALID[uint64_t(k) * a.W + w];
-            du[kk] = a.DESCW[uint64_t(k) * a.W + w];
-          } else {
-            const bool v = a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID;
-            valid[kk] = v ? (w == a.W - 1 ? lastmask : ~0ull) : 0ull;
-            du[kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
-          }
-        }
-        fast = fast && du[kk] != -1;  // -1: egress word whose destinations mix descriptors
-        allow[kk] = allow_all ? ~0ull : 0ull;
-      }
-      if (!allow_all && fast) {
-        for (uint32_t x0 = 0; x0 < m; x0 += PL_BATCH) {
-          uint64_t pm[PL_BATCH];
-          uint32_t bits[PL_BATCH];
-#pragma unroll
-          for (uint32_t u = 0; u < PL_BATCH; u++) {
-            const uint32_t x = x0 + u;
-            uint4 e = make_uint4(PL_SKIP, 0u, 1u, 0u);
-            bits[u] = 0;
-            if (x < min(m, PL_LDS)) {
-              e = sh.e[x];
-              bits[u] = sh.bits[x];
-            } else if (x < m) {
-              e = spill[x];
-              bits[u] = EGRESS ? a.portbits[e.y] : e.y;
-            }
-            pm[u] = e.x == PL_ONES ? ~0ull : (e.x != PL_SKIP && w >= e.z && w <= e.w) ? a.PM[uint64_t(e.x) * a.W + w] : 0ull;
-          }
-          uint64_t undecided = 0;
-#pragma unroll
-          for (int kk = 0; kk < KC; kk++) {
-            if (du[kk] < 0) continue;
-            const uint32_t sft = EGRESS ? uint32_t(du[kk]) : k0 + kk;
-#pragma unroll
-            for (uint32_t u = 0; u < PL_BATCH; u++) allow[kk] |= ((bits[u] >> sft) & 1u) ? pm[u] : 0ull;
-            undecided |= valid[kk] & ~allow[kk];
-          }
-          if (!undecided) break;
-        }
-      } else if (!allow_all) {  // mixed descriptors / no bit rows (ingress K > 32): the byte port table
-        for (uint32_t x = 0; x < m; x++) {
-          const uint4 e = x < PL_LDS ? sh.e[x] : spill[x];
-          const uint64_t pm = e.x == PL_ONES ? ~0ull : (e.x != PL_SKIP && w >= e.z && w <= e.w) ? a.PM[uint64_t(e.x) * a.W + w] : 0ull;
-          if (!pm) continue;
-#pragma unroll
-          for (int kk = 0; kk < KC; kk++) allow[kk] |= pm & port_mask<EGRESS>(a, a.portok + uint64_t(e.y) * a.D, du[kk], k0 + kk, w);
-        }
-      }
-#pragma unroll
-      for (int kk = 0; kk < KC; kk++) {
-        const uint32_t k = k0 + kk;
-        if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
-      }
-    }
+    // the class's (slot chunk, word) items, PL_ITEMS per thread at once (their loads overlap)
+    for (uint32_t it0 = threadIdx.x; it0 < items; it0 += PL_ITEMS * blockDim.x)
+      pl_items<EGRESS>(a, sh, spill, i, m, allow_all, kbits, it0, items, lastmask);
     __syncthreads();  // LDS reused by the next representative
   }
 }
@@ -1361,7 +1402,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
           const uint4 jp = il[x0 + u];
           port[u] = jp.y;
           if (EGRESS && a.portbits) pbits[u] = a.portbits[jp.y];  // block-uniform: one scalar load per peer
-          if (w >= jp.z && w <= jp.w) pm[u] = a.PM[uint64_t(jp.x) * a.W + w];  // inside the peer's nonzero words
+          if (w >= jp.z && w <= jp.w)  // inside the peer's nonzero words
+            pm[u] = a.PM[uint64_t(jp.x) * a.W + w] & cnz_mask(a.ip_cnz, a.W, jp.x, w);
         }
       }
       uint64_t undecided = 0;
@@ -1443,6 +1485,7 @@ struct FrontB {
   const DWordIP* words;
   uint64_t* PM;
   uint32_t* rng;
+  uint64_t* cnz;
   uint32_t Ru, E, EW, L;
   const uint32_t* pod_peers_u;
   const DPeer* peers;
@@ -1454,7 +1497,7 @@ struct FrontB {
 };
 __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   uint32_t b = blockIdx.x;
-  if (b < f.nb[0]) return ip_rows_fast_blk(f.Ri, f.P, f.W, f.tests, f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, b, f.nb[0], f.ip_grp);
+  if (b < f.nb[0]) return ip_rows_fast_blk(f.Ri, f.P, f.W, f.tests, f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, f.cnz, b, f.nb[0], f.ip_grp);
   b -= f.nb[0];
   if (b < f.nb[1]) {
     if (f.pod_direct)
@@ -1504,46 +1547,43 @@ __global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
 }
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
-// tail is made of the shorter ingress blocks
-template <int KCE>  // egress job slots per thread (class_variant_eg bit 0: 4, else 8)
+// tail is made of the shorter ingress blocks (4 job slots per thread: profiles/r01_front_e_kc_ab.txt)
 __global__ __launch_bounds__(256) void k_front_e(FrontRows f) {
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_ido_blk<true, KCE>(f.ra[1], b, f.nb[1]);
+  if (b < f.nb[1]) class_rows_ido_blk<true, 4>(f.ra[1], b, f.nb[1]);
   else class_rows_ido_blk<false, 4>(f.ra[0], b - f.nb[1], f.nb[0]);
 }
 
-// The HBM-bound kernel: every target pod's plane rows are a copy of its class rows.
-// One block per pod.  Blocks are dealt round-robin over the 8 XCDs, so block b works on row
-// (b % 8) * per_xcd + b / 8: each XCD streams a contiguous, class-clustered range of rows and
-// re-reads a class row from its own L2.  16-byte non-temporal stores when the pitch allows.
-// One launch writes `planes` planes (1, or 2 = ingress then egress rows as one row list).
+// The HBM-bound kernel: every target pod's plane rows are a copy of its class rows.  ONE launch
+// writes both planes (and the status plane, in block slices).  The row list is the planes' row
+// orders (pods clustered by class) one after the other, or, for planes of >= 8 GB, alternating
+// ingress / egress rows so every XCD writes into both planes; it is cut into 8 contiguous
+// segments, one per XCD (block b runs on XCD b % 8), so an XCD streams a class-clustered range and
+// re-reads a class row from its own L2.  Stores are non-temporal 16-byte writes.
+// (Measured and dropped in round 1: persistent grids, chunked XCD deals, rows-per-block groups,
+// plain / sc1 stores, address-linear fill-like segments, per-plane launches —
+// profiles/r01_emit_*.txt.)
 struct EmitArgs {
   uint32_t n_rows;            // pods in [row_lo, row_hi) per plane
-  uint32_t planes;
   uint32_t row_lo;
-  uint32_t per_xcd;           // of the planes * n_rows row list
+  uint32_t per_xcd;           // rows of the 2 * n_rows row list per XCD segment
   const uint32_t* order[2];   // pods in [row_lo,row_hi) clustered by the plane's class
   const uint32_t *pod_id[2], *class_of[2];
   const uint64_t* A[2];
   uint64_t* out[2];
   uint64_t row_words;         // K * W
-  uint32_t blocks_per_xcd;    // persistent launch: blocks of one XCD stride over its row segment
-  uint32_t chunk;             // CHUNK variant: rows per XCD chunk
+  uint32_t chunk;             // k_emit_flat: rows per block
   const uint8_t* st_src;      // job status plane [P][K] (the run's third output), copied by the
   uint8_t* st_dst;            // emit's blocks in slices: no separate copy node ends the step
   uint64_t st_bytes;
-  uint32_t interleave;        // two planes: the row list alternates ingress / egress rows
-  uint32_t deal;              // k_emit_wide: rows dealt to the XCDs in chunks of `chunk` (else segments)
+  uint32_t interleave;        // the row list alternates ingress / egress rows
 };
 
-// Row r of a launch's row list -> (plane, pod).  The list is the planes' class-clustered row
-// orders, one after the other, or (interleave, two planes) alternating ingress / egress rows, so
-// every XCD's segment of the list writes into both planes.
+// Row r of the row list -> (plane, pod).
 __device__ __forceinline__ void emit_row_of(const EmitArgs& a, uint32_t r, uint32_t& pl, uint32_t& p) {
   if (a.interleave) {
     pl = r & 1u;
-    const uint32_t idx = r >> 1;
-    p = a.order[pl][idx];
+    p = a.order[pl][r >> 1];
   } else {
     pl = r >= a.n_rows ? 1u : 0u;
     p = a.order[pl][r - pl * a.n_rows];
@@ -1560,145 +1600,36 @@ __device__ __forceinline__ void emit_status(const EmitArgs& a) {
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
-template <bool VEC, int UNROLL, bool NT>
-__device__ __forceinline__ void emit_row(const EmitArgs& a, uint32_t r) {
+// Rows of an odd word count or planes not 16-byte aligned: 8-byte copies, one block per row.
+__global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
+  emit_status(a);
+  const uint32_t b = blockIdx.x, x = b & 7, r = x * a.per_xcd + (b >> 3);
+  if (r >= min(2 * a.n_rows, (x + 1) * a.per_xcd)) return;
   uint32_t pl, p;
   emit_row_of(a, r, pl, p);
   const uint64_t* src = a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words;
   uint64_t* dst = a.out[pl] + uint64_t(p - a.row_lo) * a.row_words;
-  if (VEC) {
-    const uint64_t n2 = a.row_words / 2;
-    const u64x2* si = reinterpret_cast<const u64x2*>(src);
-    u64x2* di = reinterpret_cast<u64x2*>(dst);
-    const uint64_t step = uint64_t(blockDim.x) * UNROLL;
-    for (uint64_t x0 = threadIdx.x; x0 < n2; x0 += step) {
-      u64x2 v[UNROLL];
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++) {
-        uint64_t x = x0 + uint64_t(u) * blockDim.x;
-        if (x < n2) v[u] = si[x];
-      }
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++) {
-        uint64_t x = x0 + uint64_t(u) * blockDim.x;
-        if (x < n2) {
-          if (NT) __builtin_nontemporal_store(v[u], &di[x]);
-          else di[x] = v[u];
-        }
-      }
-    }
-  } else {
-    for (uint64_t x = threadIdx.x; x < a.row_words; x += blockDim.x) dst[x] = src[x];
-  }
+  for (uint64_t i = threadIdx.x; i < a.row_words; i += blockDim.x) dst[i] = src[i];
 }
 
-// One plane: row r of the output = its pod's class row.  VEC: 16-byte accesses (pitch even);
-// UNROLL: 16-byte chunks per thread kept in flight before the stores; NT: non-temporal stores
-// (the planes are write-once streams); XCD: consecutive (class-clustered) rows go to the same
-// XCD (blocks b, b+8, ... share one), so each class row is read from HBM about once per XCD.
-// Default grid = one block per row; option "emit_blocks" bounds it (persistent blocks striding
-// over their XCD's row segment) to leave CU slots to the other graph branch — measured slower
-// on config #3/#4 (profiles/r01_emit_sweep.txt), so off by default.
-// CHUNK (variant 6): one block per row, rows dealt to the XCDs in chunks of a.chunk consecutive
-// rows (chunk c -> XCD c % 8), so the 8 XCDs stream neighbouring chunks instead of 8 row ranges
-// a whole plane apart, while consecutive (same-class) rows still share one XCD's L2.
-template <bool VEC, int UNROLL, bool NT, bool XCD = true, bool CHUNK = false>
-__global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
-  emit_status(a);
-  const uint32_t b = blockIdx.x, n = a.n_rows * a.planes;
-  uint32_t r, r_end, r_step;
-  if (CHUNK) {
-    const uint32_t j = b >> 3;
-    r = ((j / a.chunk) * 8 + (b & 7)) * a.chunk + j % a.chunk;
-    if (r < n) emit_row<VEC, UNROLL, NT>(a, r);
-    return;
-  }
-  if (XCD) {  // block b runs on XCD b % 8: rows [x*per_xcd, (x+1)*per_xcd), stride blocks_per_xcd
-    const uint32_t x = b & 7;
-    r = x * a.per_xcd + (b >> 3);
-    r_end = min(n, (x + 1) * a.per_xcd);
-    r_step = a.blocks_per_xcd;
-  } else {
-    r = b;
-    r_end = n;
-    r_step = a.blocks_per_xcd * 8;
-  }
-  for (; r < r_end; r += r_step) emit_row<VEC, UNROLL, NT>(a, r);
-}
-
-// Variant 7 / 8: one block per G consecutive rows of an XCD's segment (rows are clustered by
-// class, so they mostly share one class row): each 16-byte chunk of the class row is loaded once
-// and stored to every row of the group using that class row (rows with another class row load
-// their own).  G x fewer loads per store than one block per row.
-template <int G, int UNROLL>
-__global__ __launch_bounds__(256) void k_emit_group(EmitArgs a) {
-  emit_status(a);
-  const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
-  const uint32_t r0 = x * a.per_xcd + (b >> 3) * G, r_end = min(n, (x + 1) * a.per_xcd);
-  if (r0 >= r_end) return;
-  const u64x2* src[G];
-  u64x2* dst[G];
-  bool same[G];
-#pragma unroll
-  for (int g = 0; g < G; g++) {
-    const uint32_t r = r0 + g;
-    src[g] = nullptr;
-    dst[g] = nullptr;
-    if (r < r_end) {
-      uint32_t pl, p;
-      emit_row_of(a, r, pl, p);
-      src[g] = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
-      dst[g] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
-    }
-    same[g] = src[g] == src[0];
-  }
-  const uint64_t n2 = a.row_words / 2, step = uint64_t(blockDim.x) * UNROLL;
-  for (uint64_t x0 = threadIdx.x; x0 < n2; x0 += step) {
-    u64x2 v[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; u++) {
-      const uint64_t i = x0 + uint64_t(u) * blockDim.x;
-      if (i < n2) v[u] = src[0][i];
-    }
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      if (!dst[g]) continue;
-      if (same[g]) {
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) {
-          const uint64_t i = x0 + uint64_t(u) * blockDim.x;
-          if (i < n2) __builtin_nontemporal_store(v[u], &dst[g][i]);
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) {
-          const uint64_t i = x0 + uint64_t(u) * blockDim.x;
-          if (i < n2) __builtin_nontemporal_store(src[g][i], &dst[g][i]);
-        }
-      }
-    }
-  }
-}
-
-// Variant 9 (auto for short rows): one block per a.chunk consecutive rows of an XCD's segment,
-// the threads sweeping the rows' 16-byte chunks as one flat range (row = index / chunks per row),
-// so rows shorter than a block's 4 KB-per-pass still keep every lane storing.  The rows' source
-// and destination addresses are staged in LDS first.
+// Short rows (< 16 KB, auto): one block per a.chunk consecutive rows of an XCD's segment, the
+// threads sweeping the rows' 16-byte chunks as one flat range (row = index / chunks per row), so
+// rows shorter than a block's pass still keep every lane storing.  The rows' source and
+// destination addresses are staged in LDS first.
 constexpr uint32_t EMIT_FLAT_MAX_ROWS = 256;
 template <int UNROLL>
 __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   emit_status(a);
   __shared__ const u64x2* s_src[EMIT_FLAT_MAX_ROWS];
   __shared__ u64x2* s_dst[EMIT_FLAT_MAX_ROWS];
-  const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
+  const uint32_t b = blockIdx.x, n = a.n_rows * 2, x = b & 7;
   const uint32_t r0 = x * a.per_xcd + (b >> 3) * a.chunk;
   const uint32_t r_end = min(n, (x + 1) * a.per_xcd);
   if (r0 >= r_end) return;
   const uint32_t nr = min(a.chunk, r_end - r0);
   if (threadIdx.x < nr) {
-    const uint32_t r = r0 + threadIdx.x;
     uint32_t pl, p;
-    emit_row_of(a, r, pl, p);
+    emit_row_of(a, r0 + threadIdx.x, pl, p);
     s_src[threadIdx.x] = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
     s_dst[threadIdx.x] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
   }
@@ -1720,26 +1651,16 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   }
 }
 
-// Variant 10 (auto for rows of >= 64 KB): one block of BS = 512 threads per row (XCD-mapped as
-// variant 0) with UNROLL chosen on the host so one pass of BS x UNROLL 16-byte chunks covers the
-// row (config #3: 100 KB rows, 512 x 13 x 16 B = 104 KB): every lane's loads are in flight before
-// its stores and no second, partly idle pass follows (profiles/r01_emit_wide_sweep.txt: 3-4 %
-// faster than 256 x 16 in two passes; 1024 x 7, 256 x 25, 512 x 7, plain or sc1 stores, and
-// fill-like address-linear 16 / 32 KB segments were all slower).  STORE 0 = non-temporal,
-// 1 = plain, 2 = sc1.
-template <int BS, int UNROLL, int STORE>
+// Rows of >= 16 KB (auto): one block of BS threads per row, UNROLL chosen on the host so ONE pass
+// of BS x UNROLL 16-byte chunks covers the row (config #3: 100 KB rows, 512 x 13 x 16 B; config #4:
+// 25 KB rows, 256 x 7 x 16 B): every lane's loads are in flight before its stores and no second,
+// partly idle pass follows (profiles/r01_emit_wide_sweep.txt, r01_emit_medium_rows_ab.txt).
+template <int BS, int UNROLL>
 __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   emit_status(a);
-  const uint32_t b = blockIdx.x, n = a.n_rows * a.planes, x = b & 7;
-  uint32_t r;
-  if (a.deal) {  // rows dealt to the XCDs in chunks of a.chunk: the 8 XCDs write neighbouring chunks
-    const uint32_t j = b >> 3;
-    r = ((j / a.chunk) * 8 + x) * a.chunk + j % a.chunk;
-    if (r >= n) return;
-  } else {  // XCD x writes its own contiguous segment of the row list
-    r = x * a.per_xcd + (b >> 3);
-    if (r >= min(n, (x + 1) * a.per_xcd)) return;
-  }
+  const uint32_t b = blockIdx.x, n = a.n_rows * 2, x = b & 7;
+  const uint32_t r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
+  if (r >= min(n, (x + 1) * a.per_xcd)) return;
   uint32_t pl, p;
   emit_row_of(a, r, pl, p);
   const u64x2* si = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
@@ -1751,14 +1672,8 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
     for (int u = 0; u < UNROLL; u++)
       if (x0 + u * BS < n2) v[u] = si[x0 + u * BS];
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) {
-      const uint32_t i = x0 + u * BS;
-      if (i < n2) {
-        if (STORE == 0) __builtin_nontemporal_store(v[u], &di[i]);
-        else if (STORE == 1) di[i] = v[u];
-        else asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(&di[i]), "v"(v[u]) : "memory");
-      }
-    }
+    for (int u = 0; u < UNROLL; u++)
+      if (x0 + u * BS < n2) __builtin_nontemporal_store(v[u], &di[x0 + u * BS]);
   }
 }
 
@@ -2072,38 +1987,23 @@ struct cyc_ctx {
   DevBuf act[2], sel_list;
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
   double act_targets[2] = {0, 0};  // mean namespace targets per active identity (range plan)
-  int emit_variant = -1;  // tuning knob (cyc_set_option "emit_variant"; -1 = auto by row length)
-  int64_t emit_chunk = 64;  // cyc_set_option "emit_chunk": rows per XCD chunk (emit_variant 6)
-  int64_t emit_blocks = 0;  // cyc_set_option "emit_blocks": persistent emit grid (0 = a block per row)
-  int class_variant[2] = {3, 3};  // cyc_set_option "class_variant_in" / "_eg" (enq_class_rows;
-                                  // defaults measured best on configs #3/#4: profiles/r01_class_sweep.txt)
-  int use_graphs = -1;  // cyc_set_option "graphs": 1 = graph replay, 2 = the same DAG enqueued eagerly
-                       // on three streams with events (no graph launch), 0 = eager on one stream with
-                       // phase events, -1 = auto: 2 when the fused front applies (its 6 launches on
-                       // one stream start ~8 us sooner after the previous step's emit than a graph
-                       // replay: profiles/r01_front_fused_ab.txt), else 1
-  int pod_rows = -1;   // cyc_set_option "pod_rows": pod-peer PM rows per pod directly (1), through
-                       // identity outcomes and word runs (0), or -1 = direct when identities >= pods / 2
-  int member_wave = -1;  // cyc_set_option "member_wave": membership with a wave (1) or a thread (0) per
-                         // identity, -1 = auto by identity count
-  int pod_words = -1;  // cyc_set_option "pod_words": pod-peer words in the class rows from IDO (1), from
-                       // materialised PM rows (0), or IDO when every word has <= IDO_MAX_RUNS runs (-1)
-  int graph_stagger = 1;  // cyc_set_option "graph_stagger": 1 = egress class rows wait for the ingress
-                          // ones (they run under the ingress emit), 0 = branches unordered
-  hipEvent_t stagger_ev = nullptr;
-  int emit_deal = 0;  // cyc_set_option "emit_deal": k_emit_wide rows dealt in chunks of "emit_chunk"
-  int emit_interleave = -1;  // cyc_set_option "emit_interleave": the merged emit alternates plane rows
-                            // (1), keeps them one plane after the other (0), -1 = auto by plane size
-  int emit_merged = 1;  // cyc_set_option "emit_merged": both planes in ONE emit launch after both
-                        // directions' class rows.  A plane's emit grid fills every CU, so a second
-                        // branch's front queued behind it would only run once that emit drains.
-  bool graph_branches = true;  // cyc_set_option "graph_branches": ingress / egress as two graph branches
-  int64_t class_rpb_opt = 4;  // cyc_set_option "class_rpb": IDO class-row representatives per block
+  // Diagnostic path selectors (cyc_set_option; results never change, the GPU tests force each path):
+  int use_graphs = -1;  // "graphs": 1 = graph replay, 2 = the same DAG enqueued eagerly on three
+                        // streams with events (no graph launch), 0 = eager on one stream with phase
+                        // events, -1 = auto: 2 when the fused front applies (its launches on one
+                        // stream start ~8 us sooner after the previous step's emit than a graph
+                        // replay: profiles/r01_front_fused_ab.txt), else 1
+  int pod_rows = -1;    // "pod_rows": pod-peer PM rows per pod directly (1), through identity outcomes
+                        // and word runs (0), or -1 = direct when identities >= pods / 2
+  int member_wave = -1; // "member_wave": membership with a wave (1) or a thread (0) per identity,
+                        // -1 = auto by identity count
+  int pod_words = -1;   // "pod_words": pod-peer words in the class rows from identity sets (1, IDO),
+                        // from materialised PM rows (0), or IDO when every word has <= IDO_MAX_RUNS runs
+  int64_t class_rpb_opt = 4;  // "class_rpb": IDO class-row representatives per block
                               // (config3 N=1 -1%: profiles/r01_class_rpb_ab.txt)
-  uint32_t ip_group = IP_GROUP;  // cyc_set_option "ip_group": IP-peer tests per wave in the IP rows
-  int port_bits = 1;  // cyc_set_option "port_bits": egress class rows test ports through descriptor bit rows
-  int front_fused = 1;  // cyc_set_option "front_fused": the graphed front as 5 block-range-fused launches
-                       // on one stream (enq_front_fused; IDO builds), 0 = the two-branch DAG
+  uint32_t ip_group = IP_GROUP;  // "ip_group": IP-peer tests per block in the IP rows
+  int front_fused = 1;  // "front_fused": the front as block-range-fused launches on one stream
+                        // (enq_front_fused), 0 = the two-branch DAG
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
   hipEvent_t fork_ev = nullptr, join_ev = nullptr, sel_ev = nullptr, ports_ev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
@@ -2304,7 +2204,7 @@ static void prepare_device(cyc_ctx* c) {
     }
   }
   c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
-  c->ip_rng.alloc(std::max<uint64_t>(R * 8, 16));
+  c->ip_rng.alloc(std::max<uint64_t>(R * 8 + R * ((W + 63) / 64) * 8, 16));  // [R][2] word spans, then [R][W/64] cnz
   c->ER.alloc(pb.may_err ? std::max<uint64_t>(R * W * 8, 16) : 16);
   {
     c->plan = plan_peers(pb, c->ids[1]);
@@ -2314,8 +2214,9 @@ static void prepare_device(cyc_ctx* c) {
     upload(c->run_mask, pl.run_mask);
     upload(c->runs, pl.runs);
     upload(c->id_nsls, c->ids[1].nsls);
-    {  // per-word, per-family address intervals for k_ip_rows_fast
-      std::vector<DWordIP> wi(pb.W);
+    {  // per-word, per-family address intervals for k_ip_rows_fast, then one record per 64-word chunk
+      const uint32_t NC = (pb.W + 63) / 64;
+      std::vector<DWordIP> wi(pb.W + NC);
       for (uint32_t w = 0; w < pb.W; w++) {
         DWordIP d{};
         d.min4 = 0xFFFFFFFFu;
@@ -2334,6 +2235,25 @@ static void prepare_device(cyc_ctx* c) {
           }
         }
         wi[w] = d;
+      }
+      for (uint32_t ch = 0; ch < NC; ch++) {
+        DWordIP d{};
+        d.min4 = 0xFFFFFFFFu;
+        for (int i = 0; i < 4; i++) d.min6[i] = 0xFFFFFFFFu;
+        for (uint32_t w = ch * 64; w < std::min<uint32_t>(pb.W, ch * 64 + 64); w++) {
+          const DWordIP& x = wi[w];
+          if (x.m4) {
+            d.m4 |= 1ull << (w - ch * 64);
+            d.min4 = std::min(d.min4, x.min4);
+            d.max4 = std::max(d.max4, x.max4);
+          }
+          if (x.m6) {
+            d.m6 |= 1ull << (w - ch * 64);
+            if (std::lexicographical_compare(x.min6, x.min6 + 4, d.min6, d.min6 + 4)) std::copy(x.min6, x.min6 + 4, d.min6);
+            if (std::lexicographical_compare(d.max6, d.max6 + 4, x.max6, x.max6 + 4)) std::copy(x.max6, x.max6 + 4, d.max6);
+          }
+        }
+        wi[pb.W + ch] = d;
       }
       upload(c->ip_words, wi);
     }
@@ -2386,6 +2306,9 @@ static void prepare_device(cyc_ctx* c) {
   c->order_lo = c->order_hi = -1;
 }
 
+// nonzero-word masks of the IP peers' PM rows, after the word spans in the ip_rng buffer
+static uint64_t* ip_cnz(cyc_ctx* c) { return reinterpret_cast<uint64_t*>(c->ip_rng.as<uint32_t>() + 2 * c->pb.peers.size()); }
+
 static unsigned grid1(uint64_t n, unsigned block) { return unsigned(std::min<uint64_t>((n + block - 1) / block, 1u << 20)); }
 
 static MemberArgs member_args(cyc_ctx* c, int d) {
@@ -2418,8 +2341,9 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   return a;
 }
 
-// PM-build class rows (k_class_rows_pl): blocks per direction; they stride over the representatives
-static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c->n_act[d], 2048u); }
+// PM-build class rows (k_class_rows_pl, PL_THREADS per block): blocks per direction, striding over
+// the representatives; about two blocks in flight per CU slot
+static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c->n_act[d], 2048u * 256u / PL_THREADS); }
 
 // Range plan for rows [lo,hi): (1) the rows ordered so pods sharing class rows are adjacent
 // (L2 / Infinity-Cache reuse in k_emit); (2) the identities those rows use, per direction —
@@ -2538,14 +2462,14 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
 // as two independent branches: one direction's front hides under the other's HBM-bound emit.
 enum { COMMON_SELECTORS = 1, COMMON_PORTS = 2, COMMON_FILL = 4, COMMON_ALL = 7 };
 // Descriptor bit rows of the port table for the egress class rows (cyc_set_option "port_bits")
-static bool port_bits_on(const cyc_ctx* c) { return c->port_bits && std::max<size_t>(c->pb.descs.size(), 1) <= 32; }
+static bool port_bits_on(const cyc_ctx* c) { return std::max<size_t>(c->pb.descs.size(), 1) <= 32; }
 
 static void enq_common(cyc_ctx* c, hipStream_t st, int parts = COMMON_ALL) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size());
   if ((parts & COMMON_FILL) && !pb.may_err && c->Ri)  // IP-peer word spans (k_ip_rows_fast)
-    k_fill_u32<<<grid1(c->ip_rng.bytes / 4, 256), 256, 0, st>>>(c->ip_rng.as<uint32_t>(), c->ip_rng.bytes / 4, 0xFFFFFFFFu);
+    k_fill_u32<<<grid1(c->pb.peers.size() * 2, 256), 256, 0, st>>>(c->ip_rng.as<uint32_t>(), c->pb.peers.size() * 2, 0xFFFFFFFFu);
   if (!(parts & COMMON_SELECTORS)) goto ports;
   // 1. selectors x label sets
   if (uint64_t(c->n_sel) * pb.L && c->dense_sel)
@@ -2634,7 +2558,7 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
       const uint32_t grp = c->ip_group;
       k_ip_rows_fast<<<unsigned(ip_rows_blocks(Ri, W, grp)), 256, 0, st>>>(
           Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>(),
-          c->ip_rng.as<uint32_t>(), grp);
+          c->ip_rng.as<uint32_t>(), ip_cnz(c), grp);
     }
   }
 }
@@ -2702,14 +2626,7 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.DM = c->DM.as<uint64_t>();
   ra.A = dd.A.as<uint64_t>();
   ra.AE = pb.may_err ? dd.AE.as<uint64_t>() : nullptr;
-  // variant (cyc_set_option "class_variant_in" / "class_variant_eg"): bit 0 = 4 slots per
-  // thread instead of 8, bit 1 = block rows stride over the representatives (bounded grid)
-  const int var = d == 0 ? c->class_variant[0] : c->class_variant[1];
-  const uint32_t kct = (var & 1) ? 4 : 8;
-  const bool loop = (var & 2) != 0;
-  const uint64_t per_rep = uint64_t((W + 255) / 256) * ((K + kct - 1) / kct);
-  ra.rep_blocks = loop ? uint32_t(std::min<uint64_t>(c->n_act[d], std::max<uint64_t>(64, (16384 + per_rep - 1) / per_rep)))
-                       : c->n_act[d];
+  ra.rep_blocks = c->n_act[d];  // k_class_rows (panic path): a block row per representative slot
   ra.reps = dd.reps.as<uint32_t>();
   ra.rep_cnt = dd.rep_cnt();
   ra.IDOB = c->idob.as<uint64_t>();
@@ -2720,6 +2637,7 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.ip_cnt = dd.ip_cnt.as<uint32_t>();
   ra.ip_list = dd.ip_list.as<uint4>();
   ra.ip_rng = c->ip_rng.as<uint32_t>();
+  ra.ip_cnz = ip_cnz(c);
   ra.E = c->dir[1].n;
   ra.EW = (ra.E + 63) / 64;
   ra.NB = d == 0 ? K : D;
@@ -2736,60 +2654,33 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   DirDev& dd = c->dir[d];
   if (!dd.n || !K || !W || !c->n_act[d]) return;
   RowArgs ra = row_args(c, d);
-  const int var = d == 0 ? c->class_variant[0] : c->class_variant[1];
-  const uint32_t kct = (var & 1) ? 4 : 8;
-  const bool loop = (var & 2) != 0;
-  const uint64_t per_rep = uint64_t((W + 255) / 256) * ((K + kct - 1) / kct);
-  if (ido_mode(c)) {  // identity sets first (one wave per representative and 4 slots / descriptors)
+  if (pb.may_err) {  // the ordered walk with panic bits: one block row per identity, 8 slots per thread
+    const unsigned g = unsigned(uint64_t((W + 255) / 256) * ((K + 7) / 8) * ra.rep_blocks);
+    if (d == 0) k_class_rows<false><<<g, 256, 0, st>>>(ra);
+    else k_class_rows<true><<<g, 256, 0, st>>>(ra);
+  } else if (ido_mode(c)) {
+    // identity sets first (one wave per representative and 4 slots / descriptors), then the rows
     const uint64_t waves = uint64_t(c->n_act[d]) * ((ra.NB + 3) / 4);
     if (d == 0) k_class_ident<false, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
     else k_class_ident<true, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
     ra.ht_clear_words = 0;
-  }
-  unsigned g = unsigned(per_rep * ra.rep_blocks);
-#define CYC_ROWS(EG, ERR, KCT, LOOP) k_class_rows<EG, ERR, KCT, LOOP><<<g, 256, 0, st>>>(ra)
-  if (!pb.may_err && !ido_mode(c)) {  // per-class flattened peer lists (the IP word spans are final here)
-    if (d == 0) k_class_rows_pl<false><<<pl_blocks(c, d), 256, 0, st>>>(ra);
-    else k_class_rows_pl<true><<<pl_blocks(c, d), 256, 0, st>>>(ra);
-  } else if (pb.may_err) {
-    if (d == 0) CYC_ROWS(false, true, 8, false);
-    else CYC_ROWS(true, true, 8, false);
-  } else if (ido_mode(c)) {
-    // KC = kct job slots per thread (class_variant bit 0: 4, else 8)
-    const uint32_t rows = d == 0 ? std::min<uint32_t>(kct, K) : D;
+    const uint32_t rows = d == 0 ? std::min<uint32_t>(4, K) : D;
     const size_t per = size_t(rows) * ra.EW * 8;
     ra.rpb = class_rpb(c, per);
-    const unsigned gi = unsigned(uint64_t((W + 255) / 256) * ((K + kct - 1) / kct) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
-    const size_t lds = per * ra.rpb;
-    if (kct == 4) {
-      if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, lds, st>>>(ra);
-      else k_class_rows_ido<true, 4><<<gi, 256, lds, st>>>(ra);
-    } else {
-      if (d == 0) k_class_rows_ido<false, 8><<<gi, 256, lds, st>>>(ra);
-      else k_class_rows_ido<true, 8><<<gi, 256, lds, st>>>(ra);
-    }
-  } else if (d == 0) {
-    if (kct == 4) loop ? CYC_ROWS(false, false, 4, true) : CYC_ROWS(false, false, 4, false);
-    else loop ? CYC_ROWS(false, false, 8, true) : CYC_ROWS(false, false, 8, false);
-  } else {
-    if (kct == 4) loop ? CYC_ROWS(true, false, 4, true) : CYC_ROWS(true, false, 4, false);
-    else loop ? CYC_ROWS(true, false, 8, true) : CYC_ROWS(true, false, 8, false);
+    const unsigned gi = unsigned(uint64_t((W + 255) / 256) * ((K + 3) / 4) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
+    if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
+    else k_class_rows_ido<true, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
+  } else {  // per-class flattened peer lists (the IP word spans are final here)
+    if (d == 0) k_class_rows_pl<false><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
+    else k_class_rows_pl<true><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
   }
-#undef CYC_ROWS
 }
 
-// 7. emit of direction d's plane (d = 2: both planes in one launch, out = ingress, out2 = egress)
-// k_emit_wide grid: one block per row slot of the XCD segments, or of the chunked deal.
-static unsigned wide_grid(const EmitArgs& ea) {
-  if (!ea.deal) return ea.per_xcd * 8;
-  const uint64_t n = uint64_t(ea.n_rows) * ea.planes, per = 8ull * ea.chunk;
-  return unsigned((n + per - 1) / per * per);
-}
-
+// 7. the emit: both planes (ingress rows to out_in, egress rows to out_eg) in one launch.
 // d_status (may be null): the status plane, copied by the emit's blocks.  Returns false if no
 // emit was launched (no rows in the range; the caller then copies the status plane itself).
-static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t lo, int64_t hi, uint64_t* out2 = nullptr,
-                     uint8_t* d_status = nullptr) {
+static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, int64_t lo, int64_t hi,
+                     uint8_t* d_status) {
   Problem& pb = c->pb;
   const uint32_t K = pb.K, W = pb.W;
   if (hi <= lo || !K || !W) return false;
@@ -2798,106 +2689,64 @@ static bool enq_emit(cyc_ctx* c, int d, hipStream_t st, uint64_t* out, int64_t l
   ea.st_dst = d_status;
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
   ea.n_rows = uint32_t(hi - lo);
-  ea.planes = d == 2 ? 2 : 1;
   ea.row_lo = uint32_t(lo);
-  // auto (-1): alternate the planes' rows when each plane is >= 8 GB (config #3 on one GPU: the
-  // merged emit 3.42 -> 3.11 ms on two of three boxes, 1 % on the third; with 5 GB or less per
-  // plane — 2, 4, 8 shards — interleaving cost 1-4 %; profiles/r01_emit_interleave_sweep.txt)
-  const bool big = uint64_t(ea.n_rows) * K * W * 8 >= (8ull << 30);
-  ea.interleave = ea.planes == 2 && (c->emit_interleave > 0 || (c->emit_interleave < 0 && big)) ? 1u : 0u;
-  ea.deal = c->emit_deal ? 1u : 0u;
-  for (uint32_t pl = 0; pl < ea.planes; pl++) {
-    const int dd = d == 2 ? int(pl) : d;
-    ea.order[pl] = c->order[dd].as<uint32_t>();
-    ea.pod_id[pl] = c->dir[dd].pod_id.as<uint32_t>();
-    ea.class_of[pl] = c->dir[dd].class_of.as<uint32_t>();
-    ea.A[pl] = c->dir[dd].A.as<uint64_t>();
-    ea.out[pl] = pl ? out2 : out;
+  // alternate the planes' rows when each plane is >= 8 GB (config #3 on one GPU: emit 3.42 ->
+  // 3.11 ms on two of three boxes, -1 % on the third; 1-4 % slower for planes of <= 5 GB — 2, 4
+  // and 8 shards — profiles/r01_emit_interleave_sweep.txt)
+  ea.interleave = uint64_t(ea.n_rows) * K * W * 8 >= (8ull << 30) ? 1u : 0u;
+  for (uint32_t pl = 0; pl < 2; pl++) {
+    ea.order[pl] = c->order[pl].as<uint32_t>();
+    ea.pod_id[pl] = c->dir[pl].pod_id.as<uint32_t>();
+    ea.class_of[pl] = c->dir[pl].class_of.as<uint32_t>();
+    ea.A[pl] = c->dir[pl].A.as<uint64_t>();
   }
+  ea.out[0] = out_in;
+  ea.out[1] = out_eg;
   ea.row_words = uint64_t(K) * W;
-  ea.per_xcd = (ea.n_rows * ea.planes + 7) / 8;
-  // persistent grid: emit_blocks per launch (0 = one block per row)
-  ea.blocks_per_xcd = c->emit_blocks ? std::min<uint32_t>(ea.per_xcd, std::max<uint32_t>(1, uint32_t(c->emit_blocks / 8)))
-                                     : ea.per_xcd;
-  const bool aligned = reinterpret_cast<uintptr_t>(out) % 16 == 0 && (!out2 || reinterpret_cast<uintptr_t>(out2) % 16 == 0);
-  const bool vec = (ea.row_words % 2 == 0) && aligned;
-  unsigned g = ea.blocks_per_xcd * 8;
-  ea.chunk = uint32_t(std::max<int64_t>(1, c->emit_chunk));
-  if (vec && c->emit_variant == 6) {  // one block per row slot of the chunked deal
-    const uint32_t n = ea.n_rows * ea.planes, per = 8 * ea.chunk;
-    g = (n + per - 1) / per * per;
+  ea.per_xcd = (ea.n_rows * 2 + 7) / 8;
+  const bool aligned = reinterpret_cast<uintptr_t>(out_in) % 16 == 0 && reinterpret_cast<uintptr_t>(out_eg) % 16 == 0;
+  const unsigned g = ea.per_xcd * 8;  // one block per row slot of the 8 XCD segments
+  if (ea.row_words % 2 || !aligned) {
+    k_emit_words<<<g, 256, 0, st>>>(ea);
+    return true;
   }
-  // emit_variant -1 (default) = auto by plane-row length: >= 64 KB one 512-thread single-pass
-  // block per row (10), >= 16 KB one 256-thread single-pass block per row (11; config #4's 25 KB
-  // rows: 256 x 7 x 16 B, emit -6 % vs two-pass variant 0), else the flat multi-row sweep over
-  // ~32 KB per block (9)
   const uint64_t row_bytes = ea.row_words * 8;
-  const int variant = c->emit_variant >= 0 ? c->emit_variant : (row_bytes >= 65536 ? 10 : row_bytes >= 16384 ? 11 : 9);
-  if (vec && (variant == 7 || variant == 8)) {  // one block per row group of an XCD segment
-    const uint32_t G = variant == 7 ? 2 : 4;
-    g = (ea.per_xcd + G - 1) / G * 8;
+  if (row_bytes >= 65536) {  // 512-thread single pass: smallest UNROLL covering the row (16 = two passes)
+    const uint64_t need = (ea.row_words / 2 + 511) / 512;
+    if (need <= 8) k_emit_wide<512, 8><<<g, 512, 0, st>>>(ea);
+    else if (need <= 10) k_emit_wide<512, 10><<<g, 512, 0, st>>>(ea);
+    else if (need <= 12) k_emit_wide<512, 12><<<g, 512, 0, st>>>(ea);
+    else if (need <= 13) k_emit_wide<512, 13><<<g, 512, 0, st>>>(ea);
+    else if (need <= 14) k_emit_wide<512, 14><<<g, 512, 0, st>>>(ea);
+    else k_emit_wide<512, 16><<<g, 512, 0, st>>>(ea);
+  } else if (row_bytes >= 16384) {  // 256-thread single pass (16-64 KB rows)
+    const uint64_t need = (ea.row_words / 2 + 255) / 256;
+    if (need <= 4) k_emit_wide<256, 4><<<g, 256, 0, st>>>(ea);
+    else if (need <= 6) k_emit_wide<256, 6><<<g, 256, 0, st>>>(ea);
+    else if (need <= 7) k_emit_wide<256, 7><<<g, 256, 0, st>>>(ea);
+    else if (need <= 8) k_emit_wide<256, 8><<<g, 256, 0, st>>>(ea);
+    else if (need <= 10) k_emit_wide<256, 10><<<g, 256, 0, st>>>(ea);
+    else if (need <= 12) k_emit_wide<256, 12><<<g, 256, 0, st>>>(ea);
+    else k_emit_wide<256, 16><<<g, 256, 0, st>>>(ea);
+  } else {  // flat multi-row sweep over ~32 KB per block
+    ea.chunk = uint32_t(std::min<uint64_t>(EMIT_FLAT_MAX_ROWS, std::max<uint64_t>(1, 32768 / row_bytes)));
+    k_emit_flat<8><<<(ea.per_xcd + ea.chunk - 1) / ea.chunk * 8, 256, 0, st>>>(ea);
   }
-  if (vec && variant == 9) {
-    ea.chunk = uint32_t(std::min<uint64_t>(EMIT_FLAT_MAX_ROWS, std::max<uint64_t>(1, 32768 / (ea.row_words * 8))));
-    g = (ea.per_xcd + ea.chunk - 1) / ea.chunk * 8;
-  }
-#define CYC_EMIT(V, U, N, X) k_emit<V, U, N, X><<<g, 256, 0, st>>>(ea)
-  if (!vec) CYC_EMIT(false, 1, false, true);
-  else switch (variant) {  // 0 = default (measured fastest, profiles/r01_emit_sweep.txt:
-                                   // UNROLL 16 x 16 B in flight per thread, nt stores, XCD-mapped)
-      case 1: CYC_EMIT(true, 1, true, true); break;
-      case 2: CYC_EMIT(true, 4, false, true); break;
-      case 3: CYC_EMIT(true, 4, true, true); break;
-      case 4: CYC_EMIT(true, 8, true, true); break;
-      case 5: CYC_EMIT(true, 16, true, false); break;
-      case 6: k_emit<true, 16, true, true, true><<<g, 256, 0, st>>>(ea); break;
-      case 7: k_emit_group<2, 8><<<g, 256, 0, st>>>(ea); break;
-      case 8: k_emit_group<4, 8><<<g, 256, 0, st>>>(ea); break;
-      case 9: k_emit_flat<8><<<g, 256, 0, st>>>(ea); break;
-      case 10: {
-        // smallest UNROLL whose single pass covers the row (16 when the row needs more passes)
-        const uint64_t need = (ea.row_words / 2 + 511) / 512;
-        const unsigned gw = wide_grid(ea);
-        if (need <= 8) k_emit_wide<512, 8, 0><<<gw, 512, 0, st>>>(ea);
-        else if (need <= 10) k_emit_wide<512, 10, 0><<<gw, 512, 0, st>>>(ea);
-        else if (need <= 12) k_emit_wide<512, 12, 0><<<gw, 512, 0, st>>>(ea);
-        else if (need <= 13) k_emit_wide<512, 13, 0><<<gw, 512, 0, st>>>(ea);
-        else if (need <= 14) k_emit_wide<512, 14, 0><<<gw, 512, 0, st>>>(ea);
-        else k_emit_wide<512, 16, 0><<<gw, 512, 0, st>>>(ea);
-        break;
-      }
-      case 11: {  // 256-thread single pass: smallest UNROLL covering the row (16-64 KB rows)
-        const uint64_t need = (ea.row_words / 2 + 255) / 256;
-        const unsigned gw = wide_grid(ea);
-        if (need <= 4) k_emit_wide<256, 4, 0><<<gw, 256, 0, st>>>(ea);
-        else if (need <= 6) k_emit_wide<256, 6, 0><<<gw, 256, 0, st>>>(ea);
-        else if (need <= 7) k_emit_wide<256, 7, 0><<<gw, 256, 0, st>>>(ea);
-        else if (need <= 8) k_emit_wide<256, 8, 0><<<gw, 256, 0, st>>>(ea);
-        else if (need <= 10) k_emit_wide<256, 10, 0><<<gw, 256, 0, st>>>(ea);
-        else if (need <= 12) k_emit_wide<256, 12, 0><<<gw, 256, 0, st>>>(ea);
-        else k_emit_wide<256, 16, 0><<<gw, 256, 0, st>>>(ea);
-        break;
-      }
-      default: CYC_EMIT(true, 16, true, true); break;
-    }
-#undef CYC_EMIT
   return true;
 }
 
 // The fused front (k_front_a..e, one stream): the same block ranges the two-branch DAG launches
 // as ~15 kernels (enq_common, enq_peer_rows, enq_member, enq_class_rows), grouped by dependency
-// level.  Applies to IDO builds with dense selectors and 4 job slots per class-row thread (the
-// defaults on configs #2-#4); returns false (nothing enqueued) otherwise.
+// level.  Applies to no-panic builds with dense selectors whose pod-peer rows (PM builds) are
+// computed per pod in one level; returns false (nothing enqueued) otherwise.
 static bool front_fused_ok(const cyc_ctx* c) {
   const Problem& pb = c->pb;
-  if (!c->front_fused || !c->emit_merged || pb.may_err) return false;
+  if (!c->front_fused || pb.may_err) return false;
   if (!pb.P || !pb.K || !pb.W) return false;
   if (uint64_t(c->n_sel) * pb.L && !c->dense_sel) return false;
-  if (ido_mode(c)) return (c->class_variant[0] & 1) != 0;  // KC = 4 ingress; egress 4 or 8 (k_front_e<KCE>)
-  // PM builds: pod-peer rows per pod (one level) and k_class_rows<…, 4, LOOP> in both directions
+  if (ido_mode(c)) return true;
   const uint32_t E = c->dir[1].n, Rp = c->rp_off[2] - c->rp_off[0];
-  const bool direct = !(Rp && E) || (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= pb.P);
-  return direct && c->class_variant[0] == 3 && c->class_variant[1] == 3;
+  return !(Rp && E) || (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= pb.P);
 }
 
 static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nullptr, hipEvent_t ev_rows = nullptr) {
@@ -2912,7 +2761,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   // A: IP word spans | port table | slot words | selectors
   FrontA fa{};
   fa.fill_p = c->ip_rng.as<uint32_t>();
-  fa.fill_n = c->Ri ? c->ip_rng.bytes / 4 : 0;
+  fa.fill_n = c->Ri ? pb.peers.size() * 2 : 0;  // the word spans (cnz needs no reset)
   fa.nb[0] = blocks((fa.fill_n + 255) / 256);
   fa.M = M;
   fa.D = D;
@@ -2951,6 +2800,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.words = c->ip_words.as<DWordIP>();
   fb.PM = c->PM.as<uint64_t>();
   fb.rng = c->ip_rng.as<uint32_t>();
+  fb.cnz = ip_cnz(c);
   fb.ip_grp = c->ip_group;
   fb.nb[0] = Ri ? blocks(ip_rows_blocks(Ri, W, fb.ip_grp)) : 0u;
   const uint32_t Rp = c->rp_off[2] - c->rp_off[0], u0 = c->rpu_off[0], Ru = c->rpu_off[2] - u0;
@@ -2996,8 +2846,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + 3) / 4) + 3) / 4);
     const size_t per = size_t(d == 0 ? std::min<uint32_t>(4, K) : D) * fd.ra[d].EW * 8;
     fe.ra[d].rpb = class_rpb(c, per);
-    const uint32_t kcd = (d == 1 && !(c->class_variant[1] & 1)) ? 8u : 4u;
-    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + kcd - 1) / kcd) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
+    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + 3) / 4) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
     lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
   const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
@@ -3015,14 +2864,13 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (fc.nb[0] + fc.nb[1]) k_front_c<<<fc.nb[0] + fc.nb[1], 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
-    if (fd.nb[0] + fd.nb[1]) k_front_d_pm<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
+    if (fd.nb[0] + fd.nb[1]) k_front_d_pm<<<fd.nb[0] + fd.nb[1], PL_THREADS, 0, st>>>(fd);
     if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
     return true;
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
   if (fe.nb[0] + fe.nb[1]) {
-    if (c->class_variant[1] & 1) k_front_e<4><<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
-    else k_front_e<8><<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
+    k_front_e<<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
   }
   if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
   return true;
@@ -3042,37 +2890,30 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
     for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
     HIPCHK(hipEventRecord(c->ev[2], st));
   }
-  bool status_done;
-  if (c->emit_merged) {
-    status_done = enq_emit(c, 2, st, d_in, lo, hi, d_eg, d_status);
-  } else {
-    status_done = enq_emit(c, 0, st, d_in, lo, hi, nullptr, d_status);
-    enq_emit(c, 1, st, d_eg, lo, hi);
-  }
+  const bool status_done = enq_emit(c, st, d_in, d_eg, lo, hi, d_status);
   HIPCHK(hipEventRecord(c->ev[3], st));
   if (!status_done && d_status && uint64_t(pb.P) * pb.K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
 }
 
-// Graph capture: shared front on st, then the ingress branch on st and the egress branch on st2
-// (fork / join through events, recorded into the graph as dependencies).
+// Graph capture / eager DAG: the fused front on st when it applies; else the two-branch DAG:
+// [st3] IP rows of both directions + port tables || [st] selectors, then per direction (ingress on
+// st, egress on st2) pod-peer sets -> membership / classes -> (wait for st3) class rows, joined
+// into one emit of both planes (fork / join through events, graph dependencies when captured).
 static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStream_t st3, uint64_t* d_in, uint64_t* d_eg,
                              uint8_t* d_status, int64_t lo, int64_t hi) {
   Problem& pb = c->pb;
-  if (!c->graph_branches) st2 = st3 = st;
   if (front_fused_ok(c) && enq_front_fused(c, st)) {
-    if (enq_emit(c, 2, st, d_in, lo, hi, d_eg, d_status)) return;
-  } else if (c->emit_merged) {
-    // DAG: [st3] IP rows of both directions + port tables || [st] selectors, then per direction
-    // pod-peer sets -> membership / classes -> (wait for st3) class rows; one emit of both planes.
+    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status)) return;
+  } else {
     HIPCHK(hipEventRecord(c->fork_ev, st));
-    if (st3 != st) HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
+    HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
     enq_common(c, st3, COMMON_FILL | COMMON_PORTS);
     enq_peer_rows(c, 2, st3, PEERS_IP);  // both directions' IP rows in one launch
     HIPCHK(hipEventRecord(c->ports_ev, st3));
     enq_common(c, st, COMMON_SELECTORS);
     HIPCHK(hipEventRecord(c->sel_ev, st));
-    if (st2 != st) HIPCHK(hipStreamWaitEvent(st2, c->sel_ev, 0));
+    HIPCHK(hipStreamWaitEvent(st2, c->sel_ev, 0));
     for (int d = 1; d >= 0; d--) {
       hipStream_t s = d ? st2 : st;
       enq_peer_rows(c, d, s, PEERS_POD);
@@ -3083,25 +2924,7 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
     HIPCHK(hipEventRecord(c->join_ev, st2));
     HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
     // the emit also writes the status plane; the copy node below only ends steps without rows
-    if (enq_emit(c, 2, st, d_in, lo, hi, d_eg, d_status)) return;
-  } else {
-    // one branch per direction, each ending with its own plane's emit
-    enq_common(c, st);
-    HIPCHK(hipEventRecord(c->fork_ev, st));
-    HIPCHK(hipStreamWaitEvent(st2, c->fork_ev, 0));
-    const bool stagger = c->graph_stagger && st2 != st;
-    for (int d = 0; d < 2; d++) {
-      hipStream_t s = d ? st2 : st;
-      enq_peer_rows(c, d, s);
-      enq_member(c, d, s);
-      // stagger: the egress class rows start when the ingress ones are done
-      if (stagger && d == 1) HIPCHK(hipStreamWaitEvent(s, c->stagger_ev, 0));
-      enq_class_rows(c, d, s);
-      if (stagger && d == 0) HIPCHK(hipEventRecord(c->stagger_ev, s));
-      enq_emit(c, d, s, d ? d_eg : d_in, lo, hi);
-    }
-    HIPCHK(hipEventRecord(c->join_ev, st2));
-    HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
+    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status)) return;
   }
   // The step always ends with the status-plane copy (into a sink buffer when the caller passed no
   // status pointer), so every captured graph has the same shape: one node after the join.
@@ -3145,7 +2968,6 @@ static void ensure_cap_streams(cyc_ctx* c) {
   HIPCHK(hipEventCreateWithFlags(&c->ports_ev, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&c->stagger_ev, hipEventDisableTiming));
 }
 
 static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
@@ -3193,7 +3015,10 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     c->timed_graph = false;
   }
 
-  // 8. panic path: the first panicking job in job order, as the reference would hit it
+  // 8. panic path: the first panicking job in job order, as the reference would hit it.  Configs
+  // run in order (one RunProbeForConfig each); within one, the job expansion (may panic on a pod
+  // without containers) precedes the evaluation, which precedes the table build (duplicate keys).
+  uint32_t eval_cfg = pb.n_cfg, eval_s = 0, eval_d = 0, eval_idx = 0;
   if (pb.may_err) {
     if (P >= (1u << 24) || K > 65536)  // k_first_error's job-order key: (s*P + d)*65536 + idx < 2^64
       throw Panic{CYC_ERR_ARG, "inputs that can panic are limited to 2^24 pods and 65536 job slots"};
@@ -3221,20 +3046,21 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     std::vector<unsigned long long> first(std::max<uint32_t>(pb.n_cfg, 1), ~0ull);
     HIPCHK(hipMemcpyAsync(first.data(), c->first_err.p, uint64_t(pb.n_cfg) * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    uint32_t cfg = 0;
-    while (cfg < pb.n_cfg && first[cfg] == ~0ull) cfg++;
-    if (cfg < pb.n_cfg) {
-      const uint32_t idx = uint32_t(first[cfg] % 65536);
-      const uint64_t rest = first[cfg] / 65536;
-      const uint32_t d = uint32_t(rest % P), s = uint32_t(rest / P);
-      // duplicate-key fatal of an EARLIER config's table wins (tables are built per config)
-      for (uint32_t cc = 0; cc < cfg; cc++)
-        if (!pb.dup_key_msg[cc].empty()) return fail(c, CYC_ERR_DUPLICATE_KEY, pb.dup_key_msg[cc]);
-      return describe_panic(c, s, d, cfg, idx);
-    }
+    for (uint32_t cc = 0; cc < pb.n_cfg; cc++)
+      if (first[cc] != ~0ull) {
+        eval_cfg = cc;
+        eval_idx = uint32_t(first[cc] % 65536);
+        const uint64_t rest = first[cc] / 65536;
+        eval_d = uint32_t(rest % P);
+        eval_s = uint32_t(rest / P);
+        break;
+      }
   }
-  for (uint32_t cc = 0; cc < pb.n_cfg; cc++)
+  for (uint32_t cc = 0; cc < pb.n_cfg; cc++) {
+    if (pb.expand_panic[cc]) return fail(c, CYC_ERR_PANIC_RUNTIME, "runtime error: index out of range [0] with length 0");
+    if (cc == eval_cfg) return describe_panic(c, eval_s, eval_d, eval_cfg, eval_idx);
     if (!pb.dup_key_msg[cc].empty()) return fail(c, CYC_ERR_DUPLICATE_KEY, pb.dup_key_msg[cc]);
+  }
   return (int)CYC_OK;
 }
 
@@ -3371,7 +3197,6 @@ void cyc_ctx_destroy(cyc_ctx* c) {
     if (c->ports_ev) (void)hipEventDestroy(c->ports_ev);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
-    if (c->stagger_ev) (void)hipEventDestroy(c->stagger_ev);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -3667,126 +3492,35 @@ int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
 int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return CYC_ERR_ARG;
   if (c->stream) (void)hipSetDevice(c->device);  // drop_graph may destroy this context's execs
-  if (std::string(name) == "emit_variant") {
-    c->emit_variant = int(value);
+  const std::string n(name);
+  auto range = [&](int64_t lo, int64_t hi) {
+    if (value < lo || value > hi) throw Panic{CYC_ERR_ARG, n + " must be in " + std::to_string(lo) + ".." + std::to_string(hi)};
+  };
+  return guarded(c, [&]() -> int {
+    if (n == "graphs") range(-1, 2), c->use_graphs = int(value);
+    else if (n == "front_fused") range(0, 1), c->front_fused = int(value);
+    else if (n == "pod_words") range(-1, 1), c->pod_words = int(value);
+    else if (n == "pod_rows") range(-1, 1), c->pod_rows = int(value);
+    else if (n == "member_wave") range(-1, 1), c->member_wave = int(value);
+    else if (n == "class_rpb") range(1, 64), c->class_rpb_opt = value;
+    else if (n == "ip_group") range(1, 64), c->ip_group = uint32_t(value);
+    else return fail(c, CYC_ERR_ARG, "unknown option " + n);
     drop_graph(c);
     return (int)CYC_OK;
-  }
-  if (std::string(name) == "emit_chunk") {
-    if (value < 1) return fail(c, CYC_ERR_ARG, "emit_chunk must be >= 1");
-    c->emit_chunk = value;
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "emit_blocks") {
-    if (value < 0) return fail(c, CYC_ERR_ARG, "emit_blocks must be >= 0");
-    c->emit_blocks = value;
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "class_variant_in" || std::string(name) == "class_variant_eg") {
-    if (value < 0 || value > 3) return fail(c, CYC_ERR_ARG, "class_variant must be 0..3");
-    c->class_variant[std::string(name) == "class_variant_eg" ? 1 : 0] = int(value);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "graph_branches") {
-    c->graph_branches = value != 0;
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "pod_words") {
-    if (value < -1 || value > 1) return fail(c, CYC_ERR_ARG, "pod_words must be -1, 0 or 1");
-    c->pod_words = int(value);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "pod_rows") {
-    if (value < -1 || value > 1) return fail(c, CYC_ERR_ARG, "pod_rows must be -1, 0 or 1");
-    c->pod_rows = int(value);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "member_wave") {
-    if (value < -1 || value > 1) return fail(c, CYC_ERR_ARG, "member_wave must be -1, 0 or 1");
-    c->member_wave = int(value);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "emit_deal") {
-    c->emit_deal = int(value != 0);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "emit_interleave") {
-    if (value < -1 || value > 1) return fail(c, CYC_ERR_ARG, "emit_interleave must be -1, 0 or 1");
-    c->emit_interleave = int(value);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "emit_merged") {
-    c->emit_merged = int(value != 0);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "class_rpb") {
-    if (value < 1 || value > 64) return fail(c, CYC_ERR_ARG, "class_rpb must be 1..64");
-    c->class_rpb_opt = value;
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "ip_group") {
-    if (value < 1 || value > 64) return fail(c, CYC_ERR_ARG, "ip_group must be 1..64");
-    c->ip_group = uint32_t(value);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "port_bits") {
-    c->port_bits = int(value != 0);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "front_fused") {
-    c->front_fused = int(value != 0);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "graph_stagger") {
-    c->graph_stagger = int(value != 0);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  if (std::string(name) == "graphs") {
-    if (value < -1 || value > 2) return fail(c, CYC_ERR_ARG, "graphs must be -1, 0, 1 or 2");
-    c->use_graphs = int(value);
-    drop_graph(c);
-    return (int)CYC_OK;
-  }
-  return fail(c, CYC_ERR_ARG, std::string("unknown option ") + name);
+  });
 }
 
 int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   if (!c || !name || !value) return CYC_ERR_ARG;
   const std::string n(name);
-  if (n == "emit_variant") *value = c->emit_variant;
-  else if (n == "emit_blocks") *value = c->emit_blocks;
-  else if (n == "emit_chunk") *value = c->emit_chunk;
-  else if (n == "class_variant_in") *value = c->class_variant[0];
-  else if (n == "class_variant_eg") *value = c->class_variant[1];
-  else if (n == "graph_branches") *value = c->graph_branches;
-  else if (n == "graph_stagger") *value = c->graph_stagger;
+  if (n == "graphs") *value = c->use_graphs;
   else if (n == "front_fused") *value = c->front_fused;
-  else if (n == "port_bits") *value = c->port_bits;
-  else if (n == "ip_group") *value = c->ip_group;
+  else if (n == "pod_rows") *value = c->pod_rows;
+  else if (n == "member_wave") *value = c->member_wave;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
+  else if (n == "ip_group") *value = c->ip_group;
   else if (n == "launch") *value = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);  // in effect
   else if (n == "front_fused_active") *value = front_fused_ok(c) ? 1 : 0;
-  else if (n == "emit_merged") *value = c->emit_merged;
-  else if (n == "emit_interleave") *value = c->emit_interleave;
-  else if (n == "emit_deal") *value = c->emit_deal;
-  else if (n == "member_wave") *value = c->member_wave;
-  else if (n == "pod_rows") *value = c->pod_rows;
-  else if (n == "graphs") *value = c->use_graphs;
   else if (n == "pod_words") {
     if (!c->prepared) return fail(c, CYC_ERR_ARG, "pod_words: call cyc_probe_prepare first");
     *value = ido_mode(c) ? 1 : 0;

@@ -1101,6 +1101,13 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
   pb.slot_desc.assign(size_t(pb.P) * pb.K, -1);
   pb.slot_status.assign(size_t(pb.P) * pb.K, 0);
   pb.dup_key_msg.assign(probes.size(), "");
+  pb.expand_panic.assign(probes.size(), 0);
+  {
+    bool bare = false, any_cont = false;
+    for (auto& p : res.pods) (p.conts.empty() ? bare : any_cont) = true;
+    for (size_t c = 0; c < probes.size(); c++)  // PortProtocol: every (from, to) pair builds a job;
+      pb.expand_panic[c] = bare && (probes[c].all_available ? any_cont : true);  // AllAvailable: one per dst container
+  }
   std::unordered_map<std::string, int> key_count;
   bool dup_pod = false;
   std::string dup_pod_key;

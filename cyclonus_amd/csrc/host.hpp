@@ -181,6 +181,9 @@ struct Problem {
   bool may_err = false;
   // first duplicate table key per config, if any (table.go:45 via utils.DoOrDie)
   std::vector<std::string> dup_key_msg;
+  // per config: the job expansion itself panics (a pod without containers is some job's podFrom:
+  // FromContainer = podFrom.Containers[0].Name, resources.go:296,349 -> index out of range)
+  std::vector<uint8_t> expand_panic;
 };
 
 Problem build_problem(const PolicyIR& pol, const Resources& res, const std::vector<ProbeConfig>& probes);

@@ -48,7 +48,9 @@ typedef enum {
   CYC_ERR_DUPLICATE_KEY = 7,   /* table.go:45 via utils.DoOrDie (log.Fatalf) */
   CYC_ERR_HIP = 8,
   CYC_ERR_OOM = 9,
-  CYC_ERR_RCCL = 10
+  CYC_ERR_RCCL = 10,
+  CYC_ERR_PANIC_RUNTIME = 11   /* Go runtime panic in the job expansion: a pod without containers is a
+                                  job's podFrom (resources.go:296,349, Containers[0]) */
 } cyc_status;
 
 typedef enum {
@@ -150,50 +152,34 @@ const char* cyc_table_error(const cyc_table* t);
 void cyc_table_destroy(cyc_table* t);
 
 /* Average device time (ms) of the last run's kernels, measured with HIP events on the launch
- * stream: [0] whole pipeline, [1] the emit launch(es) (the HBM-roofline kernel; one launch writes
- * both planes unless "emit_merged" is 0), [2] class rows of both directions.  Graph runs report
- * only [0] ([1], [2] = -1). */
+ * stream: [0] whole pipeline, [1] the emit launch (the HBM-roofline kernel; one launch writes both
+ * planes), [2] class rows of both directions.  Graph runs report only [0] ([1], [2] = -1). */
 int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 
 /* Diagnostic: number of distinct classes (class rows computed) of the last run, [0] ingress,
  * [1] egress (synchronises the device). */
 int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
 
-/* Tuning knobs (no effect on results): "emit_variant" selects the emit kernel: -1 (default) =
- * auto (10 for plane rows of >= 64 KB, 11 for >= 16 KB, else 9), 0..5 one block per row with
- * different store patterns, 6 rows dealt to the XCDs in chunks ("emit_chunk" rows), 7 / 8 one
- * block per 2 / 4 rows, 9 the flat multi-row sweep (~32 KB of rows per block, for short rows),
- * 10 / 11 one 512- / 256-thread block per row covering it in a single pass;
- * "class_variant_in" / "class_variant_eg" 0..3 the class-row kernel shape (bit 0: 4 job slots
- * per thread instead of 8; bit 1: block rows stride over the class representatives);
- * "emit_blocks" the persistent emit grid (0 = one block per row); "emit_merged" (default 1) writes
- * both planes in one emit launch; "emit_interleave" -1 (default: auto = 1 for planes of >= 8 GB)
- * / 0 / 1 alternates the two planes' rows in that launch's row list; "emit_deal" (default 0) deals
- * the rows of emit variants 10 / 11 to the XCDs in chunks of "emit_chunk" rows; "graph_branches" (default 1) runs ingress and egress as two
- * concurrent branches of the step graph; "graph_stagger" (default 1, two-launch emit only) starts
- * the egress class rows after the ingress ones;
- * "pod_words" -1 (default: auto) / 0 / 1 has the class rows read pod-peer words from materialised
- * peer rows (0) or expand them from per-identity outcomes through each word's identity runs (1);
- * "pod_rows" -1 (default: auto = 1 when identities >= pods / 2) / 0 / 1 builds materialised
- * pod-peer rows through identity outcomes and word runs (0) or per pod with one ballot per word (1);
- * "member_wave" -1 (default: auto = 1 for <= 4096 identities) / 0 / 1 computes target membership
- * with a thread (0) or a wave (1) per pod identity;
- * "front_fused" (default 1) runs the front (selectors .. class rows) as 5 launches on one stream,
- * each a concatenation of independent block ranges of both directions (IDO builds with dense
- * selectors and class_variant bit 0 set; otherwise the two-branch DAG); "class_rpb" (default 4,
- * 1..64) class representatives per IDO class-row block; "port_bits" (default 1) has the egress
- * class rows test port matchers through per-matcher descriptor bit rows (<= 32 descriptors);
- * "ip_group" (default 8, 1..64) IP-peer tests per wave in the IP rows;
- * "graphs" -1 (default: auto = 2 when the fused front applies, else 1); 1 replays the pipeline as
- * one captured hipGraph when the inputs cannot panic (then cyc_last_timings reports only the
- * whole-pipeline time); 2 enqueues the same launches eagerly (the fused front on the caller's
- * stream, or the three-stream DAG), 0 runs every kernel in order on the caller's stream with
- * per-phase events.  cyc_get_option also reports "launch" (the graphs mode in effect) and
- * "front_fused_active" (needs cyc_probe_prepare). */
+/* Diagnostic path selectors (results never change; the GPU tests force every path):
+ *   "graphs"      -1 (default: auto = 2 when the fused front applies, else 1); 1 replays the step as
+ *                 one captured hipGraph when the inputs cannot panic (then cyc_last_timings reports
+ *                 only the whole-pipeline time); 2 enqueues the same launches eagerly (the fused
+ *                 front on the caller's stream, or the three-stream DAG); 0 runs every kernel in
+ *                 order on the caller's stream with per-phase events
+ *   "front_fused" 1 (default): the front as block-range-fused launches on one stream, one per
+ *                 dependency level (no-panic builds with dense selectors); 0: the two-branch DAG
+ *   "pod_words"   -1 (default: auto) / 0 / 1: class rows read pod-peer words from materialised peer
+ *                 rows (0) or expand them from per-identity outcomes through each word's identity
+ *                 runs (1, needs <= 4 runs per word and no possible panic)
+ *   "pod_rows"    -1 (default: auto = 1 when identities >= pods / 2) / 0 / 1: materialised pod-peer
+ *                 rows through identity outcomes and word runs (0) or per pod (1)
+ *   "member_wave" -1 (default: auto = 1 for <= 4096 identities) / 0 / 1: target membership with a
+ *                 thread (0) or a wave (1) per pod identity
+ *   "class_rpb"   4 (default, 1..64): class representatives per identity-set class-row block
+ *   "ip_group"    8 (default, 1..64): IP peers per IP-row block
+ * cyc_get_option also reports "launch" (the graphs mode in effect) and "front_fused_active" (both
+ * need cyc_probe_prepare); "pod_words" reports the mode the prepared probe uses (0 or 1). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
-
-/* The setting in effect for a tuning knob of cyc_set_option; for "pod_words" the mode the
- * prepared probe actually uses (0 or 1, auto resolved; needs cyc_probe_prepare). */
 int cyc_get_option(cyc_ctx* ctx, const char* name, int64_t* value);
 
 /* Single-cell API (policy.go:131-174): traffic_json is a JSON array of matcher.Traffic objects;

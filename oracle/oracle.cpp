@@ -1110,6 +1110,17 @@ int orc_probe_run(void* hv, const char* probes_json, uint8_t* status, uint64_t* 
     }
     for (size_t c = 0; c < cfgs.size(); c++) {
       int nslot = (c + 1 < cfgs.size() ? off[c + 1] : K) - off[c];
+      // GetJobsForProbeConfig (resources.go:284-364) builds every job of this config first, and each
+      // job reads podFrom.Containers[0].Name (:296, :349): a container-less source pod panics there
+      for (size_t s = 0; s < P; s++)
+        for (size_t d = 0; d < P; d++) {
+          const bool builds_job = !cfgs[c].allAvailable || !pods[d].containers.empty();
+          if (builds_job && pods[s].containers.empty()) {
+            set_err(err, errcap, "runtime error: index out of range [0] with length 0");
+            if (panic_cell) *panic_cell = -1;
+            return 1;
+          }
+        }
       for (size_t s = 0; s < P; s++)
         for (size_t d = 0; d < P; d++)
           for (int i = 0; i < nslot; i++) {

@@ -1,0 +1,20 @@
+"""Build an A/B variant of libcyclonus_hip.so with extra -D flags (dev helper):
+    python scripts/build_variant.py NAME -DCYC_PL_BATCH=16   -> cyclonus_amd/_build/var_NAME/libcyclonus_hip.so
+Run it with CYC_HIP_LIB=<that path> (cyclonus_amd/_lib.py)."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from cyclonus_amd import build as b  # noqa: E402
+
+name, defs = sys.argv[1], sys.argv[2:]
+out = os.path.join(b.BUILD, f"var_{name}")
+os.makedirs(out, exist_ok=True)
+common = ["-O3", "-std=c++17", "-fPIC", "-I", b.CSRC, "-I", b.INCLUDE, *defs]
+host = os.path.join(b.BUILD, "host.cpp.o")
+eng = os.path.join(out, "engine.hip.o")
+subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", *common, "-munsafe-fp-atomics", "-c", os.path.join(b.CSRC, "engine.hip"), "-o", eng], check=True)
+subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "libcyclonus_hip.so"), host, eng], check=True)
+print(os.path.join(out, "libcyclonus_hip.so"))

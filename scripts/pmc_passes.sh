@@ -1,0 +1,10 @@
+# PMC passes (each its own run) over eager steps: pmc_passes.sh OUT CONFIG [NAME=VALUE ...]
+set -e
+OUT=gpurun_out/$1; CFG=$2; shift 2; mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+P="python3 scripts/profile_eager.py $CFG 3 $@"
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $OUT/sq1_$CFG -o sq1 -- $P > $OUT/sq1_$CFG.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/sq2_$CFG -o sq2 -- $P > $OUT/sq2_$CFG.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/tcc_$CFG -o tcc -- $P > $OUT/tcc_$CFG.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch_$CFG -o fetch -- $P > $OUT/fetch_$CFG.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write_$CFG -o write -- $P > $OUT/write_$CFG.log 2>&1

@@ -1,7 +1,7 @@
 """Run N eager (non-graph) pipeline steps of a synthetic config, for rocprofv3 --kernel-trace --stats
 (per-kernel durations without the two-branch graph overlap).
 
-    rocprofv3 --kernel-trace --stats -d OUT -o run -- python scripts/profile_eager.py config3 20
+    rocprofv3 --kernel-trace --stats -d OUT -o run -- python scripts/profile_eager.py config3 20 [NAME=VALUE ...]
 """
 import json
 import os
@@ -15,6 +15,7 @@ from cyclonus_amd.engine import Engine
 
 name = sys.argv[1] if len(sys.argv) > 1 else "config3"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+opts = [a.split("=") for a in sys.argv[3:]]  # cyc_set_option NAME=VALUE
 data = synth.CONFIGS[name]()
 eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
 sh = eng.prepare(data["probes"])
@@ -24,6 +25,8 @@ d_eg = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
 d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 eng.set_option("graphs", 0)
+for k, v in opts:
+    eng.set_option(k, int(v))
 for _ in range(n):
     eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), st)
 torch.cuda.synchronize()

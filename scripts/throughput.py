@@ -1,7 +1,7 @@
 """Back-to-back step throughput (what bench.py times) under cyc_set_option settings, interleaved
 repetitions so box drift hits every setting alike.
 
-    python scripts/throughput.py config3 emit_variant=0,9 [steps=20] [reps=3] [shards=N] [rank=R] [init.<option>=v]
+    python scripts/throughput.py config3 ip_group=4,8 [steps=20] [reps=3] [shards=N] [rank=R] [init.<option>=v]
 """
 import itertools
 import json

@@ -217,6 +217,9 @@ def test_config5_generate_sweep_batched(gpu):
 
 
 def test_graph_and_eager_paths_agree(gpu):
+    """Every launch path gives the same table: graph replay / re-capture, the DAG enqueued eagerly,
+    eager with phase events, the fused front or the DAG, membership by wave or thread, pod-peer
+    rows per pod or through word runs, IP rows with 1..64 peers per block."""
     import torch
 
     eng = Engine(0)
@@ -226,29 +229,14 @@ def test_graph_and_eager_paths_agree(gpu):
         sh = eng.prepare(probes)
         P, K, W = sh["pods"], sh["slots"], sh["words"]
         outs = []
-        # (graphs, graph_branches, emit_blocks, emit_variant): eager, two-branch graph (replayed),
-        # single-branch graph, tiny persistent emit grid, one block per row, other store variants,
-        # the graph's DAG enqueued eagerly on three streams (graphs = 2)
-        for graphs, branches, blocks, variant, cls in ((0, 1, 1024, 0, 0), (1, 1, 1024, 0, 0), (1, 1, 1024, 0, 0),
-                                                       (1, 0, 1024, 0, 1), (1, 1, 8, 0, 2), (0, 1, 0, 0, 3),
-                                                       (0, 1, 16, 3, 1), (1, 1, 0, 5, 2), (1, 1, 0, 6, 3), (0, 0, 0, 6, 0),
-                                                       (1, 1, 0, 7, 1), (0, 1, 0, 8, 2), (1, 0, 0, 8, 0), (1, 1, 0, 9, 1),
-                                                       (0, 1, 0, 9, 3), (1, 1, 0, -1, 0), (1, 1, 0, 10, 2), (0, 1, 0, 10, 1),
-                                                       (2, 1, 0, -1, 1), (2, 0, 0, 9, 2), (2, 1, 0, 5, 3), (1, 1, 0, 11, 0),
-                                                       (0, 1, 0, 11, 2)):
-            eng.set_option("emit_chunk", 1 + seed % 3)
-            eng.set_option("pod_rows", (variant + seed) % 3 - 1)  # direct / word runs / auto
-            eng.set_option("emit_interleave", (variant + seed) % 2)  # merged emit: planes alternate
-            eng.set_option("emit_deal", int(variant in (10, 11) and seed % 2 == 0))  # wide emit: chunked XCD deal
-            eng.set_option("emit_merged", int(variant != 5))
-            eng.set_option("port_bits", (variant + seed + cls) % 2)  # egress port test: bit rows / byte table
-            eng.set_option("ip_group", (1, 3, 8)[(variant + seed) % 3])  # IP rows: tests per wave
+        for graphs, fused, mw, pod_rows, grp in ((0, 1, -1, -1, 8), (1, 1, -1, -1, 8), (1, 1, -1, -1, 8), (2, 1, 1, 1, 3),
+                                                 (1, 0, 0, 0, 1), (2, 0, -1, 1, 64), (0, 0, 1, 0, 8), (-1, 1, 0, -1, 5),
+                                                 (-1, 0, 1, 1, 2)):
             eng.set_option("graphs", graphs)
-            eng.set_option("graph_branches", branches)
-            eng.set_option("emit_blocks", blocks)
-            eng.set_option("emit_variant", variant)
-            eng.set_option("class_variant_in", cls)
-            eng.set_option("class_variant_eg", 3 - cls)
+            eng.set_option("front_fused", fused)
+            eng.set_option("member_wave", mw)
+            eng.set_option("pod_rows", pod_rows)
+            eng.set_option("ip_group", grp)
             d_in = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_eg = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_st = torch.zeros((P, K), dtype=torch.uint8, device="cuda")
@@ -348,25 +336,20 @@ def test_pod_words_from_identity_runs(gpu, seed):
     want = Oracle(pols, res).probe(probes)
     eng = Engine(0).build_policies(pols).load_resources(res)
     eng.prepare(probes)
-    # (pod_words, graphs, class_variant, front_fused, member_wave): 4 or 8 job slots per thread,
-    # graph and eager paths, the fused single-stream front and the two-branch DAG (replayed and
-    # enqueued eagerly), membership by wave or thread, and the PM path
-    # and several class representatives per class-row block (class_rpb)
-    for mode, graphs, cv, fused, mw, rpb in ((1, 1, 3, 1, -1, 1), (1, 1, 3, 1, 1, 3), (1, 1, 3, 1, 0, 4),
-                                             (1, 1, 3, 0, -1, 2), (1, 2, 3, 1, 0, 1), (1, 2, 3, 0, 1, 5),
-                                             (1, 0, 0, 1, -1, 2), (1, 0, 3, 1, -1, 3), (1, 1, 1, 1, -1, 4),
-                                             (0, 1, 3, 1, -1, 1), (0, 0, 0, 1, -1, 1)):
+    # (pod_words, graphs, front_fused, member_wave, class_rpb): graph and eager paths, the fused
+    # single-stream front and the two-branch DAG (replayed and enqueued eagerly), membership by wave
+    # or thread, several class representatives per class-row block, and the PM path
+    for mode, graphs, fused, mw, rpb in ((1, 1, 1, -1, 1), (1, 1, 1, 1, 3), (1, 1, 1, 0, 4), (1, 1, 0, -1, 2),
+                                         (1, 2, 1, 0, 1), (1, 2, 0, 1, 5), (1, 0, 1, -1, 2), (1, 0, 0, -1, 3),
+                                         (1, -1, 1, -1, 4), (0, 1, 1, -1, 1), (0, 0, 1, -1, 1), (0, 2, 0, 1, 1)):
         eng.set_option("pod_words", mode)
         eng.set_option("graphs", graphs)
-        eng.set_option("class_variant_in", cv)
-        eng.set_option("class_variant_eg", 2 if (fused and rpb == 3) else cv)  # 2: fused egress rows, 8 slots per thread
         eng.set_option("front_fused", fused)
         eng.set_option("member_wave", mw)
         eng.set_option("class_rpb", rpb)
-        eng.set_option("port_bits", (seed + rpb) % 2)
         assert eng.get_option("pod_words") == mode, "deployment-style words must allow the IDO path"
         for rep in range(2):  # the second run finds the hash tables the first one emptied
-            assert_same(want, eng.run_host(), f"seed {seed} pod_words {mode} graphs {graphs} variant {cv} "
+            assert_same(want, eng.run_host(), f"seed {seed} pod_words {mode} graphs {graphs} "
                                               f"fused {fused} member_wave {mw} rpb {rpb} run {rep}")
 
 
@@ -388,10 +371,11 @@ def test_edge_shapes(gpu, seed):
 
 
 @pytest.mark.parametrize("bad", [False, True])
-def test_direct_pod_rows_and_flat_emit(gpu, bad):
-    """Pod-peer rows computed per pod (pod_rows = 1) and through identity runs (0), and the flat
-    multi-row emit (emit_variant 9), one 256-thread block per row (0) and the single-pass 512-thread
-    block per row (10), membership by wave or by thread: all equal the oracle, panics too."""
+def test_direct_pod_rows_and_membership(gpu, bad):
+    """Pod-peer rows computed per pod (pod_rows = 1) and through identity runs (0), membership by
+    wave or by thread, on growing problems (the emit picks its kernel by row length: 8-byte copies
+    for odd word counts, the flat multi-row sweep, single-pass blocks): all equal the oracle,
+    panics too."""
     eng = Engine(0)
     for seed in range(40):
         pols, res, probes = random_problem(70_000 + seed, n_pods=30 + 7 * seed, bad=bad)
@@ -400,21 +384,43 @@ def test_direct_pod_rows_and_flat_emit(gpu, bad):
         except OraclePanic as e:
             want = Panicked(str(e))
         eng.build_policies(pols).load_resources(res)
-        for pod_rows, variant, mw in ((1, 9, 1), (0, 0, 0), (1, 0, 1), (0, 9, 0), (1, 10, 1), (0, 11, 0)):
+        for pod_rows, mw in ((1, 1), (0, 0), (1, 0), (0, 1)):
             eng.set_option("pod_rows", pod_rows)
-            eng.set_option("emit_variant", variant)
             eng.set_option("member_wave", mw)  # membership: a wave (1) or a thread (0) per identity
             try:
                 eng.prepare(probes)
                 got = eng.run_host()
             except CyclonusPanic as e:
                 got = Panicked(e.msg)
-            assert_same(want, got, f"seed {seed} pod_rows {pod_rows} emit {variant}")
+            assert_same(want, got, f"seed {seed} pod_rows {pod_rows} member_wave {mw}")
+
+
+def test_emit_row_lengths(gpu):
+    """The emit kernels by plane-row length (K x W words): odd word counts (8-byte copies), short
+    rows (flat multi-row sweep), 16-64 KB rows (256-thread single pass) and >= 64 KB rows
+    (512-thread single pass), each bit-exact vs the oracle on sampled cells and whole rows."""
+    from cyclonus_amd import synth
+
+    for n_ns, probes in ((3, [{"Port": 80, "Protocol": "TCP"}]), (10, [{"AllAvailable": True}]),
+                         (20, [{"AllAvailable": True}] * 1), (50, [{"AllAvailable": True}])):
+        data = synth.config3(n_ns=n_ns)
+        data["probes"] = probes
+        pols, res = data["policies"], data["resources"]
+        eng = Engine(0).build_policies(json.dumps(pols)).load_resources(json.dumps(res))
+        sh = eng.prepare(probes)
+        st, ing, eg = eng.run_host()
+        orc = Oracle(pols, res)
+        P, K = sh["pods"], sh["slots"]
+        rng = np.random.default_rng(n_ns)
+        for pod in [0, P - 1] + [int(x) for x in rng.integers(0, P, 6)]:
+            for k in range(K):
+                assert np.array_equal(ing[pod, k], orc.row(probes, "ingress", pod, k, threads=8)), (n_ns, pod, k)
+                assert np.array_equal(eg[pod, k], orc.row(probes, "egress", pod, k, threads=8)), (n_ns, pod, k)
 
 
 def test_graph_joins_without_status_or_rows(gpu):
     """Captured graphs for steps without a status plane (null pointer) or without rows (an empty
-    row range), with one or two emit launches, replayed and re-captured: results unchanged."""
+    row range), on the fused front and the DAG, replayed and re-captured: results unchanged."""
     import torch
 
     pols, res, probes = random_problem(90_001, n_pods=120)
@@ -423,8 +429,9 @@ def test_graph_joins_without_status_or_rows(gpu):
     sh = eng.prepare(probes)
     P, K, W = sh["pods"], sh["slots"], sh["words"]
     st = torch.cuda.current_stream().cuda_stream
-    for merged in (1, 0):
-        eng.set_option("emit_merged", merged)
+    eng.set_option("graphs", 1)
+    for merged in (1, 0):  # fused front / DAG
+        eng.set_option("front_fused", merged)
         for _ in range(3):  # replays of the same graph
             d_in = torch.zeros((P, K, W), dtype=torch.int64, device="cuda")
             d_eg = torch.zeros((P, K, W), dtype=torch.int64, device="cuda")
@@ -448,7 +455,7 @@ def test_launch_modes_and_knobs(gpu):
     fused = not eng.shape["may_panic"]  # no-panic build: the fused front applies
     assert eng.get_option("front_fused_active") == int(fused)
     assert eng.get_option("launch") == (2 if fused else 1)
-    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("port_bits", 0), ("graphs", 1), ("graphs", -1)):
+    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("ip_group", 3), ("graphs", 1), ("graphs", -1)):
         eng.set_option(name, v)
         assert eng.get_option(name) == v
         assert_same(want, eng.run_host(), f"{name}={v}")
@@ -457,7 +464,7 @@ def test_launch_modes_and_knobs(gpu):
     assert_same(want, eng.run_host(), "DAG graph")
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
-    for name, v in (("class_rpb", 0), ("class_rpb", 65), ("graphs", 3)):
+    for name, v in (("class_rpb", 0), ("class_rpb", 65), ("graphs", 3), ("emit_variant", 1), ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
     # a build that may panic keeps the graph path (the panic walk needs the ordered peer rows)
