@@ -394,10 +394,11 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
 // Also records each IP peer's nonzero word span in rng[2 * peer] (first word) and
 // rng[2 * peer + 1] (~last word), both atomicMin'd from 0xFFFFFFFF: CIDRs are address ranges and
 // pods of a namespace have neighbouring addresses, so a peer's row is mostly zero words the
-// class rows can skip without loading them.  Only NONZERO words are stored: cnz[peer][chunk]
-// (one u64 per 64-word chunk, written by the chunk's wave) marks them, and readers AND the PM
-// word with its cnz bit (both loads issued together), so the zero words — most of a row — cost no
-// HBM writes at all.
+// class rows can skip without loading them.  Rows are stored chunk-dense: cnz[peer][chunk] (one
+// u64 per 64-word chunk, written by the chunk's wave) has the chunk's nonzero words; a chunk with
+// none stores no PM word at all, any other chunk stores all 64.  Readers issue the PM and cnz loads
+// together and drop the PM word of an all-zero chunk, so the zero chunks — most of a row — cost
+// no HBM writes.
 __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
                                             const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
                                             uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng,
@@ -424,8 +425,10 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
       }
     }
   }
-  if (valid && uniform && res) PM[uint64_t(t.peer) * W + w] = res;
   uint64_t nz = __ballot(valid && uniform && res != 0);
+  // chunk-dense: a chunk with any nonzero word (or a straddling word still to test) stores all its
+  // words; an all-zero chunk stores none, only its mask word below
+  if ((nz | __ballot(valid && !uniform)) && valid && uniform) PM[uint64_t(t.peer) * W + w] = res;
   const uint32_t w0 = chunk * 64;
   uint32_t lo = nz ? w0 + __ffsll((unsigned long long)nz) - 1 : 0xFFFFFFFFu;
   uint32_t hi = nz ? w0 + 63 - __clzll((long long)nz) : 0u;
@@ -448,7 +451,7 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
       }
     }
     const uint64_t m = __ballot(o == 1);
-    if (lane == 0 && m) PM[uint64_t(t.peer) * W + ww] = m;
+    if (lane == 0) PM[uint64_t(t.peer) * W + ww] = m;
     if (m) {
       nz |= 1ull << wl;
       lo = min(lo, ww);
@@ -464,9 +467,9 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
   }
 }
 
-// A nonzero-word mask bit of IP peer j's PM row (see ip_row_word): ~0 if word w was written.
+// ~0 if word w of IP peer j's PM row was stored (its chunk has a nonzero word; see ip_row_word).
 __device__ __forceinline__ uint64_t cnz_mask(const uint64_t* __restrict__ cnz, uint32_t W, uint32_t j, uint32_t w) {
-  return ((cnz[uint64_t(j) * ((W + 63) / 64) + w / 64] >> (w % 64)) & 1) ? ~0ull : 0ull;
+  return cnz[uint64_t(j) * ((W + 63) / 64) + w / 64] ? ~0ull : 0ull;
 }
 
 // A block handles one group of `grp` IP peers over 4 chunks of 64 words (a wave per chunk, lane =
@@ -981,7 +984,10 @@ __device__ __forceinline__ uint64_t port_mask(const RowArgs& a, const uint8_t* p
     if (pok[d]) okm |= dm[uint64_t(d) * a.W];
   return okm;
 }
-constexpr uint32_t PEER_BATCH = 4;
+#ifndef CYC_PEER_BATCH
+#define CYC_PEER_BATCH 4
+#endif
+constexpr uint32_t PEER_BATCH = CYC_PEER_BATCH;  // IDO class rows: IP peers whose PM words are loaded at once
 
 template <bool EGRESS, bool ERR, int KC>
 __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uint32_t kc, uint32_t w) {
@@ -1101,6 +1107,10 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
 #ifndef CYC_PL_BATCH
 #define CYC_PL_BATCH 8  // list entries whose PM words are loaded at once (16: occupancy 6 -> 4)
 #endif
+#ifndef CYC_PL_SPAN
+#define CYC_PL_SPAN 0  // class rows by spans (pl_span_rows) where the port bit rows allow it
+#endif
+constexpr bool PL_SPAN = CYC_PL_SPAN != 0;
 #ifndef CYC_PL_THREADS
 #define CYC_PL_THREADS 128  // threads per class-row block (one representative per block)
 #endif
@@ -1113,6 +1123,9 @@ __device__ __forceinline__ uint64_t pl_word(const RowArgs& a, const uint4& e, ui
   if (e.x == PL_ONES) return ~0ull;
   const uint32_t lo = e.z & ~PL_IP;
   if (e.x == PL_SKIP || w < lo || w > e.w) return 0ull;
+#ifdef CYC_DIAG_NO_PM
+  return uint64_t(e.x) * 0x9E3779B97F4A7C15ull ^ w;
+#endif
   const uint64_t v = a.PM[uint64_t(e.x) * a.W + w];
   return (e.z & PL_IP) ? v & cnz_mask(a.ip_cnz, a.W, e.x, w) : v;
 }
@@ -1124,9 +1137,12 @@ struct PlShared {  // one per block, shared by both directions' instantiations o
 };
 
 #ifndef CYC_PL_ITEMS
-#define CYC_PL_ITEMS 2
+#define CYC_PL_ITEMS 1
 #endif
 constexpr int PL_ITEMS = CYC_PL_ITEMS;
+#ifndef CYC_PL_WAVES
+#define CYC_PL_WAVES  // e.g. __attribute__((amdgpu_waves_per_eu(8, 8))) for A/Bs
+#endif
 
 // PL_ITEMS (slot chunk, pod word) items of class representative i: items it0, it0 + blockDim.x, ...
 template <bool EGRESS>
@@ -1163,50 +1179,60 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
       allow[q][kk] = allow_all ? ~0ull : 0ull;
     }
   }
-  if (!allow_all && fast) {
-    // the entries are the same for every thread of the block: their fields are read once per wave
-    // into scalar registers; entries without a passing slot were dropped at build time
+  if (!allow_all && fast && m <= PL_LDS) {
+    // The entries are the same for every thread of the block: a batch's fields are read from LDS
+    // into scalar registers first, then all of the batch's PM (and nonzero-mask) loads are issued,
+    // and only then combined — one memory round trip per batch, not one per entry.
     for (uint32_t x0 = 0; x0 < m; x0 += PL_BATCH) {
-      uint64_t pm[NI][PL_BATCH];
-      uint32_t bits[PL_BATCH];
+      uint32_t ex[PL_BATCH], ez[PL_BATCH], ew[PL_BATCH], bits[PL_BATCH];
 #pragma unroll
       for (uint32_t u = 0; u < PL_BATCH; u++) {
-        const uint32_t x = x0 + u;
-        uint4 e = make_uint4(PL_SKIP, 0u, 1u, 0u);
-        uint32_t b = 0;
-        if (x < min(m, PL_LDS)) {
-          e = sh.e[x];
-          b = sh.bits[x];
-        } else if (x < m) {
-          e = spill[x];
-          b = EGRESS ? a.portbits[e.y] : e.y;
-        }
-        e.x = __builtin_amdgcn_readfirstlane(e.x);
-        e.z = __builtin_amdgcn_readfirstlane(e.z);
-        e.w = __builtin_amdgcn_readfirstlane(e.w);
+        const uint32_t x = min(x0 + u, PL_LDS - 1);
+        uint4 e = sh.e[x];
+        const uint32_t b = sh.bits[x];
+        if (x0 + u >= m) e.x = PL_SKIP;
+        ex[u] = __builtin_amdgcn_readfirstlane(e.x);
+        ez[u] = __builtin_amdgcn_readfirstlane(e.z);
+        ew[u] = __builtin_amdgcn_readfirstlane(e.w);
         bits[u] = __builtin_amdgcn_readfirstlane(b);
-#pragma unroll
-        for (int q = 0; q < NI; q++) pm[q][u] = pl_word(a, e, w[q]);
       }
+      uint64_t v[NI][PL_BATCH], c[NI][PL_BATCH];
+#pragma unroll
+      for (uint32_t u = 0; u < PL_BATCH; u++)
+#pragma unroll
+        for (int q = 0; q < NI; q++) {
+          v[q][u] = 0;
+          c[q][u] = ~0ull;
+          if (ex[u] < PL_SKIP && w[q] >= (ez[u] & ~PL_IP) && w[q] <= ew[u]) {
+            v[q][u] = a.PM[uint64_t(ex[u]) * a.W + w[q]];
+            if (ez[u] & PL_IP) c[q][u] = a.ip_cnz[uint64_t(ex[u]) * ((a.W + 63) / 64) + w[q] / 64];
+          }
+        }
       uint64_t undecided = 0;
 #pragma unroll
-      for (int q = 0; q < NI; q++)
+      for (int q = 0; q < NI; q++) {
+        // entries are sorted by port bits: OR each run of equal bits first, then test its slots once
+        uint64_t acc = 0;
 #pragma unroll
-        for (int kk = 0; kk < KC; kk++) {
-          if (du[q][kk] < 0) continue;
-          if (EGRESS) {
+        for (uint32_t u = 0; u < PL_BATCH; u++) {
+          acc |= ex[u] == PL_ONES ? ~0ull : (c[q][u] ? v[q][u] : 0ull);
+          if (u + 1 < PL_BATCH && bits[u + 1] == bits[u]) continue;  // the run goes on (uniform)
+          if (acc) {
 #pragma unroll
-            for (uint32_t u = 0; u < PL_BATCH; u++) allow[q][kk] |= ((bits[u] >> uint32_t(du[q][kk])) & 1u) ? pm[q][u] : 0ull;
-          } else {  // ingress: the slot's port test is the same for the whole block
-#pragma unroll
-            for (uint32_t u = 0; u < PL_BATCH; u++)
-              if ((bits[u] >> (k0[q] + kk)) & 1u) allow[q][kk] |= pm[q][u];
+            for (int kk = 0; kk < KC; kk++) {
+              if (du[q][kk] < 0) continue;
+              if (EGRESS) allow[q][kk] |= ((bits[u] >> uint32_t(du[q][kk])) & 1u) ? acc : 0ull;
+              else if ((bits[u] >> (k0[q] + kk)) & 1u) allow[q][kk] |= acc;  // the same for the whole block
+            }
           }
-          undecided |= valid[q][kk] & ~allow[q][kk];
+          acc = 0;
         }
+#pragma unroll
+        for (int kk = 0; kk < KC; kk++) undecided |= valid[q][kk] & ~allow[q][kk];
+      }
       if (!undecided) break;
     }
-  } else if (!allow_all) {  // mixed descriptors / no bit rows (ingress K > 32): the byte port table
+  } else if (!allow_all) {  // mixed descriptors, no bit rows (ingress K > 32), lists past the LDS part
     for (uint32_t x = 0; x < m; x++) {
       const uint4 e = x < PL_LDS ? sh.e[x] : spill[x];
 #pragma unroll
@@ -1224,12 +1250,79 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
       const uint32_t k = k0[q] + kk;
+#ifdef CYC_DIAG_NO_STORE
+      if (k < a.K && (allow[q][kk] & valid[q][kk]) == 0x123456789ull) a.A[(uint64_t(i) * a.K + k) * a.W + w[q]] = 1;
+      continue;
+#endif
       if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w[q]] = allow[q][kk] & valid[q][kk];
     }
 }
 
+// The class rows by SPANS (port bit rows available, list in LDS): entries are walked once per
+// chunk of pod words, each thread ORing the PM words of the entries' nonzero spans that fall on
+// its own words into a per-(descriptor | slot) accumulator row in LDS — work in proportion to the
+// spans, not to words x entries (most entries cover a few words: CIDRs are address ranges) — and
+// the accumulators become the class rows in one pass over the words: egress through each word's
+// slot descriptor (DESCW, or the DM masks of mixed words), ingress slot by slot.
+constexpr uint32_t PL_ACC_BYTES = 16384;  // accumulator rows per block (dynamic LDS)
 template <bool EGRESS>
-__device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
+__device__ __forceinline__ void pl_span_rows(const RowArgs& a, const PlShared& sh, uint64_t* acc, uint32_t i, uint32_t m,
+                                             bool allow_all, uint64_t lastmask) {
+  const uint32_t NB = EGRESS ? a.D : a.K, bs = blockDim.x;
+  const uint32_t wc = max(64u, PL_ACC_BYTES / 8 / max(NB, 1u));  // words per chunk
+  for (uint32_t w0 = 0; w0 < a.W; w0 += wc) {
+    const uint32_t w1 = min(a.W, w0 + wc), nw = w1 - w0;
+    if (!allow_all) {
+      for (uint32_t x = threadIdx.x; x < NB * nw; x += bs) acc[x] = 0;
+      __syncthreads();
+      for (uint32_t x = 0; x < m; x++) {
+        const uint32_t ex = __builtin_amdgcn_readfirstlane(sh.e[x].x);
+        if (ex == PL_SKIP) continue;
+        const uint32_t ez = __builtin_amdgcn_readfirstlane(sh.e[x].z), ew = __builtin_amdgcn_readfirstlane(sh.e[x].w);
+        const uint32_t lo = max(ez & ~PL_IP, w0), hi = min(ew, w1 - 1);
+        if (lo > hi) continue;  // the entry's span misses this chunk
+        const uint32_t bits = __builtin_amdgcn_readfirstlane(sh.bits[x]);
+        // this thread's words are w0 + threadIdx.x + j * bs
+        uint32_t w = w0 + threadIdx.x;
+        if (w < lo) w += (lo - w + bs - 1) / bs * bs;
+        for (; w <= hi; w += bs) {
+          uint64_t pm = ~0ull;
+          if (ex != PL_ONES) {
+            pm = a.PM[uint64_t(ex) * a.W + w];
+            if (ez & PL_IP) pm &= cnz_mask(a.ip_cnz, a.W, ex, w);
+          }
+          if (!pm) continue;
+          for (uint32_t b = bits; b; b &= b - 1) acc[uint32_t(__ffs(b) - 1) * nw + (w - w0)] |= pm;  // own word: no race
+        }
+      }
+      __syncthreads();
+    }
+    for (uint32_t w = w0 + threadIdx.x; w < w1; w += bs) {
+      const uint64_t wmask = w == a.W - 1 ? lastmask : ~0ull;
+      for (uint32_t k = 0; k < a.K; k++) {
+        uint64_t v = 0;
+        if (EGRESS) {
+          const uint64_t valid = a.VALID[uint64_t(k) * a.W + w];
+          const int32_t du = a.DESCW[uint64_t(k) * a.W + w];
+          if (allow_all) v = valid;
+          else if (du >= 0) v = acc[uint32_t(du) * nw + (w - w0)] & valid;
+          else if (du == -1) {  // destinations with mixed job descriptors (rare)
+            const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
+            for (uint32_t d = 0; d < a.D; d++) v |= acc[d * nw + (w - w0)] & dm[uint64_t(d) * a.W];
+            v &= valid;
+          }
+        } else if (a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) {
+          v = (allow_all ? ~0ull : acc[k * nw + (w - w0)]) & wmask;
+        }
+        a.A[(uint64_t(i) * a.K + k) * a.W + w] = v;
+      }
+    }
+    __syncthreads();  // the accumulators are reused by the next chunk
+  }
+}
+
+template <bool EGRESS>
+__device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint64_t* acc, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
   ht_clear_slice(a, bid_, nblk_);
   const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC, items = nkc * a.W;
@@ -1241,7 +1334,15 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
     if (threadIdx.x == 0) sh.all = 0;
     uint32_t m = 0;
+#ifdef CYC_DIAG_NO_LIST
+    if (nt) {
+      if (threadIdx.x == 0) sh.all = 0;
+      __syncthreads();
+    }
+    for (uint32_t t0 = 0; t0 < 0; t0 += PL_TGT) {
+#else
     for (uint32_t t0 = 0; t0 < nt; t0 += PL_TGT) {  // targets in chunks: offsets, counts, prefix sums
+#endif
       const uint32_t ntc = min(PL_TGT, nt - t0);
       for (uint32_t t = threadIdx.x; t < ntc; t += blockDim.x) {
         const DTarget tg = a.tgt[lst[t0 + t]];
@@ -1278,10 +1379,13 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
           }
           if (EGRESS) {
             if (a.portbits) bits = a.portbits[pr.port];
-          } else if (a.K <= 32) {
+          } else if (a.K <= 32) {  // a bit per job slot of this representative
+            const uint32_t pb = a.portbits ? a.portbits[pr.port] : 0u;
             for (uint32_t k = 0; k < a.K; k++) {
               const uint64_t ik = uint64_t(i) * a.K + k;
-              if (a.id_status[ik] == CYC_JOB_VALID && a.portok[uint64_t(pr.port) * a.D + a.id_desc[ik]]) bits |= 1u << k;
+              if (a.id_status[ik] != CYC_JOB_VALID) continue;
+              const int32_t du = a.id_desc[ik];
+              if (a.portbits ? ((pb >> du) & 1u) : a.portok[uint64_t(pr.port) * a.D + du]) bits |= 1u << k;
             }
           }
           en.y = EGRESS || a.K > 32 ? pr.port : bits;  // spilled entries carry the bits themselves
@@ -1298,18 +1402,41 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
       m += mc;
       __syncthreads();
     }
+    if (threadIdx.x == 0 && m <= 64) {  // group entries by port bits: each group's slot test runs once
+      for (uint32_t x = 1; x < m; x++) {
+        const uint4 e = sh.e[x];
+        const uint32_t b = sh.bits[x];
+        uint32_t y = x;
+        for (; y > 0 && sh.bits[y - 1] > b; y--) {
+          sh.e[y] = sh.e[y - 1];
+          sh.bits[y] = sh.bits[y - 1];
+        }
+        sh.e[y] = e;
+        sh.bits[y] = b;
+      }
+    }
+    __syncthreads();
     const bool allow_all = nt == 0 || sh.all;
     const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
     // the class's (slot chunk, word) items, PL_ITEMS per thread at once (their loads overlap)
-    for (uint32_t it0 = threadIdx.x; it0 < items; it0 += PL_ITEMS * blockDim.x)
-      pl_items<EGRESS>(a, sh, spill, i, m, allow_all, kbits, it0, items, lastmask);
+#ifdef CYC_DIAG_NO_ITEMS
+    if (m < 100000) continue;
+#endif
+    const uint32_t NB = EGRESS ? a.D : a.K;
+    if (acc && kbits && m <= PL_LDS && NB <= 32) {
+      pl_span_rows<EGRESS>(a, sh, acc, i, m, allow_all, lastmask);
+    } else {
+      for (uint32_t it0 = threadIdx.x; it0 < items; it0 += PL_ITEMS * blockDim.x)
+        pl_items<EGRESS>(a, sh, spill, i, m, allow_all, kbits, it0, items, lastmask);
+    }
     __syncthreads();  // LDS reused by the next representative
   }
 }
 template <bool EGRESS>
 __global__ __launch_bounds__(256) void k_class_rows_pl(RowArgs a) {
   __shared__ PlShared sh;
-  class_rows_pl_blk<EGRESS>(a, sh, blockIdx.x, gridDim.x);
+  extern __shared__ uint64_t pl_acc[];
+  class_rows_pl_blk<EGRESS>(a, sh, PL_SPAN ? pl_acc : nullptr, blockIdx.x, gridDim.x);
 }
 
 // Class rows from identity sets (IDO builds).  Block = (class representative, KC job slots,
@@ -1539,11 +1666,13 @@ __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   else class_ident_blk<true, 4>(f.ra[1], b - f.nb[0], f.nb[1]);
 }
 // PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
-__global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
+__global__ __launch_bounds__(256) CYC_PL_WAVES void k_front_d_pm(FrontRows f) {
   __shared__ PlShared sh;
+  extern __shared__ uint64_t pl_acc[];
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_pl_blk<true>(f.ra[1], sh, b, f.nb[1]);
-  else class_rows_pl_blk<false>(f.ra[0], sh, b - f.nb[1], f.nb[0]);
+  uint64_t* acc = PL_SPAN ? pl_acc : nullptr;
+  if (b < f.nb[1]) class_rows_pl_blk<true>(f.ra[1], sh, acc, b, f.nb[1]);
+  else class_rows_pl_blk<false>(f.ra[0], sh, acc, b - f.nb[1], f.nb[0]);
 }
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
@@ -2607,8 +2736,8 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.PM = c->PM.as<uint64_t>();
   ra.ER = c->ER.as<uint64_t>();
   ra.portok = c->portok.as<uint8_t>();
-  // egress: descriptor bit rows (k_portbits in enq_common; the fused front sets its own)
-  ra.portbits = d == 1 && port_bits_on(c) && pb.pms.size() && pb.descs.size() ? c->portbits.as<uint32_t>() : nullptr;
+  // descriptor bit rows of the port table (k_portbits; computed whenever D <= 32)
+  ra.portbits = port_bits_on(c) && pb.pms.size() && pb.descs.size() ? c->portbits.as<uint32_t>() : nullptr;
   ra.D = D;
   ra.n_ident = dd.n;
   ra.K = K;
@@ -2671,8 +2800,8 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
     else k_class_rows_ido<true, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
   } else {  // per-class flattened peer lists (the IP word spans are final here)
-    if (d == 0) k_class_rows_pl<false><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
-    else k_class_rows_pl<true><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
+    if (d == 0) k_class_rows_pl<false><<<pl_blocks(c, d), PL_THREADS, PL_SPAN ? PL_ACC_BYTES : 0, st>>>(ra);
+    else k_class_rows_pl<true><<<pl_blocks(c, d), PL_THREADS, PL_SPAN ? PL_ACC_BYTES : 0, st>>>(ra);
   }
 }
 
@@ -2864,7 +2993,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (fc.nb[0] + fc.nb[1]) k_front_c<<<fc.nb[0] + fc.nb[1], 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
-    if (fd.nb[0] + fd.nb[1]) k_front_d_pm<<<fd.nb[0] + fd.nb[1], PL_THREADS, 0, st>>>(fd);
+    if (fd.nb[0] + fd.nb[1]) k_front_d_pm<<<fd.nb[0] + fd.nb[1], PL_THREADS, PL_SPAN ? PL_ACC_BYTES : 0, st>>>(fd);
     if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
     return true;
   }
