@@ -391,18 +391,20 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
   return (!lt128(mn, lo) && !lt128(hi, mx)) ? 1 : 2;
 }
 
-// Also records each IP peer's nonzero word span in rng[2 * peer] (first word) and
-// rng[2 * peer + 1] (~last word), both atomicMin'd from 0xFFFFFFFF: CIDRs are address ranges and
+// Also records each IP peer's nonzero word span in rng[4 * peer] (first word) and
+// rng[4 * peer + 1] (~last word), both atomicMin'd from 0xFFFFFFFF, and the complement of its
+// nonzero-chunk mask in the u64 at rng + 4 * peer + 2 (atomicAnd'd from ~0; chunks < 64 — the
+// wave-per-chunk class rows test an entry against their chunk with it): CIDRs are address ranges and
 // pods of a namespace have neighbouring addresses, so a peer's row is mostly zero words the
 // class rows can skip without loading them.  Rows are stored chunk-dense: cnz[peer][chunk] (one
-// u64 per 64-word chunk, written by the chunk's wave) has the chunk's nonzero words; a chunk with
+// u32 per 64-word chunk, written by the chunk's wave) is 1 if the chunk has a nonzero word; a chunk with
 // none stores no PM word at all, any other chunk stores all 64.  Readers issue the PM and cnz loads
 // together and drop the PM word of an all-zero chunk, so the zero chunks — most of a row — cost
 // no HBM writes.
 __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
                                             const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
                                             uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng,
-                                            uint64_t* __restrict__ cnz) {
+                                            uint32_t* __restrict__ cnz) {
   bool uniform = true;
   uint64_t res = 0;
   if (valid) {
@@ -459,16 +461,17 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
     }
   }
   if (lane == 0) {
-    cnz[uint64_t(t.peer) * ((W + 63) / 64) + chunk] = nz;
+    cnz[uint64_t(t.peer) * ((W + 63) / 64) + chunk] = nz ? 1u : 0u;
     if (lo != 0xFFFFFFFFu) {
-      atomicMin(&rng[2 * t.peer], lo);
-      atomicMin(&rng[2 * t.peer + 1], ~hi);
+      atomicMin(&rng[4 * t.peer], lo);
+      atomicMin(&rng[4 * t.peer + 1], ~hi);
+      if (chunk < 64) atomicAnd(reinterpret_cast<unsigned long long*>(rng) + 2 * t.peer + 1, ~(1ull << chunk));
     }
   }
 }
 
 // ~0 if word w of IP peer j's PM row was stored (its chunk has a nonzero word; see ip_row_word).
-__device__ __forceinline__ uint64_t cnz_mask(const uint64_t* __restrict__ cnz, uint32_t W, uint32_t j, uint32_t w) {
+__device__ __forceinline__ uint64_t cnz_mask(const uint32_t* __restrict__ cnz, uint32_t W, uint32_t j, uint32_t w) {
   return cnz[uint64_t(j) * ((W + 63) / 64) + w / 64] ? ~0ull : 0ull;
 }
 
@@ -480,7 +483,7 @@ constexpr uint32_t IP_GROUP = 8, IP_GROUP_MAX = 64, IP_EX_LDS = 256;
 __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng, uint64_t* __restrict__ cnz, uint32_t bid_, uint32_t nblk_,
+                                                      uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t bid_, uint32_t nblk_,
                                                       uint32_t grp = IP_GROUP) {
   __shared__ DIPTest s_t[IP_GROUP_MAX];
   __shared__ DCidr s_ex[IP_EX_LDS];
@@ -517,7 +520,7 @@ __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32
 __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng, uint64_t* __restrict__ cnz, uint32_t grp) {
+                                                      uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t grp) {
   ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, cnz, blockIdx.x, gridDim.x, grp);
 }
 
@@ -840,8 +843,9 @@ struct RowArgs {
   const uint32_t* ip_off;    // [n_ident] host upper bound: IP peers of the identity's namespace's targets
   uint32_t* ip_cnt;          // [n_ident] IP peers of the class's targets, listed in ip_list as
   uint4* ip_list;            // (peer, port matcher, first, last nonzero PM word)
-  const uint32_t* ip_rng;    // [R][2] first word, ~last word of each IP peer's nonzero PM words (no-panic runs)
-  const uint64_t* ip_cnz;    // [R][W/64] which PM words of an IP peer were written (no-panic runs)
+  const uint32_t* ip_rng;    // [R][4] per IP peer (no-panic runs): first word, ~last word of its nonzero PM
+                             // words, then (u64) ~ the mask of its chunks holding one (chunks < 64)
+  const uint32_t* ip_cnz;    // [R][W/64] 1 if the 64-word chunk of an IP peer's PM row was written
   uint32_t E, EW, NB;
   uint32_t rpb;              // IDO class rows: representatives per block (class_rows_ido_blk)
   // the direction's hash table (keys + reps), emptied for the NEXT run by the first class-row
@@ -962,7 +966,7 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
       for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
         const DPeer pr = a.peers[j];
         if (pr.kind == 0) break;  // AllPeers: the identity sets already allow everything
-        if (pr.kind == 3 && a.ip_rng[2 * j] != 0xFFFFFFFFu) il[m++] = make_uint4(j, pr.port, a.ip_rng[2 * j], ~a.ip_rng[2 * j + 1]);
+        if (pr.kind == 3 && a.ip_rng[4 * j] != 0xFFFFFFFFu) il[m++] = make_uint4(j, pr.port, a.ip_rng[4 * j], ~a.ip_rng[4 * j + 1]);
       }
     }
     a.ip_cnt[i] = m;
@@ -1036,7 +1040,7 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
           break;
         }
         uint64_t pm = ~0ull, er = 0;
-        if (!ERR && pr.kind == 3 && (w < a.ip_rng[2 * j] || w > ~a.ip_rng[2 * j + 1])) continue;  // zero word
+        if (!ERR && pr.kind == 3 && (w < a.ip_rng[4 * j] || w > ~a.ip_rng[4 * j + 1])) continue;  // zero word
         if (pr.kind >= 2) {
           pm = a.PM[uint64_t(j) * a.W + w];
           if (ERR) er = a.ER[uint64_t(j) * a.W + w];
@@ -1107,10 +1111,10 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
 #ifndef CYC_PL_BATCH
 #define CYC_PL_BATCH 8  // list entries whose PM words are loaded at once (16: occupancy 6 -> 4)
 #endif
-#ifndef CYC_PL_SPAN
-#define CYC_PL_SPAN 0  // class rows by spans (pl_span_rows) where the port bit rows allow it
+#ifndef CYC_PL_WAVE
+#define CYC_PL_WAVE 1  // class rows a wave per 64-word chunk (pl_wave_chunks) where it applies
 #endif
-constexpr bool PL_SPAN = CYC_PL_SPAN != 0;
+constexpr bool PL_WAVE = CYC_PL_WAVE != 0;
 #ifndef CYC_PL_THREADS
 #define CYC_PL_THREADS 128  // threads per class-row block (one representative per block)
 #endif
@@ -1258,71 +1262,118 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
     }
 }
 
-// The class rows by SPANS (port bit rows available, list in LDS): entries are walked once per
-// chunk of pod words, each thread ORing the PM words of the entries' nonzero spans that fall on
-// its own words into a per-(descriptor | slot) accumulator row in LDS — work in proportion to the
-// spans, not to words x entries (most entries cover a few words: CIDRs are address ranges) — and
-// the accumulators become the class rows in one pass over the words: egress through each word's
-// slot descriptor (DESCW, or the DM masks of mixed words), ingress slot by slot.
-constexpr uint32_t PL_ACC_BYTES = 16384;  // accumulator rows per block (dynamic LDS)
-template <bool EGRESS>
-__device__ __forceinline__ void pl_span_rows(const RowArgs& a, const PlShared& sh, uint64_t* acc, uint32_t i, uint32_t m,
-                                             bool allow_all, uint64_t lastmask) {
-  const uint32_t NB = EGRESS ? a.D : a.K, bs = blockDim.x;
-  const uint32_t wc = max(64u, PL_ACC_BYTES / 8 / max(NB, 1u));  // words per chunk
-  for (uint32_t w0 = 0; w0 < a.W; w0 += wc) {
-    const uint32_t w1 = min(a.W, w0 + wc), nw = w1 - w0;
-    if (!allow_all) {
-      for (uint32_t x = threadIdx.x; x < NB * nw; x += bs) acc[x] = 0;
-      __syncthreads();
-      for (uint32_t x = 0; x < m; x++) {
-        const uint32_t ex = __builtin_amdgcn_readfirstlane(sh.e[x].x);
-        if (ex == PL_SKIP) continue;
-        const uint32_t ez = __builtin_amdgcn_readfirstlane(sh.e[x].z), ew = __builtin_amdgcn_readfirstlane(sh.e[x].w);
-        const uint32_t lo = max(ez & ~PL_IP, w0), hi = min(ew, w1 - 1);
-        if (lo > hi) continue;  // the entry's span misses this chunk
-        const uint32_t bits = __builtin_amdgcn_readfirstlane(sh.bits[x]);
-        // this thread's words are w0 + threadIdx.x + j * bs
-        uint32_t w = w0 + threadIdx.x;
-        if (w < lo) w += (lo - w + bs - 1) / bs * bs;
-        for (; w <= hi; w += bs) {
-          uint64_t pm = ~0ull;
-          if (ex != PL_ONES) {
-            pm = a.PM[uint64_t(ex) * a.W + w];
-            if (ez & PL_IP) pm &= cnz_mask(a.ip_cnz, a.W, ex, w);
-          }
-          if (!pm) continue;
-          for (uint32_t b = bits; b; b &= b - 1) acc[uint32_t(__ffs(b) - 1) * nw + (w - w0)] |= pm;  // own word: no race
-        }
-      }
-      __syncthreads();
-    }
-    for (uint32_t w = w0 + threadIdx.x; w < w1; w += bs) {
-      const uint64_t wmask = w == a.W - 1 ? lastmask : ~0ull;
-      for (uint32_t k = 0; k < a.K; k++) {
-        uint64_t v = 0;
-        if (EGRESS) {
-          const uint64_t valid = a.VALID[uint64_t(k) * a.W + w];
-          const int32_t du = a.DESCW[uint64_t(k) * a.W + w];
-          if (allow_all) v = valid;
-          else if (du >= 0) v = acc[uint32_t(du) * nw + (w - w0)] & valid;
-          else if (du == -1) {  // destinations with mixed job descriptors (rare)
-            const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
-            for (uint32_t d = 0; d < a.D; d++) v |= acc[d * nw + (w - w0)] & dm[uint64_t(d) * a.W];
-            v &= valid;
-          }
-        } else if (a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) {
-          v = (allow_all ? ~0ull : acc[k * nw + (w - w0)]) & wmask;
-        }
-        a.A[(uint64_t(i) * a.K + k) * a.W + w] = v;
-      }
-    }
-    __syncthreads();  // the accumulators are reused by the next chunk
+// The class rows a WAVE PER 64-WORD CHUNK (port bit rows available, at most PL_NB descriptors /
+// slots, at most 64 chunks): lane = pod word.  The class's entries sit one per lane (row, port
+// bits, mask of the chunks where the entry's PM row has a nonzero word — for IP rows recorded by
+// the IP-row pass, so zero chunks are never read); per chunk one ballot picks the entries that
+// matter there (a CIDR covers a few chunks) and their PM words are loaded PL_WBATCH at a time, all
+// in flight together, then ORed into an accumulator per descriptor (egress) or slot (ingress)
+// bit.  The accumulators become the class rows through each word's slot descriptor (DESCW; the DM
+// masks for mixed words).
+#ifndef CYC_PL_WBATCH
+#define CYC_PL_WBATCH 8
+#endif
+constexpr uint32_t PL_WBATCH = CYC_PL_WBATCH, PL_NB = 4;
+// An entry's lane fields for the wave-per-chunk rows: row, port bits, mask of the 64-word chunks
+// holding a nonzero PM word of it (IP rows: from the IP-row pass; other rows: all)
+struct PlLane {
+  uint32_t row, bits;
+  uint64_t cm;
+};
+__device__ __forceinline__ PlLane pl_lane(const RowArgs& a, const uint4* src, uint32_t x, uint32_t m) {
+  PlLane l{PL_SKIP, 0u, 0ull};
+  if (x < m) {
+    const uint4 e = src[x];  // (row, port bits, first word | PL_IP, last word)
+    l.row = e.x;
+    l.bits = e.y;
+    if (e.x == PL_SKIP || !e.y) l.cm = 0;
+    else if (e.x != PL_ONES && (e.z & PL_IP)) l.cm = ~reinterpret_cast<const uint64_t*>(a.ip_rng)[2 * e.x + 1];
+    else l.cm = ~0ull;
   }
+  return l;
 }
 
 template <bool EGRESS>
-__device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint64_t* acc, uint32_t bid_, uint32_t nblk_) {
+__device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared& sh, const uint4* spill, uint32_t i,
+                                               uint32_t m, bool allow_all, uint64_t lastmask) {
+  static_assert(PL_LDS % 64 == 0, "a lane group of entries is all in LDS or all spilled");
+  const uint32_t lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+  const uint32_t chunks = (a.W + 63) / 64;  // <= 64 (pl_wave_ok)
+  const PlLane g0 = pl_lane(a, sh.e, lane, m);  // entries 0..63, one per lane, for every chunk
+  for (uint32_t c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < chunks; c += nwaves) {
+    const uint32_t w = c * 64 + lane;
+    const bool live = w < a.W;
+    const uint32_t wl = live ? w : a.W - 1;  // dead lanes load a valid word and store nothing
+    uint64_t valid[PL_NB];
+    int32_t du[PL_NB];
+#pragma unroll
+    for (uint32_t k = 0; k < PL_NB; k++) {  // slot words, loaded with the first batch
+      valid[k] = 0;
+      du[k] = -2;
+      if (k < a.K) {
+        if (EGRESS) {
+          valid[k] = a.VALID[uint64_t(k) * a.W + wl];
+          du[k] = a.DESCW[uint64_t(k) * a.W + wl];
+        } else if (a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) {
+          valid[k] = w == a.W - 1 ? lastmask : ~0ull;
+        }
+      }
+    }
+    uint64_t acc[PL_NB];
+#pragma unroll
+    for (uint32_t d = 0; d < PL_NB; d++) acc[d] = allow_all ? ~0ull : 0ull;
+    for (uint32_t x0 = 0; x0 < (allow_all ? 0u : m); x0 += 64) {
+      PlLane g = g0;  // (uniform branches: an LDS or a global load, never a flat one)
+      if (x0 >= PL_LDS) g = pl_lane(a, spill, x0 + lane, m);
+      else if (x0) g = pl_lane(a, sh.e, x0 + lane, m);
+      // the entries with a nonzero PM word in this chunk; their words are loaded PL_WBATCH at a time
+      uint64_t todo = __ballot((g.cm >> c) & 1ull);
+      while (todo) {
+        uint32_t bits[PL_WBATCH];
+        uint64_t v[PL_WBATCH];
+#pragma unroll
+        for (uint32_t u = 0; u < PL_WBATCH; u++) {
+          bits[u] = 0;
+          v[u] = 0;
+          if (todo) {
+            const uint32_t src = __ffsll((unsigned long long)todo) - 1;
+            todo &= todo - 1;
+            const uint32_t row = __builtin_amdgcn_readlane(g.row, src);
+            bits[u] = __builtin_amdgcn_readlane(g.bits, src);
+            v[u] = row == PL_ONES ? ~0ull : a.PM[uint64_t(row) * a.W + wl];
+          }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PL_WBATCH; u++)
+#pragma unroll
+          for (uint32_t d = 0; d < PL_NB; d++)
+            if ((bits[u] >> d) & 1u) acc[d] |= v[u];
+      }
+    }
+    if (!live) continue;
+#pragma unroll
+    for (uint32_t k = 0; k < PL_NB; k++) {
+      if (k >= a.K) break;
+      uint64_t r = 0;
+      if (!EGRESS) r = acc[k] & valid[k];
+      else if (du[k] >= 0) {
+#pragma unroll
+        for (uint32_t d = 0; d < PL_NB; d++) r = uint32_t(du[k]) == d ? acc[d] : r;
+        r &= valid[k];
+      } else if (du[k] == -1) {  // destinations with mixed job descriptors (rare)
+        const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
+#pragma unroll
+        for (uint32_t d = 0; d < PL_NB; d++)
+          if (d < a.D) r |= acc[d] & dm[uint64_t(d) * a.W];
+        r &= valid[k];
+      }
+      a.A[(uint64_t(i) * a.K + k) * a.W + w] = r;
+    }
+  }
+}
+
+template <bool EGRESS, bool WAVE>
+__device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
   ht_clear_slice(a, bid_, nblk_);
   const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC, items = nkc * a.W;
@@ -1373,9 +1424,9 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
         } else {
           en = make_uint4(pr.kind == 1 ? PL_ONES : j, pr.port, 0u, a.W - 1);
           if (pr.kind == 3) {  // bit 31 of z: an IP row (only the cnz-marked words were written)
-            en.z = a.ip_rng[2 * j] | PL_IP;
-            en.w = ~a.ip_rng[2 * j + 1];
-            if (a.ip_rng[2 * j] == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
+            en.z = a.ip_rng[4 * j] | PL_IP;
+            en.w = ~a.ip_rng[4 * j + 1];
+            if (a.ip_rng[4 * j] == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
           }
           if (EGRESS) {
             if (a.portbits) bits = a.portbits[pr.port];
@@ -1388,7 +1439,8 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
               if (a.portbits ? ((pb >> du) & 1u) : a.portok[uint64_t(pr.port) * a.D + du]) bits |= 1u << k;
             }
           }
-          en.y = EGRESS || a.K > 32 ? pr.port : bits;  // spilled entries carry the bits themselves
+          // spilled entries (and every entry of the wave-per-chunk rows) carry the bits themselves
+          en.y = WAVE || (!EGRESS && a.K <= 32) ? bits : pr.port;
           if (kbits && !bits) en.x = PL_SKIP;  // the port matcher passes no slot / descriptor here
         }
         const uint32_t x = m + e;
@@ -1402,7 +1454,7 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
       m += mc;
       __syncthreads();
     }
-    if (threadIdx.x == 0 && m <= 64) {  // group entries by port bits: each group's slot test runs once
+    if (!WAVE && threadIdx.x == 0 && m <= 64) {  // group entries by port bits: each group's slot test runs once
       for (uint32_t x = 1; x < m; x++) {
         const uint4 e = sh.e[x];
         const uint32_t b = sh.bits[x];
@@ -1422,9 +1474,8 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
 #ifdef CYC_DIAG_NO_ITEMS
     if (m < 100000) continue;
 #endif
-    const uint32_t NB = EGRESS ? a.D : a.K;
-    if (acc && kbits && m <= PL_LDS && NB <= 32) {
-      pl_span_rows<EGRESS>(a, sh, acc, i, m, allow_all, lastmask);
+    if (WAVE) {
+      pl_wave_chunks<EGRESS>(a, sh, spill, i, m, allow_all, lastmask);
     } else {
       for (uint32_t it0 = threadIdx.x; it0 < items; it0 += PL_ITEMS * blockDim.x)
         pl_items<EGRESS>(a, sh, spill, i, m, allow_all, kbits, it0, items, lastmask);
@@ -1432,11 +1483,10 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     __syncthreads();  // LDS reused by the next representative
   }
 }
-template <bool EGRESS>
+template <bool EGRESS, bool WAVE>
 __global__ __launch_bounds__(256) void k_class_rows_pl(RowArgs a) {
   __shared__ PlShared sh;
-  extern __shared__ uint64_t pl_acc[];
-  class_rows_pl_blk<EGRESS>(a, sh, PL_SPAN ? pl_acc : nullptr, blockIdx.x, gridDim.x);
+  class_rows_pl_blk<EGRESS, WAVE>(a, sh, blockIdx.x, gridDim.x);
 }
 
 // Class rows from identity sets (IDO builds).  Block = (class representative, KC job slots,
@@ -1612,7 +1662,7 @@ struct FrontB {
   const DWordIP* words;
   uint64_t* PM;
   uint32_t* rng;
-  uint64_t* cnz;
+  uint32_t* cnz;
   uint32_t Ru, E, EW, L;
   const uint32_t* pod_peers_u;
   const DPeer* peers;
@@ -1666,13 +1716,12 @@ __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   else class_ident_blk<true, 4>(f.ra[1], b - f.nb[0], f.nb[1]);
 }
 // PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
+template <bool WAVE>
 __global__ __launch_bounds__(256) CYC_PL_WAVES void k_front_d_pm(FrontRows f) {
   __shared__ PlShared sh;
-  extern __shared__ uint64_t pl_acc[];
   const uint32_t b = blockIdx.x;
-  uint64_t* acc = PL_SPAN ? pl_acc : nullptr;
-  if (b < f.nb[1]) class_rows_pl_blk<true>(f.ra[1], sh, acc, b, f.nb[1]);
-  else class_rows_pl_blk<false>(f.ra[0], sh, acc, b - f.nb[1], f.nb[0]);
+  if (b < f.nb[1]) class_rows_pl_blk<true, WAVE>(f.ra[1], sh, b, f.nb[1]);
+  else class_rows_pl_blk<false, WAVE>(f.ra[0], sh, b - f.nb[1], f.nb[0]);
 }
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
@@ -2131,6 +2180,8 @@ struct cyc_ctx {
   int64_t class_rpb_opt = 4;  // "class_rpb": IDO class-row representatives per block
                               // (config3 N=1 -1%: profiles/r01_class_rpb_ab.txt)
   uint32_t ip_group = IP_GROUP;  // "ip_group": IP-peer tests per block in the IP rows
+  int pl_wave = 1;      // "pl_wave": PM-build class rows a wave per 64-word chunk where they fit (1),
+                        // or a thread per (slot chunk, word) item (0)
   int front_fused = 1;  // "front_fused": the front as block-range-fused launches on one stream
                         // (enq_front_fused), 0 = the two-branch DAG
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
@@ -2333,7 +2384,7 @@ static void prepare_device(cyc_ctx* c) {
     }
   }
   c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
-  c->ip_rng.alloc(std::max<uint64_t>(R * 8 + R * ((W + 63) / 64) * 8, 16));  // [R][2] word spans, then [R][W/64] cnz
+  c->ip_rng.alloc(std::max<uint64_t>(R * 16 + R * ((W + 63) / 64) * 4, 16));  // [R][4] word spans + chunk masks, then [R][W/64] cnz
   c->ER.alloc(pb.may_err ? std::max<uint64_t>(R * W * 8, 16) : 16);
   {
     c->plan = plan_peers(pb, c->ids[1]);
@@ -2435,8 +2486,8 @@ static void prepare_device(cyc_ctx* c) {
   c->order_lo = c->order_hi = -1;
 }
 
-// nonzero-word masks of the IP peers' PM rows, after the word spans in the ip_rng buffer
-static uint64_t* ip_cnz(cyc_ctx* c) { return reinterpret_cast<uint64_t*>(c->ip_rng.as<uint32_t>() + 2 * c->pb.peers.size()); }
+// nonzero-chunk flags of the IP peers' PM rows, after the word spans and chunk masks in the ip_rng buffer
+static uint32_t* ip_cnz(cyc_ctx* c) { return c->ip_rng.as<uint32_t>() + 4 * c->pb.peers.size(); }
 
 static unsigned grid1(uint64_t n, unsigned block) { return unsigned(std::min<uint64_t>((n + block - 1) / block, 1u << 20)); }
 
@@ -2598,7 +2649,7 @@ static void enq_common(cyc_ctx* c, hipStream_t st, int parts = COMMON_ALL) {
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size());
   if ((parts & COMMON_FILL) && !pb.may_err && c->Ri)  // IP-peer word spans (k_ip_rows_fast)
-    k_fill_u32<<<grid1(c->pb.peers.size() * 2, 256), 256, 0, st>>>(c->ip_rng.as<uint32_t>(), c->pb.peers.size() * 2, 0xFFFFFFFFu);
+    k_fill_u32<<<grid1(c->pb.peers.size() * 4, 256), 256, 0, st>>>(c->ip_rng.as<uint32_t>(), c->pb.peers.size() * 4, 0xFFFFFFFFu);
   if (!(parts & COMMON_SELECTORS)) goto ports;
   // 1. selectors x label sets
   if (uint64_t(c->n_sel) * pb.L && c->dense_sel)
@@ -2777,6 +2828,14 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   return ra;
 }
 
+// PM-build class rows a wave per 64-word chunk (pl_wave_chunks): both directions' accumulators fit
+// (descriptors and slots <= PL_NB) and every peer's port bits are available.
+static bool pl_wave_ok(const cyc_ctx* c) {
+  const Problem& pb = c->pb;
+  return PL_WAVE && c->pl_wave && pb.K <= PL_NB && pb.descs.size() <= PL_NB && pb.descs.size() && pb.pms.size() &&
+         port_bits_on(c) && pb.W <= 64 * 64;
+}
+
 static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   Problem& pb = c->pb;
   const uint32_t K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
@@ -2800,8 +2859,11 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
     else k_class_rows_ido<true, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
   } else {  // per-class flattened peer lists (the IP word spans are final here)
-    if (d == 0) k_class_rows_pl<false><<<pl_blocks(c, d), PL_THREADS, PL_SPAN ? PL_ACC_BYTES : 0, st>>>(ra);
-    else k_class_rows_pl<true><<<pl_blocks(c, d), PL_THREADS, PL_SPAN ? PL_ACC_BYTES : 0, st>>>(ra);
+    const bool wave = pl_wave_ok(c);
+    if (d == 0 && wave) k_class_rows_pl<false, true><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
+    else if (d == 0) k_class_rows_pl<false, false><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
+    else if (wave) k_class_rows_pl<true, true><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
+    else k_class_rows_pl<true, false><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
   }
 }
 
@@ -2890,7 +2952,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   // A: IP word spans | port table | slot words | selectors
   FrontA fa{};
   fa.fill_p = c->ip_rng.as<uint32_t>();
-  fa.fill_n = c->Ri ? pb.peers.size() * 2 : 0;  // the word spans (cnz needs no reset)
+  fa.fill_n = c->Ri ? pb.peers.size() * 4 : 0;  // the word spans and chunk masks (cnz needs no reset)
   fa.nb[0] = blocks((fa.fill_n + 255) / 256);
   fa.M = M;
   fa.D = D;
@@ -2993,7 +3055,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (fc.nb[0] + fc.nb[1]) k_front_c<<<fc.nb[0] + fc.nb[1], 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
-    if (fd.nb[0] + fd.nb[1]) k_front_d_pm<<<fd.nb[0] + fd.nb[1], PL_THREADS, PL_SPAN ? PL_ACC_BYTES : 0, st>>>(fd);
+    if (fd.nb[0] + fd.nb[1] && pl_wave_ok(c)) k_front_d_pm<true><<<fd.nb[0] + fd.nb[1], PL_THREADS, 0, st>>>(fd);
+    else if (fd.nb[0] + fd.nb[1]) k_front_d_pm<false><<<fd.nb[0] + fd.nb[1], PL_THREADS, 0, st>>>(fd);
     if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
     return true;
   }
@@ -3633,6 +3696,7 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "member_wave") range(-1, 1), c->member_wave = int(value);
     else if (n == "class_rpb") range(1, 64), c->class_rpb_opt = value;
     else if (n == "ip_group") range(1, 64), c->ip_group = uint32_t(value);
+    else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
     else return fail(c, CYC_ERR_ARG, "unknown option " + n);
     drop_graph(c);
     return (int)CYC_OK;
@@ -3648,7 +3712,11 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "member_wave") *value = c->member_wave;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "ip_group") *value = c->ip_group;
-  else if (n == "launch") *value = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);  // in effect
+  else if (n == "pl_wave") *value = c->pl_wave;
+  else if (n == "pl_wave_active") {
+    if (!c->prepared) return fail(c, CYC_ERR_ARG, "pl_wave_active: call cyc_probe_prepare first");
+    *value = !ido_mode(c) && pl_wave_ok(c) ? 1 : 0;
+  } else if (n == "launch") *value = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);  // in effect
   else if (n == "front_fused_active") *value = front_fused_ok(c) ? 1 : 0;
   else if (n == "pod_words") {
     if (!c->prepared) return fail(c, CYC_ERR_ARG, "pod_words: call cyc_probe_prepare first");

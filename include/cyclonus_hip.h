@@ -177,8 +177,11 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  *                 thread (0) or a wave (1) per pod identity
  *   "class_rpb"   4 (default, 1..64): class representatives per identity-set class-row block
  *   "ip_group"    8 (default, 1..64): IP peers per IP-row block
- * cyc_get_option also reports "launch" (the graphs mode in effect) and "front_fused_active" (both
- * need cyc_probe_prepare); "pod_words" reports the mode the prepared probe uses (0 or 1). */
+ *   "pl_wave"     1 (default) / 0: materialised-row class rows a wave per 64-word chunk where they
+ *                 fit (<= 4 job slots and descriptors), or a thread per (slot chunk, word) item
+ * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
+ * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
+ * uses (0 or 1). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
 int cyc_get_option(cyc_ctx* ctx, const char* name, int64_t* value);
 

@@ -308,6 +308,32 @@ def test_ip_interval_words(gpu, seed):
     assert_same(o, g, f"ip intervals seed {seed}")
 
 
+def test_pm_class_rows_wave_and_items(gpu):
+    """PM-build class rows (pod_words = 0) a wave per 64-word chunk (pl_wave = 1: <= 4 slots and
+    descriptors) and a thread per item (pl_wave = 0) against the oracle: IP-interval problems (IP
+    rows with skipped and straddling chunks) and random problems, which include classes with more
+    list entries than the LDS part holds only at sizes the oracle cannot check — those run through
+    tests/test_gpu_fullrows.py."""
+    eng = Engine(0)
+    seen_wave = 0
+    problems = [_ip_interval_problem(s, n_pods=300 + 97 * s) for s in range(3)]
+    problems += [random_problem(95_000 + s, n_pods=120) for s in range(40)]
+    for n, (pols, res, probes) in enumerate(problems):
+        want = Oracle(pols, res).probe(probes)
+        try:
+            eng.build_policies(pols).load_resources(res)
+            eng.prepare(probes)
+        except CyclonusPanic:
+            continue
+        eng.set_option("pod_words", 0)
+        for wave in (1, 0):
+            eng.set_option("pl_wave", wave)
+            assert_same(want, eng.run_host(), f"problem {n} pl_wave={wave}")
+        eng.set_option("pl_wave", 1)
+        seen_wave += eng.get_option("pl_wave_active")
+    assert seen_wave >= 10
+
+
 def _deployment_problem(seed, min_run=22):
     """Random policies over deployment-style pods: each random pod template is replicated into a
     contiguous run of >= min_run pods (same namespace, labels and containers; own name and IP),
