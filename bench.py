@@ -13,6 +13,7 @@ there is no collective on the data path).  Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -261,11 +262,17 @@ def main():
 
     # HBM traffic of k_emit from the committed PMC passes for this same workload (rocprofv3
     # --pmc FETCH_SIZE / WRITE_SIZE, corrected per MI355X_MICROARCH.md; scripts/pmc_summary.py)
-    traffic, traffic_src = None, None
-    pmc_path = os.path.join(ROOT, "profiles", f"r01_pmc_{args.config}.json")
-    if os.path.exists(pmc_path) and world == 1:
-        pmc = json.load(open(pmc_path))
-        traffic, traffic_src = pmc.get("emit_hbm_bytes_per_launch"), os.path.relpath(pmc_path, ROOT)
+    # (the newest round's file); MFMA use from the same file's --pmc SQ_*MFMA* pass
+    traffic, traffic_src, mfma = None, None, None
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc_{args.config}.json")))
+    if pmcs and world == 1:
+        pmc = json.load(open(pmcs[-1]))
+        traffic, traffic_src = pmc.get("emit_hbm_bytes_per_launch"), os.path.relpath(pmcs[-1], ROOT)
+        if pmc.get("mfma"):
+            m = pmc["mfma"]
+            mfma = {"insts_per_step": m["mfma_insts_per_step"], "busy_cycles_per_step": m["mfma_busy_cycles_per_step"],
+                    "util": m["util"], "source": traffic_src,
+                    "note": "no GEMM-shaped step on this path (DESIGN.md section 4): measured, not assumed"}
 
     if rank == 0:
         line = {
@@ -310,6 +317,7 @@ def main():
                 "emit_ms_per_launch": emit_launch_ms,
                 "launches_per_step": launches,
                 "fill_ceiling_GBs": fill_gbs,
+                "mfma": mfma,
             },
             "launch": launch_desc,
             "pipeline_ms": {"total": pipe_ms, "emit": emit_ms, "class_rows": rows_ms, "front": pipe_ms - emit_ms - rows_ms},

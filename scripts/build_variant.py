@@ -1,5 +1,6 @@
 """Build an A/B variant of libcyclonus_hip.so with extra -D flags (dev helper):
     python scripts/build_variant.py NAME -DCYC_PL_BATCH=16   -> cyclonus_amd/_build/var_NAME/libcyclonus_hip.so
+    python scripts/build_variant.py NAME --rev HEAD           -> the engine.hip of a git revision
 Run it with CYC_HIP_LIB=<that path> (cyclonus_amd/_lib.py)."""
 import os
 import subprocess
@@ -12,9 +13,17 @@ from cyclonus_amd import build as b  # noqa: E402
 name, defs = sys.argv[1], sys.argv[2:]
 out = os.path.join(b.BUILD, f"var_{name}")
 os.makedirs(out, exist_ok=True)
+src = os.path.join(b.CSRC, "engine.hip")
+if "--rev" in defs:
+    rev = defs[defs.index("--rev") + 1]
+    defs = [d for d in defs if d not in ("--rev", rev)]
+    src = os.path.join(out, "engine_rev.hip")
+    with open(src, "w") as f:
+        f.write(subprocess.run(["git", "-C", ROOT, "show", f"{rev}:cyclonus_amd/csrc/engine.hip"], check=True,
+                               capture_output=True, text=True).stdout)
 common = ["-O3", "-std=c++17", "-fPIC", "-I", b.CSRC, "-I", b.INCLUDE, *defs]
 host = os.path.join(b.BUILD, "host.cpp.o")
 eng = os.path.join(out, "engine.hip.o")
-subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", *common, "-munsafe-fp-atomics", "-c", os.path.join(b.CSRC, "engine.hip"), "-o", eng], check=True)
+subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", *common, "-munsafe-fp-atomics", "-c", src, "-o", eng], check=True)
 subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "libcyclonus_hip.so"), host, eng], check=True)
 print(os.path.join(out, "libcyclonus_hip.so"))

@@ -7,8 +7,8 @@ timeout -s KILL 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 C=$(python3 - $OUT/counters_list.txt <<'EOF'
 import re, sys
 txt = open(sys.argv[1], errors="replace").read()
-want = ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_I8", "SQ_INSTS_VALU_MFMA_F8", "SQ_INSTS_VALU_MFMA_F16",
-        "SQ_INSTS_VALU_MFMA_BF16", "SQ_INSTS_VALU_MFMA_F32", "SQ_INSTS_VALU_MFMA_F64"]
+want = ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_INSTS_VALU_MFMA_I8", "SQ_INSTS_VALU_MFMA_F8",
+        "SQ_INSTS_VALU_MFMA_F16", "SQ_INSTS_VALU_MFMA_BF16", "SQ_INSTS_VALU_MFMA_F32", "SQ_INSTS_VALU_MFMA_F64"]
 have = [w for w in want if re.search(r"\b" + w + r"\b", txt)][:6]
 print(" ".join(have + ["SQ_BUSY_CYCLES", "SQ_INSTS_VALU"]))
 EOF
