@@ -1855,118 +1855,6 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   }
 }
 
-// The IDO EMIT (no-panic identity-set builds, fused front): the class rows are never stored.  A
-// block takes a run of rows of one plane whose pods share an identity (so one class row), stages
-// the class's identity-set rows, computes the class row a 16-byte piece per thread at a time
-// (expand the word's identity runs; OR the class's IP peers' PM words) and writes each piece to
-// every row of the run.  This drops k_front_e's class-row stores and the emit's class-row loads
-// (config #3: 2 x 200 MB each) and hides the class-row latency under the plane stores.
-constexpr uint32_t EI_RUN_MAX = 64, EI_B_WORDS = 4096, EI_KMAX = 32, EI_CU = 2;
-struct EmitIdo {
-  EmitArgs e;
-  RowArgs ra[2];
-  const uint2* runs;  // (plane << 31 | first position in the plane's row order, rows)
-};
-
-// Word (slot k, pod word w) of class representative i's row (class_rows_ido_blk, one word).
-template <bool EGRESS>
-__device__ __forceinline__ uint64_t ido_word(const RowArgs& a, const uint64_t* sB, const uint8_t* s_st,
-                                             const int32_t* s_desc, uint32_t k, uint32_t w, uint32_t m,
-                                             const uint4* __restrict__ il) {
-  const WordRuns wr = a.runs[w];
-  uint64_t valid;
-  int32_t du;
-  if (EGRESS) {
-    valid = a.VALID[uint64_t(k) * a.W + w];
-    du = a.DESCW[uint64_t(k) * a.W + w];
-  } else {
-    const bool v = s_st[k] == CYC_JOB_VALID;
-    const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
-    valid = v ? (w == a.W - 1 ? lastmask : ~0ull) : 0ull;
-    du = v ? s_desc[k] : -2;
-  }
-  uint64_t allow = 0;
-  if (du >= 0) {
-    allow = expand_runs(sB + uint64_t(EGRESS ? uint32_t(du) : k) * a.EW, wr);
-  } else if (EGRESS && du == -1) {  // destinations with mixed job descriptors (rare)
-    const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
-    for (uint32_t d = 0; d < a.D; d++) allow |= expand_runs(sB + uint64_t(d) * a.EW, wr) & dm[uint64_t(d) * a.W];
-  }
-  // IP peers (ippeermatcher.go:43-50): order-free OR (no panic); stops once every valid bit allows
-  for (uint32_t x = 0; x < m && (valid & ~allow); x++) {
-    const uint4 jp = il[x];
-    if (w < jp.z || w > jp.w) continue;  // outside the peer's nonzero words
-    const uint64_t pm = a.PM[uint64_t(jp.x) * a.W + w] & cnz_mask(a.ip_cnz, a.W, jp.x, w);
-    if (!pm) continue;
-    if (EGRESS && a.portbits && du >= 0) allow |= ((a.portbits[jp.y] >> du) & 1u) ? pm : 0ull;
-    else allow |= pm & port_mask<EGRESS>(a, a.portok + uint64_t(jp.y) * a.D, du, k, w);
-  }
-  return allow & valid;
-}
-
-template <bool EGRESS, int WPP>
-__device__ __forceinline__ void emit_ido_run(const EmitIdo& a, const RowArgs& ra, uint32_t pl, uint32_t s0, uint32_t n,
-                                             uint64_t* sB, uint64_t** s_dst, uint8_t* s_st, int32_t* s_desc) {
-  const uint32_t* order = a.e.order[pl];
-  const uint32_t i = a.e.class_of[pl][a.e.pod_id[pl][order[s0]]];  // the run's class representative
-  const uint32_t rowsz = ra.NB * ra.EW;
-  const uint64_t* src = ra.B + uint64_t(i) * rowsz;
-  for (uint32_t x = threadIdx.x; x < rowsz; x += blockDim.x) sB[x] = src[x];
-  if (threadIdx.x < n) s_dst[threadIdx.x] = a.e.out[pl] + uint64_t(order[s0 + threadIdx.x] - a.e.row_lo) * a.e.row_words;
-  if (!EGRESS && threadIdx.x < ra.K) {
-    s_st[threadIdx.x] = ra.id_status[uint64_t(i) * ra.K + threadIdx.x];
-    s_desc[threadIdx.x] = ra.id_desc[uint64_t(i) * ra.K + threadIdx.x];
-  }
-  __syncthreads();
-  const uint32_t m = ra.cnt[i] ? ra.ip_cnt[i] : 0u;
-  const uint4* il = ra.ip_list + ra.ip_off[i];
-  const uint32_t np = uint32_t(a.e.row_words / WPP);  // pieces per row
-  for (uint32_t j0 = threadIdx.x; j0 < np; j0 += blockDim.x * EI_CU) {
-    uint64_t v[EI_CU][WPP];
-#pragma unroll
-    for (uint32_t u = 0; u < EI_CU; u++) {
-      const uint32_t j = j0 + u * blockDim.x;
-#pragma unroll
-      for (uint32_t h = 0; h < WPP; h++) {
-        v[u][h] = 0;
-        if (j < np) {
-          const uint32_t q = j * WPP + h, k = q / ra.W;
-          v[u][h] = ido_word<EGRESS>(ra, sB, s_st, s_desc, k, q - k * ra.W, m, il);
-        }
-      }
-    }
-    for (uint32_t r = 0; r < n; r++) {
-      uint64_t* dst = s_dst[r];
-#pragma unroll
-      for (uint32_t u = 0; u < EI_CU; u++) {
-        const uint32_t j = j0 + u * blockDim.x;
-        if (j >= np) continue;
-        if (WPP == 2) {
-          u64x2 x;
-          x.x = v[u][0];
-          x.y = v[u][WPP - 1];
-          __builtin_nontemporal_store(x, reinterpret_cast<u64x2*>(dst) + j);
-        } else {
-          __builtin_nontemporal_store(v[u][0], dst + j);
-        }
-      }
-    }
-  }
-}
-
-template <int WPP>
-__global__ __launch_bounds__(256) void k_emit_ido(EmitIdo a) {
-  emit_status(a.e);
-  extern __shared__ uint64_t sB[];  // the class's identity-set rows (NB x EW words, host-sized)
-  __shared__ uint64_t* s_dst[EI_RUN_MAX];
-  __shared__ uint8_t s_st[EI_KMAX];
-  __shared__ int32_t s_desc[EI_KMAX];
-  const uint2 run = a.runs[blockIdx.x];
-  const uint32_t pl = run.x >> 31, s0 = run.x & 0x7FFFFFFFu;
-  if (pl) emit_ido_run<true, WPP>(a, a.ra[1], 1, s0, run.y, sB, s_dst, s_st, s_desc);
-  else emit_ido_run<false, WPP>(a, a.ra[0], 0, s0, run.y, sB, s_dst, s_st, s_desc);
-}
-
 // ---------------------------------------------------------------- panic path (rare)
 struct ErrArgs {
   uint32_t P, K, W, n_cfg;
@@ -2294,11 +2182,6 @@ struct cyc_ctx {
   uint32_t ip_group = IP_GROUP;  // "ip_group": IP-peer tests per block in the IP rows
   int pl_wave = 1;      // "pl_wave": PM-build class rows a wave per 64-word chunk where they fit (1),
                         // or a thread per (slot chunk, word) item (0)
-  int emit_ido = 0;     // "emit_ido": IDO builds compute the class rows inside the emit (k_emit_ido):
-                        // 1, or 0 = class rows (k_front_e) then the copy emit, -1 = auto (rows >= 16 KB)
-  uint32_t emit_run = 16;  // "emit_run": rows per k_emit_ido block (runs of one identity are split)
-  DevBuf emit_runs;        // k_emit_ido blocks for the range plan's rows (ensure_range)
-  uint32_t n_emit_runs = 0;
   int front_fused = 1;  // "front_fused": the front as block-range-fused launches on one stream
                         // (enq_front_fused), 0 = the two-branch DAG
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
@@ -2650,7 +2533,6 @@ static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c
 static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   if (c->order_lo == lo && c->order_hi == hi) return;
   Problem& pb = c->pb;
-  std::vector<uint2> runs[2];
   for (int d = 0; d < 2; d++) {  // emit row order: clustered by this direction's identity
     std::vector<uint32_t> ord(size_t(hi - lo));
     std::iota(ord.begin(), ord.end(), uint32_t(lo));
@@ -2659,21 +2541,6 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
     std::stable_sort(ord.begin(), ord.end(),
                      [&](uint32_t x, uint32_t y) { return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y]; });
     upload(c->order[d], ord);
-    runs[d].clear();  // k_emit_ido blocks: rows of one identity, at most emit_run per block
-    for (size_t x = 0; x < ord.size();) {
-      size_t y = x + 1;
-      while (y < ord.size() && y - x < c->emit_run && i1[ord[y]] == i1[ord[x]]) y++;
-      runs[d].push_back(make_uint2(uint32_t(x) | (uint32_t(d) << 31), uint32_t(y - x)));
-      x = y;
-    }
-  }
-  {  // the planes' runs alternate, so both planes are written throughout the emit
-    std::vector<uint2> all;
-    for (size_t x = 0; x < std::max(runs[0].size(), runs[1].size()); x++)
-      for (int d = 0; d < 2; d++)
-        if (x < runs[d].size()) all.push_back(runs[d][x]);
-    c->n_emit_runs = uint32_t(all.size());
-    upload(c->emit_runs, all);
   }
   std::vector<uint8_t> peer_needed(pb.peers.size(), 0), peer_dir(pb.peers.size(), 0);
   for (const DTarget& t : pb.tgt[1])
@@ -3003,21 +2870,8 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // 7. the emit: both planes (ingress rows to out_in, egress rows to out_eg) in one launch.
 // d_status (may be null): the status plane, copied by the emit's blocks.  Returns false if no
 // emit was launched (no rows in the range; the caller then copies the status plane itself).
-// k_emit_ido applies: IDO build run through the fused front, identity-set rows and slots fit the
-// kernel's LDS, rows of >= 16 KB (auto; shorter rows: the class rows then k_emit_flat).
-static bool front_fused_ok(const cyc_ctx* c);
-static bool emit_ido_on(const cyc_ctx* c) {
-  const Problem& pb = c->pb;
-  if (!c->emit_ido || !front_fused_ok(c) || !ido_mode(c) || pb.K > EI_KMAX) return false;
-  for (int d = 0; d < 2; d++) {
-    const uint64_t nb = d == 0 ? pb.K : std::max<size_t>(pb.descs.size(), 1);
-    if (nb * ((c->dir[1].n + 63) / 64) > EI_B_WORDS) return false;
-  }
-  return c->emit_ido == 1 || uint64_t(pb.K) * pb.W * 8 >= 16384;
-}
-
 static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, int64_t lo, int64_t hi,
-                     uint8_t* d_status, bool fused_front) {
+                     uint8_t* d_status) {
   Problem& pb = c->pb;
   const uint32_t K = pb.K, W = pb.W;
   if (hi <= lo || !K || !W) return false;
@@ -3042,16 +2896,6 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.row_words = uint64_t(K) * W;
   ea.per_xcd = (ea.n_rows * 2 + 7) / 8;
   const bool aligned = reinterpret_cast<uintptr_t>(out_in) % 16 == 0 && reinterpret_cast<uintptr_t>(out_eg) % 16 == 0;
-  if (fused_front && emit_ido_on(c) && c->n_emit_runs) {
-    EmitIdo ei{};
-    ei.e = ea;
-    for (int d = 0; d < 2; d++) ei.ra[d] = row_args(c, d);
-    ei.runs = c->emit_runs.as<uint2>();
-    const size_t lds = size_t(std::max(ei.ra[0].NB, ei.ra[1].NB)) * ei.ra[0].EW * 8;
-    if (ea.row_words % 2 == 0 && aligned) k_emit_ido<2><<<c->n_emit_runs, 256, lds, st>>>(ei);
-    else k_emit_ido<1><<<c->n_emit_runs, 256, lds, st>>>(ei);
-    return true;
-  }
   const unsigned g = ea.per_xcd * 8;  // one block per row slot of the 8 XCD segments
   if (ea.row_words % 2 || !aligned) {
     k_emit_words<<<g, 256, 0, st>>>(ea);
@@ -3217,7 +3061,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     return true;
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
-  if (fe.nb[0] + fe.nb[1] && !emit_ido_on(c)) {  // (k_emit_ido computes the class rows itself)
+  if (fe.nb[0] + fe.nb[1]) {
     k_front_e<<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
   }
   if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
@@ -3230,8 +3074,7 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
                              int64_t hi) {
   Problem& pb = c->pb;
   HIPCHK(hipEventRecord(c->ev[0], st));
-  const bool fused = front_fused_ok(c) && enq_front_fused(c, st, c->ev[1], c->ev[2]);
-  if (!fused) {
+  if (!(front_fused_ok(c) && enq_front_fused(c, st, c->ev[1], c->ev[2]))) {
     enq_common(c, st);
     for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st);
     for (int d = 0; d < 2; d++) enq_member(c, d, st);
@@ -3239,7 +3082,7 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
     for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
     HIPCHK(hipEventRecord(c->ev[2], st));
   }
-  const bool status_done = enq_emit(c, st, d_in, d_eg, lo, hi, d_status, fused);
+  const bool status_done = enq_emit(c, st, d_in, d_eg, lo, hi, d_status);
   HIPCHK(hipEventRecord(c->ev[3], st));
   if (!status_done && d_status && uint64_t(pb.P) * pb.K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
@@ -3253,7 +3096,7 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
                              uint8_t* d_status, int64_t lo, int64_t hi) {
   Problem& pb = c->pb;
   if (front_fused_ok(c) && enq_front_fused(c, st)) {
-    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status, true)) return;
+    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status)) return;
   } else {
     HIPCHK(hipEventRecord(c->fork_ev, st));
     HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
@@ -3273,7 +3116,7 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
     HIPCHK(hipEventRecord(c->join_ev, st2));
     HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
     // the emit also writes the status plane; the copy node below only ends steps without rows
-    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status, false)) return;
+    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status)) return;
   }
   // The step always ends with the status-plane copy (into a sink buffer when the caller passed no
   // status pointer), so every captured graph has the same shape: one node after the join.
@@ -3854,12 +3697,6 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "class_rpb") range(1, 64), c->class_rpb_opt = value;
     else if (n == "ip_group") range(1, 64), c->ip_group = uint32_t(value);
     else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
-    else if (n == "emit_ido") range(-1, 1), c->emit_ido = int(value);
-    else if (n == "emit_run") {
-      range(1, EI_RUN_MAX);
-      c->emit_run = uint32_t(value);
-      c->order_lo = c->order_hi = -1;  // the range plan's emit runs are re-made
-    }
     else return fail(c, CYC_ERR_ARG, "unknown option " + n);
     drop_graph(c);
     return (int)CYC_OK;
@@ -3876,12 +3713,6 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "ip_group") *value = c->ip_group;
   else if (n == "pl_wave") *value = c->pl_wave;
-  else if (n == "emit_ido") *value = c->emit_ido;
-  else if (n == "emit_run") *value = c->emit_run;
-  else if (n == "emit_ido_active") {
-    if (!c->prepared) return fail(c, CYC_ERR_ARG, "emit_ido_active: call cyc_probe_prepare first");
-    *value = emit_ido_on(c) ? 1 : 0;
-  }
   else if (n == "pl_wave_active") {
     if (!c->prepared) return fail(c, CYC_ERR_ARG, "pl_wave_active: call cyc_probe_prepare first");
     *value = !ido_mode(c) && pl_wave_ok(c) ? 1 : 0;

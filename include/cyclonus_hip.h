@@ -179,12 +179,8 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  *   "ip_group"    8 (default, 1..64): IP peers per IP-row block
  *   "pl_wave"     1 (default) / 0: materialised-row class rows a wave per 64-word chunk where they
  *                 fit (<= 4 job slots and descriptors), or a thread per (slot chunk, word) item
- *   "emit_ido"    -1 (default: auto = 1 for rows >= 16 KB) / 0 / 1: identity-set builds compute the
- *                 class rows inside the emit, once per run of same-identity rows (1), or store them
- *                 first and copy (0)
- *   "emit_run"    16 (default, 1..64): rows per emit block when the emit computes the class rows
- * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active",
- * "pl_wave_active" and "emit_ido_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
+ * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
+ * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
  * uses (0 or 1). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
 int cyc_get_option(cyc_ctx* ctx, const char* name, int64_t* value);

@@ -379,41 +379,6 @@ def test_pod_words_from_identity_runs(gpu, seed):
                                               f"fused {fused} member_wave {mw} rpb {rpb} run {rep}")
 
 
-@pytest.mark.parametrize("seed", range(12))
-def test_emit_computes_ido_class_rows(gpu, seed):
-    """IDO builds with the class rows computed inside the emit (emit_ido = 1: one class row per run
-    of same-identity rows, written to every row of the run) equal the oracle and the class-row +
-    copy path (emit_ido = 0), for runs of 1..64 rows, on the graph and eager paths and on row
-    shards (each shard's runs are its own rows)."""
-    import torch
-
-    pols, res, probes = _deployment_problem(500 + seed, min_run=18 + seed)
-    want = Oracle(pols, res).probe(probes)
-    eng = Engine(0).build_policies(pols).load_resources(res)
-    sh = eng.prepare(probes)
-    eng.set_option("pod_words", 1)
-    P, K, W = sh["pods"], sh["slots"], sh["words"]
-    for emit_ido, run, graphs in ((1, 16, -1), (1, 1, 1), (1, 64, 0), (1, 7, 2), (0, 16, -1)):
-        eng.set_option("emit_ido", emit_ido)
-        eng.set_option("emit_run", run)
-        eng.set_option("graphs", graphs)
-        assert eng.get_option("emit_ido_active") == (emit_ido if K <= 32 else 0)
-        for rep in range(2):
-            assert_same(want, eng.run_host(), f"seed {seed} emit_ido {emit_ido} run {run} graphs {graphs} #{rep}")
-    eng.set_option("emit_ido", 1)
-    eng.set_option("graphs", -1)
-    n = 3
-    for r in range(n):  # row shards: [lo, hi) of both planes
-        lo, hi = r * P // n, (r + 1) * P // n
-        d_in = torch.full((hi - lo, K, W), 7, dtype=torch.int64, device="cuda")
-        d_eg = torch.full((hi - lo, K, W), 7, dtype=torch.int64, device="cuda")
-        d_st = torch.zeros((P, K), dtype=torch.uint8, device="cuda")
-        eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), torch.cuda.current_stream().cuda_stream, lo, hi)
-        torch.cuda.synchronize()
-        assert np.array_equal(d_in.cpu().numpy().view(np.uint64), want[1][lo:hi]), f"shard {r} ingress"
-        assert np.array_equal(d_eg.cpu().numpy().view(np.uint64), want[2][lo:hi]), f"shard {r} egress"
-
-
 @pytest.mark.parametrize("seed", range(6))
 def test_edge_shapes(gpu, seed):
     """Empty and ragged inputs, as the reference's tables allow them: no pods, one pod, pod counts
