@@ -1726,10 +1726,17 @@ __global__ __launch_bounds__(256) CYC_PL_WAVES void k_front_d_pm(FrontRows f) {
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
 // tail is made of the shorter ingress blocks (4 job slots per thread: profiles/r01_front_e_kc_ab.txt)
-__global__ __launch_bounds__(256) void k_front_e(FrontRows f) {
+#ifndef CYC_E_WAVES
+#define CYC_E_WAVES  // e.g. __attribute__((amdgpu_waves_per_eu(6))) for A/Bs
+#endif
+#ifndef CYC_E_KC
+#define CYC_E_KC 4  // job slots per thread in the fused IDO class rows (k_front_e)
+#endif
+constexpr int E_KC = CYC_E_KC;
+__global__ __launch_bounds__(256) CYC_E_WAVES void k_front_e(FrontRows f) {
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_ido_blk<true, 4>(f.ra[1], b, f.nb[1]);
-  else class_rows_ido_blk<false, 4>(f.ra[0], b - f.nb[1], f.nb[0]);
+  if (b < f.nb[1]) class_rows_ido_blk<true, E_KC>(f.ra[1], b, f.nb[1]);
+  else class_rows_ido_blk<false, E_KC>(f.ra[0], b - f.nb[1], f.nb[0]);
 }
 
 // The HBM-bound kernel: every target pod's plane rows are a copy of its class rows.  ONE launch
@@ -2180,6 +2187,9 @@ struct cyc_ctx {
   int64_t class_rpb_opt = 4;  // "class_rpb": IDO class-row representatives per block
                               // (config3 N=1 -1%: profiles/r01_class_rpb_ab.txt)
   uint32_t ip_group = IP_GROUP;  // "ip_group": IP-peer tests per block in the IP rows
+  int step_events = 0;  // "step_events": graph / eager-DAG runs record the whole-step timing events (1);
+                        // off by default: the two timing events cost ~9 us of idle GPU per step
+                        // (config #2 0.077 -> 0.069 ms/step, profiles/r02_step_events_ab.txt)
   int pl_wave = 1;      // "pl_wave": PM-build class rows a wave per 64-word chunk where they fit (1),
                         // or a thread per (slot chunk, word) item (0)
   int front_fused = 1;  // "front_fused": the front as block-range-fused launches on one stream
@@ -2206,7 +2216,8 @@ struct cyc_ctx {
   int64_t order_lo = -1, order_hi = -1;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   double last_ms[3] = {0, 0, 0};
-  bool timed = false;
+  bool timed = false;  // the last run recorded the step timing events
+  bool ran = false;    // a run has been enqueued
 };
 
 int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t idx);
@@ -3035,9 +3046,9 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fe.ra[d] = fd.ra[d];
     fe.ra[d].ht_clear_words = 0;
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + 3) / 4) + 3) / 4);
-    const size_t per = size_t(d == 0 ? std::min<uint32_t>(4, K) : D) * fd.ra[d].EW * 8;
+    const size_t per = size_t(d == 0 ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8;
     fe.ra[d].rpb = class_rpb(c, per);
-    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + 3) / 4) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
+    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
     lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
   const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
@@ -3174,10 +3185,10 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     // the graph's DAG, enqueued directly: the caller's stream forks to two internal streams and
     // joins them back before the emit (events), without hipGraphLaunch's per-replay latency
     ensure_cap_streams(c);
-    HIPCHK(hipEventRecord(c->ev[0], st));
+    if (c->step_events) HIPCHK(hipEventRecord(c->ev[0], st));
     capture_pipeline(c, st, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status, lo, hi);
-    HIPCHK(hipEventRecord(c->ev[3], st));
-    c->timed = true;
+    if (c->step_events) HIPCHK(hipEventRecord(c->ev[3], st));
+    c->timed = c->step_events != 0;
     c->timed_graph = true;
   } else if (graphs && !pb.may_err) {
     // The whole pipeline as one hipGraph (captured once per output buffers / row range):
@@ -3195,17 +3206,18 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
       HIPCHK(hipEventCreateWithFlags(&c->graph_done, hipEventDisableTiming));
       memcpy(c->graph_key, key, sizeof(key));
     }
-    HIPCHK(hipEventRecord(c->ev[0], st));
+    if (c->step_events) HIPCHK(hipEventRecord(c->ev[0], st));
     HIPCHK(hipGraphLaunch(c->graph_exec, st));
     HIPCHK(hipEventRecord(c->graph_done, st));  // the exec may be retired once this completes
-    HIPCHK(hipEventRecord(c->ev[3], st));
-    c->timed = true;
+    if (c->step_events) HIPCHK(hipEventRecord(c->ev[3], st));
+    c->timed = c->step_events != 0;
     c->timed_graph = true;
   } else {
     enqueue_pipeline(c, st, d_in, d_eg, d_status, lo, hi);
     c->timed = true;
     c->timed_graph = false;
   }
+  c->ran = true;
 
   // 8. panic path: the first panicking job in job order, as the reference would hit it.  Configs
   // run in order (one RunProbeForConfig each); within one, the job expansion (may panic on a pod
@@ -3651,7 +3663,7 @@ void cyc_table_destroy(cyc_table* t) {
 
 int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
   if (!c || !ms) return CYC_ERR_ARG;
-  if (!c->timed) return fail(c, CYC_ERR_ARG, "no run yet");
+  if (!c->timed) return fail(c, CYC_ERR_ARG, c->ran ? "the last run recorded no timing events (step_events = 0)" : "no run yet");
   return guarded(c, [&] {
     HIPCHK(hipEventSynchronize(c->ev[3]));
     float a = 0, b = 0, r = 0;
@@ -3668,7 +3680,7 @@ int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
 
 int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
   if (!c || !out || n < 2) return CYC_ERR_ARG;
-  if (!c->timed) return fail(c, CYC_ERR_ARG, "no run yet");
+  if (!c->ran) return fail(c, CYC_ERR_ARG, "no run yet");
   return guarded(c, [&]() -> int {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipDeviceSynchronize());
@@ -3697,6 +3709,7 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "class_rpb") range(1, 64), c->class_rpb_opt = value;
     else if (n == "ip_group") range(1, 64), c->ip_group = uint32_t(value);
     else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
+    else if (n == "step_events") range(0, 1), c->step_events = int(value);
     else return fail(c, CYC_ERR_ARG, "unknown option " + n);
     drop_graph(c);
     return (int)CYC_OK;
@@ -3713,6 +3726,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "ip_group") *value = c->ip_group;
   else if (n == "pl_wave") *value = c->pl_wave;
+  else if (n == "step_events") *value = c->step_events;
   else if (n == "pl_wave_active") {
     if (!c->prepared) return fail(c, CYC_ERR_ARG, "pl_wave_active: call cyc_probe_prepare first");
     *value = !ido_mode(c) && pl_wave_ok(c) ? 1 : 0;

@@ -153,7 +153,9 @@ void cyc_table_destroy(cyc_table* t);
 
 /* Average device time (ms) of the last run's kernels, measured with HIP events on the launch
  * stream: [0] whole pipeline, [1] the emit launch (the HBM-roofline kernel; one launch writes both
- * planes), [2] class rows of both directions.  Graph runs report only [0] ([1], [2] = -1). */
+ * planes), [2] class rows of both directions.  Eager runs ("graphs" = 0) always record them; graph
+ * and fused-eager runs only with "step_events" = 1, and report only [0] ([1], [2] = -1); without
+ * events the call fails with CYC_ERR_ARG. */
 int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 
 /* Diagnostic: number of distinct classes (class rows computed) of the last run, [0] ingress,
@@ -177,6 +179,8 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  *                 thread (0) or a wave (1) per pod identity
  *   "class_rpb"   4 (default, 1..64): class representatives per identity-set class-row block
  *   "ip_group"    8 (default, 1..64): IP peers per IP-row block
+ *   "step_events" 0 (default) / 1: graph and fused-eager runs also record the whole-step timing
+ *                 events cyc_last_timings reads (they idle the GPU ~9 us between steps)
  *   "pl_wave"     1 (default) / 0: materialised-row class rows a wave per 64-word chunk where they
  *                 fit (<= 4 job slots and descriptors), or a thread per (slot chunk, word) item
  * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and

@@ -45,6 +45,7 @@ n = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 data = synth.CONFIGS[name]()
 eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
 sh = eng.prepare(data["probes"])
+eng.set_option("step_events", 1)  # whole-step timing events (cyc_last_timings)
 P, K, W = sh["pods"], sh["slots"], sh["words"]
 d_in = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
 d_eg = torch.empty((P, K, W), dtype=torch.int64, device="cuda")

@@ -8,6 +8,7 @@ from cyclonus_amd.shard import row_range
 data = synth.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "config3"]()
 eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
 sh = eng.prepare(data["probes"])
+eng.set_option("step_events", 1)  # whole-step timing events (cyc_last_timings)
 P, K, W = sh["pods"], sh["slots"], sh["words"]
 d_in = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
 d_eg = torch.empty((P, K, W), dtype=torch.int64, device="cuda")

@@ -481,10 +481,22 @@ def test_launch_modes_and_knobs(gpu):
     fused = not eng.shape["may_panic"]  # no-panic build: the fused front applies
     assert eng.get_option("front_fused_active") == int(fused)
     assert eng.get_option("launch") == (2 if fused else 1)
-    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("ip_group", 3), ("graphs", 1), ("graphs", -1)):
+    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("ip_group", 3), ("graphs", 1), ("graphs", -1),
+                    ("step_events", 1), ("step_events", 0)):
         eng.set_option(name, v)
         assert eng.get_option(name) == v
         assert_same(want, eng.run_host(), f"{name}={v}")
+    # whole-step timing events: off by default for graph / fused-eager runs, always for eager runs
+    with pytest.raises(Exception):
+        eng.timings()
+    eng.set_option("step_events", 1)
+    eng.run_host()
+    assert eng.timings()[0] > 0
+    eng.set_option("step_events", 0)
+    eng.set_option("graphs", 0)
+    eng.run_host()
+    assert all(t >= 0 for t in eng.timings())
+    eng.set_option("graphs", -1)
     eng.set_option("front_fused", 0)
     assert eng.get_option("front_fused_active") == 0 and eng.get_option("launch") == 1
     assert_same(want, eng.run_host(), "DAG graph")
