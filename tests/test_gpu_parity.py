@@ -379,6 +379,50 @@ def test_pod_words_from_identity_runs(gpu, seed):
                                               f"fused {fused} member_wave {mw} rpb {rpb} run {rep}")
 
 
+def _wide_ports_problem(seed, n_pods=150):
+    """Pods with many containers (AllAvailable: > 32 job slots per pod) over > 32 distinct job
+    descriptors, so the descriptor bit rows (<= 32) and the slot-bit list entries (<= 32) do not
+    apply: the class rows take their byte-table port checks.  Policies mix numbered, named and
+    ranged ports with pod and IPBlock peers."""
+    import random
+
+    r = random.Random(seed)
+    pols, res, _ = random_problem(60_000 + seed, n_pods=n_pods, n_pols=14)
+    protos = ["TCP", "UDP", "SCTP"]
+    for i, p in enumerate(res["Pods"]):
+        conts = []
+        for j, (port, proto) in enumerate(r.sample([(7000 + x, pr) for x in range(25) for pr in protos], r.randint(33, 44))):
+            # distinct (protocol, port) per pod: AllAvailable job keys must not collide (table.go)
+            conts.append({"Name": f"c{j}", "Port": port, "Protocol": proto, "PortName": f"p{port}-{proto.lower()}"})
+        p["Containers"] = conts
+    for k, pol in enumerate(pols):
+        spec = pol.get("spec") or {}
+        for key, peer_key in (("ingress", "from"), ("egress", "to")):
+            for rule in spec.get(key) or []:
+                if rule is None or r.random() < 0.3:
+                    continue
+                rule["ports"] = [{"port": 7000 + r.randint(0, 24), "protocol": protos[r.randint(0, 2)]},
+                                 {"port": f"p{7000 + r.randint(0, 24)}-tcp"},
+                                 {"port": 7010, "endPort": 7010 + r.randint(0, 8), "protocol": "UDP"}][: r.randint(1, 3)]
+    return pols, res, [{"AllAvailable": True}, {"Port": 7003, "Protocol": "TCP"}]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_wide_ports(gpu, seed):
+    """> 32 job slots and > 32 job descriptors through every class-row path (identity sets, PM
+    rows by item walk; the wave-per-chunk rows do not apply) against the oracle."""
+    pols, res, probes = _wide_ports_problem(seed)
+    want = Oracle(pols, res).probe(probes)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    sh = eng.prepare(probes)
+    assert sh["slots"] > 32 and sh["descriptors"] > 32, sh
+    for pod_words, fused in ((0, 1), (0, 0), (1, 1), (-1, 1)):
+        eng.set_option("pod_words", pod_words)
+        eng.set_option("front_fused", fused)
+        assert eng.get_option("pl_wave_active") == 0
+        assert_same(want, eng.run_host(), f"seed {seed} pod_words {pod_words} fused {fused}")
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_edge_shapes(gpu, seed):
     """Empty and ragged inputs, as the reference's tables allow them: no pods, one pod, pod counts
