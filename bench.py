@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=20)  # GPU clocks settle after the host-side prepare
-    ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4", "config5"])
+    ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4", "config5", "config3u"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-assemble", action="store_true", help="skip the N>1 all-gather timing")
@@ -248,9 +248,13 @@ def main():
     value = cells / (dt / args.steps)
 
     # the emit writes each plane (ingress, egress) of this rank's rows once, both in ONE launch:
-    # rows x K x W x 8 B per plane = 2 bits per cell
+    # rows x K x W x 8 B per plane = 2 bits per cell — less the rows that already hold their class
+    # row (in-place class rows, cyc_set_option class_inplace: one row per class and plane is written
+    # by the class-row kernel, the emit copies it to the class's other rows)
     launches = 1
-    emit_bytes = rows * K * W * 8 * 2
+    inplace = eng.get_option("class_inplace_active") == 1
+    emit_rows = 2 * rows - (classes_in + classes_eg if inplace else 0)
+    emit_bytes = emit_rows * K * W * 8
     emit_launch_ms = emit_ms
     achieved = emit_bytes / (emit_launch_ms * 1e-3) / 1e9
     # the emit kernel the library picks by plane-row length (engine.hip enq_emit)
@@ -314,6 +318,8 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": emit_bytes,
+                "emit_rows_per_launch": emit_rows,
+                "class_rows_in_place": inplace,
                 "emit_ms_per_launch": emit_launch_ms,
                 "launches_per_step": launches,
                 "fill_ceiling_GBs": fill_gbs,

@@ -168,6 +168,52 @@ __global__ __launch_bounds__(256) void k_selectors_dense(uint32_t S, uint32_t L,
                                                          const uint32_t* __restrict__ LVT, uint8_t* __restrict__ selres,
                                                          const uint32_t* __restrict__ sel_list) { selectors_dense_blk(S, L, sel_off, dreqs, req_vals, LVT, selres, sel_list, blockIdx.x, gridDim.x); }
 
+// A selector's outcome on a label set, from SELRES (dense builds) or evaluated on the spot from the
+// dense label table (lazy builds: PM builds, whose pods carry ~as many label sets as there are pods,
+// evaluate only the (selector, label set) pairs a membership walk or a pod-peer word reaches instead
+// of every pair).  Same result as selectors_dense_blk: requirements in order, the first failing one
+// decides 0, an invalid operator reached with every earlier requirement matched is a panic (2).
+struct SelView {
+  const uint8_t* selres;  // null: evaluate through LVT
+  uint32_t L;
+  const uint32_t *sel_off, *req_vals, *LVT;
+  const DReq* dreqs;
+  const uint32_t* PLVT;   // LVT's columns per pod: PLVT[kx][q] = LVT[kx][label set of pod q]
+  uint32_t P;
+};
+// (tab, n) = (LVT, L) with l a label set, or (PLVT, P) with l a pod: the key's value column
+__device__ __forceinline__ uint32_t sel_eval(const SelView& v, const uint32_t* __restrict__ tab, uint32_t n, uint32_t s, uint32_t l) {
+  for (uint32_t r = v.sel_off[s]; r < v.sel_off[s + 1]; r++) {
+    const DReq q = v.dreqs[r];
+    if (q.op == REQ_INVALID) return 2;
+    const uint32_t x = tab[uint64_t(q.key) * n + l];
+    const bool present = x != 0xFFFFFFFFu;
+    bool ok;
+    switch (q.op) {
+      case REQ_EQ: ok = present && x == v.req_vals[q.voff]; break;
+      case REQ_EQ_EMPTY: ok = !present || x == v.req_vals[q.voff]; break;
+      case REQ_IN:
+      case REQ_NOTIN: {
+        bool in = false;
+        for (uint32_t j = 0; j < q.vcnt; j++) in |= (v.req_vals[q.voff + j] == x);
+        ok = present && (q.op == REQ_IN ? in : !in);
+        break;
+      }
+      case REQ_EXISTS: ok = present; break;
+      default: ok = !present; break;  // REQ_DNE
+    }
+    if (!ok) return 0;
+  }
+  return 1;
+}
+__device__ __forceinline__ uint32_t sel_at(const SelView& v, uint32_t s, uint32_t l) {
+  if (v.selres) return v.selres[uint64_t(s) * v.L + l];
+  return sel_eval(v, v.LVT, v.L, s, l);
+}
+// Pod selector s on pod q's own labels through PLVT: one coalesced load per requirement for a wave
+// of consecutive pods, instead of a pod -> label set -> table gather chain.
+__device__ __forceinline__ uint32_t sel_at_pod(const SelView& v, uint32_t s, uint32_t q) { return sel_eval(v, v.PLVT, v.P, s, q); }
+
 __device__ __forceinline__ void fill_u32_blk(uint32_t* p, uint64_t n, uint32_t v, uint32_t bid_, uint32_t nblk_) {
   const uint64_t i = bid_ * uint64_t(blockDim.x) + threadIdx.x;
   if (i < n) p[i] = v;
@@ -289,6 +335,183 @@ __global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                          const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
                                                          uint64_t* __restrict__ ER) { pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, PM, ER, blockIdx.x, gridDim.x); }
+
+// Pod-peer rows of the fused front on PM builds (no panic possible), stored sparse, 64-word chunks
+// at a time with lane = pod word (block shapes: pod_rows_sparse_blk).  The namespace
+// matcher runs first (podpeermatcher.go:21-28) and decides most words without looking at a pod:
+// an exact namespace (nskind 0: the policy's own) matches only the words holding that namespace's
+// pods — pods of a namespace are normally listed together, so a chunk whose namespace range
+// misses it is skipped whole — and a namespace selector is ONE lookup for a word whose pods share
+// a namespace.  The remaining words are evaluated a pod per lane, PR_WB words at once per wave
+// (their loads in flight together).  Rows are stored chunk-dense with their nonzero word span and chunk masks,
+// exactly like the IP rows (ip_row_word), so the class rows skip their zero chunks: with every pod
+// labelled apart (identities ~ pods) most pod-peer rows are a namespace's worth of words.
+struct DWordNS {
+  uint32_t lo, hi;  // namespace string ids of the word's (chunk's) pods: min, max
+  uint32_t nsls;    // their namespace label set when lo == hi
+  uint32_t pad;
+};
+#ifndef CYC_PR_WB
+#define CYC_PR_WB 8
+#endif
+constexpr uint32_t PR_WB = CYC_PR_WB;  // words evaluated at once per wave
+
+// labelselector.go:66-86 for one requirement, x = the pod's value of the key (~0: absent), with at
+// most two values (v0, v1; vc of them)
+__device__ __forceinline__ bool req_holds(uint32_t op, uint32_t x, uint32_t v0, uint32_t v1, uint32_t vc) {
+  const bool present = x != 0xFFFFFFFFu;
+  const bool in = (vc > 0 && x == v0) || (vc > 1 && x == v1);
+  switch (op) {
+    case REQ_EQ: return present && x == v0;
+    case REQ_EQ_EMPTY: return !present || x == v0;
+    case REQ_IN: return present && in;
+    case REQ_NOTIN: return present && !in;
+    case REQ_EXISTS: return present;
+    default: return !present;  // REQ_DNE
+  }
+}
+
+// Word masks of pod peer pr over chunk `chunk` (this lane's word w): the namespace outcome per word
+// first, then a pod per lane for the words it leaves open — only those of rank part, part + parts,
+// ... among them (a chunk's words split over `parts` waves).
+__device__ __forceinline__ uint64_t pod_chunk_words(const DPeer& pr, const SelView& sv, uint32_t P, uint32_t W, uint32_t chunk,
+                                                    uint32_t lane, uint32_t part, uint32_t parts,
+                                                    const uint32_t* __restrict__ pod_ns, const uint32_t* __restrict__ pod_nsls,
+                                                    const uint32_t* __restrict__ pod_ls, const DWordNS* __restrict__ nsw) {
+  const uint32_t w = chunk * 64 + lane;
+  const bool valid = w < W;
+  DWordNS wn{0xFFFFFFFFu, 0u, 0u, 0u};
+  if (valid) wn = nsw[w];
+  uint32_t nsm = 0;  // the word's namespace outcome: 0 no pod, 1 every pod, 2 per pod
+  if (valid) {
+    if (pr.nskind == 1) nsm = 1;
+    else if (pr.nskind == 0) nsm = (pr.nsval < wn.lo || pr.nsval > wn.hi) ? 0u : (wn.lo == wn.hi ? 1u : 2u);
+    else nsm = wn.lo == wn.hi ? (sel_at(sv, pr.nsval, wn.nsls) == 1 ? 1u : 0u) : 2u;
+  }
+  uint64_t mine = 0;
+  if (part == 0 && nsm == 1 && pr.podsel == CYC_ALL) mine = (w == W - 1 && P % 64) ? ((1ull << (P % 64)) - 1) : ~0ull;
+  uint64_t todo = __ballot(nsm == 2 || (nsm == 1 && pr.podsel != CYC_ALL));
+  // a pod selector of ONE requirement with <= 2 values (matchLabels {k: v}, the common shape) is
+  // held in scalar registers: a batch's PLVT loads then all go out together instead of one
+  // requirement walk (dependent loads) per word; other shapes walk the requirements (sel_at_pod)
+  // or, with the dense table, gather SELRES through the pod's label set
+  uint32_t r_op = REQ_INVALID, r_key = 0, r_v0 = 0, r_v1 = 0, r_vc = 0;
+  if (pr.podsel != CYC_ALL && sv.sel_off[pr.podsel + 1] - sv.sel_off[pr.podsel] == 1) {
+    const DReq q1 = sv.dreqs[sv.sel_off[pr.podsel]];
+    if (q1.op != REQ_INVALID && q1.vcnt <= 2) {
+      r_op = q1.op;
+      r_key = q1.key;
+      r_vc = q1.vcnt;
+      r_v0 = q1.vcnt > 0 ? sv.req_vals[q1.voff] : 0u;
+      r_v1 = q1.vcnt > 1 ? sv.req_vals[q1.voff + 1] : 0u;
+    }
+  }
+  const bool one = r_op != REQ_INVALID;
+  if (parts > 1) {  // this wave's share
+    uint64_t sub = 0;
+    for (uint32_t r = 0; todo; r++, todo &= todo - 1)
+      if (r % parts == part) sub |= todo & (~todo + 1);
+    todo = sub;
+  }
+  while (todo) {
+    uint32_t wl[PR_WB], nsv[PR_WB], q[PR_WB], xv[PR_WB];
+    bool live[PR_WB];
+#pragma unroll
+    for (uint32_t u = 0; u < PR_WB; u++) {
+      wl[u] = 64;
+      if (todo) {
+        wl[u] = __ffsll((unsigned long long)todo) - 1;
+        todo &= todo - 1;
+      }
+      q[u] = (chunk * 64 + wl[u]) * 64 + lane;
+      live[u] = wl[u] < 64 && q[u] < P;
+      // the pod's namespace (exact matcher) or namespace label set (selector), when needed
+      nsv[u] = live[u] && pr.nskind != 1 ? (pr.nskind == 0 ? pod_ns[q[u]] : pod_nsls[q[u]]) : 0u;
+      // the selector's key value of the pod (one requirement), or the pod's label set (dense table)
+      xv[u] = 0;
+      if (live[u] && pr.podsel != CYC_ALL) xv[u] = one ? sv.PLVT[uint64_t(r_key) * P + q[u]] : sv.selres ? pod_ls[q[u]] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < PR_WB; u++) {
+      // no panic is possible here: outcomes are 0 / 1 only, so both matchers can be evaluated
+      bool a = pr.nskind == 1 || (pr.nskind == 0 && nsv[u] == pr.nsval);
+      if (pr.nskind == 2) a = live[u] && sel_at(sv, pr.nsval, nsv[u]) == 1;
+      bool b = pr.podsel == CYC_ALL;
+      if (!b && live[u])
+        b = one ? req_holds(r_op, xv[u], r_v0, r_v1, r_vc)
+                : (sv.selres ? sv.selres[uint64_t(pr.podsel) * sv.L + xv[u]] : sel_at_pod(sv, pr.podsel, q[u])) == 1;
+      const uint64_t m = __ballot(live[u] && a && b);
+      if (lane == wl[u]) mine = m;
+    }
+  }
+  return mine;
+}
+
+// One wave stores chunk `chunk` of peer j's row (v = this lane's word) chunk-dense, with its
+// nonzero flag, and widens the row's word span and nonzero-chunk mask.
+__device__ __forceinline__ void pod_chunk_store(uint32_t j, uint32_t chunk, uint32_t W, uint32_t lane, uint64_t v,
+                                                uint64_t* __restrict__ PM, uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz) {
+  const uint32_t w = chunk * 64 + lane;
+  const uint64_t nzc = __ballot(v != 0);
+  if (nzc && w < W) PM[uint64_t(j) * W + w] = v;  // a nonzero chunk stores all its words
+  if (lane == 0) {
+    cnz[uint64_t(j) * ((W + 63) / 64) + chunk] = nzc ? 1u : 0u;
+    if (nzc) {
+      atomicMin(&rng[4 * j], chunk * 64 + __ffsll((unsigned long long)nzc) - 1);
+      atomicMin(&rng[4 * j + 1], ~(chunk * 64 + 63 - __clzll((long long)nzc)));
+      if (chunk < 64) atomicAnd(reinterpret_cast<unsigned long long*>(rng) + 2 * j + 1, ~(1ull << chunk));
+    }
+  }
+}
+
+// grp > 1: block = (grp pod peers, 4 chunks), a wave per chunk walking the group's peers (many
+// peers: the grid is large anyway).  grp == 1: block = (pod peer, 4 chunks) taken one chunk at a
+// time, each chunk's open words split over the 4 waves and met in LDS (few peers with dense rows:
+// config #2 26 us, where a wave per chunk leaves 3 waves per peer and takes 100 us).
+__device__ __forceinline__ void pod_rows_sparse_blk(uint32_t Rp, uint32_t P, uint32_t W, const uint32_t* __restrict__ plist,
+                                                    const DPeer* __restrict__ peers, const SelView& sv,
+                                                    const uint32_t* __restrict__ pod_ns,
+                                                    const uint32_t* __restrict__ pod_nsls, const uint32_t* __restrict__ pod_ls,
+                                                    const DWordNS* __restrict__ nsw, uint64_t* __restrict__ PM,
+                                                    uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t grp,
+                                                    uint32_t bid_) {
+  __shared__ uint64_t s_m[4][64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t chunks = (W + 63) / 64, cb = (chunks + 3) / 4;
+  const uint32_t x0 = (bid_ / cb) * grp;
+  if (x0 >= Rp) return;  // whole block
+  if (grp > 1) {
+    const uint32_t chunk = __builtin_amdgcn_readfirstlane((bid_ % cb) * 4 + wave);
+    if (chunk >= chunks) return;
+    const DWordNS ck = nsw[W + chunk];
+    for (uint32_t x = x0; x < min(Rp, x0 + grp); x++) {
+      const uint32_t j = plist[x];
+      const DPeer pr = peers[j];
+      if (pr.nskind == 0 && (pr.nsval < ck.lo || pr.nsval > ck.hi)) {  // no pod of the namespace here
+        if (lane == 0) cnz[uint64_t(j) * chunks + chunk] = 0;
+        continue;
+      }
+      const uint64_t v = pod_chunk_words(pr, sv, P, W, chunk, lane, 0, 1, pod_ns, pod_nsls, pod_ls, nsw);
+      pod_chunk_store(j, chunk, W, lane, v, PM, rng, cnz);
+    }
+    return;
+  }
+  const uint32_t j = plist[x0];
+  const DPeer pr = peers[j];
+  for (uint32_t ci = 0; ci < 4; ci++) {
+    const uint32_t chunk = (bid_ % cb) * 4 + ci;  // block-uniform
+    if (chunk >= chunks) break;
+    const DWordNS ck = nsw[W + chunk];
+    if (pr.nskind == 0 && (pr.nsval < ck.lo || pr.nsval > ck.hi)) {
+      if (threadIdx.x == 0) cnz[uint64_t(j) * chunks + chunk] = 0;
+      continue;
+    }
+    s_m[wave][lane] = pod_chunk_words(pr, sv, P, W, chunk, lane, wave, 4, pod_ns, pod_nsls, pod_ls, nsw);
+    __syncthreads();
+    if (wave == 0) pod_chunk_store(j, chunk, W, lane, s_m[0][lane] | s_m[1][lane] | s_m[2][lane] | s_m[3][lane], PM, rng, cnz);
+    __syncthreads();  // s_m is reused by the next chunk
+  }
+}
 
 // IP peers depend on each pod's own address: one wave per 64-pod word (one lane per pod).  A
 // block owns IPB_BATCH IP peers: their CIDR and except records (host-flattened, in evaluation
@@ -618,7 +841,7 @@ struct MemberArgs {
   const uint8_t* id_status;   // ingress: [n_ident][K]
   const uint32_t *tns_lo, *tns_hi;
   const DTarget* tgt;
-  const uint8_t* selres;
+  SelView sv;                 // target pod selectors on the identity's label set
   const uint32_t* list_off;   // host-computed upper-bound offsets
   uint32_t* list;             // matching target ids (ascending = primary-key order)
   uint32_t* cnt;
@@ -687,7 +910,7 @@ __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t
 #pragma unroll
     for (uint32_t x = 0; x < MB; x++) sel[x] = t0 + x < hi ? a.tgt[t0 + x].sel : 0u;
 #pragma unroll
-    for (uint32_t x = 0; x < MB; x++) r[x] = t0 + x < hi ? a.selres[uint64_t(sel[x]) * a.L + ls] : 0;
+    for (uint32_t x = 0; x < MB; x++) r[x] = t0 + x < hi ? uint8_t(sel_at(a.sv, sel[x], ls)) : 0;
 #pragma unroll
     for (uint32_t x = 0; x < MB; x++) {
       const uint32_t t = t0 + x;
@@ -741,7 +964,7 @@ __device__ __forceinline__ void member_wave_blk(MemberArgs a, uint32_t bid_, uin
   uint64_t h = 0x5bd1e9955bd1e995ull;
   for (uint32_t t0 = lo; t0 < hi; t0 += 64) {
     const uint32_t t = t0 + lane;
-    const uint8_t r = t < hi ? a.selres[uint64_t(a.tgt[t].sel) * a.L + ls] : 0;
+    const uint8_t r = t < hi ? uint8_t(sel_at(a.sv, a.tgt[t].sel, ls)) : 0;
     e |= __ballot(r == 2) != 0;
     const uint64_t m = __ballot(r == 1);
     if (r == 1) a.list[off + n + __popcll(m & ((1ull << lane) - 1))] = t;
@@ -831,7 +1054,8 @@ struct RowArgs {
   const uint64_t* VALID;     // egress only [K][W]
   const int32_t* DESCW;      // egress only [K][W]
   const uint64_t* DM;        // egress only [K][D][W]
-  uint64_t* A;               // [n_ident][K][W]
+  uint64_t* A;               // [n_ident][K][W], or the output plane when arow is set
+  const uint32_t* arow;      // in-place class rows: identity -> its first pod's row of the output plane
   uint64_t* AE;              // [n_ident][K][W] (ERR builds only)
   // IDO builds (no panic possible, every 64-pod word holds <= IDO_MAX_RUNS identity runs):
   // pod peers are folded per class into identity-space sets B by k_class_ident, and the class
@@ -846,6 +1070,7 @@ struct RowArgs {
   const uint32_t* ip_rng;    // [R][4] per IP peer (no-panic runs): first word, ~last word of its nonzero PM
                              // words, then (u64) ~ the mask of its chunks holding one (chunks < 64)
   const uint32_t* ip_cnz;    // [R][W/64] 1 if the 64-word chunk of an IP peer's PM row was written
+  uint32_t pod_sparse;       // PM builds' fused front: pod-peer rows are stored like IP rows (pod_rows_sparse_blk)
   uint32_t E, EW, NB;
   uint32_t rpb;              // IDO class rows: representatives per block (class_rows_ido_blk)
   // the direction's hash table (keys + reps), emptied for the NEXT run by the first class-row
@@ -853,6 +1078,11 @@ struct RowArgs {
   uint32_t* ht_clear;
   uint64_t ht_clear_words;
 };
+
+// Row of A holding representative i's class rows: its identity slot, or (in-place class rows) the
+// plane row of the first pod of identity i in the run's rows — that pod's plane row IS the class
+// row, so the emit leaves it alone and copies it to the class's other pods.
+__device__ __forceinline__ uint64_t arow_of(const RowArgs& a, uint32_t i) { return a.arow ? a.arow[i] : i; }
 
 __device__ __forceinline__ void ht_clear_slice(const RowArgs& a, uint32_t bid, uint32_t nblk) {
   if (!a.ht_clear_words) return;
@@ -1258,7 +1488,7 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
       if (k < a.K && (allow[q][kk] & valid[q][kk]) == 0x123456789ull) a.A[(uint64_t(i) * a.K + k) * a.W + w[q]] = 1;
       continue;
 #endif
-      if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w[q]] = allow[q][kk] & valid[q][kk];
+      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.W + w[q]] = allow[q][kk] & valid[q][kk];
     }
 }
 
@@ -1367,7 +1597,7 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
           if (d < a.D) r |= acc[d] & dm[uint64_t(d) * a.W];
         r &= valid[k];
       }
-      a.A[(uint64_t(i) * a.K + k) * a.W + w] = r;
+      a.A[(arow_of(a, i) * a.K + k) * a.W + w] = r;
     }
   }
 }
@@ -1423,7 +1653,7 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
           sh.all = 1;  // AllPeersMatcher
         } else {
           en = make_uint4(pr.kind == 1 ? PL_ONES : j, pr.port, 0u, a.W - 1);
-          if (pr.kind == 3) {  // bit 31 of z: an IP row (only the cnz-marked words were written)
+          if (pr.kind == 3 || (pr.kind == 2 && a.pod_sparse)) {  // bit 31 of z: a sparse row (only the cnz-marked words were written)
             en.z = a.ip_rng[4 * j] | PL_IP;
             en.w = ~a.ip_rng[4 * j + 1];
             if (a.ip_rng[4 * j] == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
@@ -1601,7 +1831,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
       const uint32_t k = k0 + kk;
-      if (k < a.K) a.A[(uint64_t(i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
+      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
     }
   }
 }
@@ -1649,7 +1879,8 @@ __global__ __launch_bounds__(256) void k_front_a(FrontA f) {
 struct FrontB {
   uint32_t nb[5];
   uint32_t ip_grp;      // IP rows: peers per wave
-  uint32_t pod_direct;  // PM builds: segment 1 = pod-peer rows per pod (k_pod_rows_direct), else identity sets
+  uint32_t pod_direct;  // PM builds with few pod-peer words: segment 1 = full pod-peer rows per pod
+                        // (pod_rows_direct_blk), else identity sets (IDO)
   uint32_t Rp;
   const uint32_t *plist, *pod_eid;
   uint32_t M, D;
@@ -1695,15 +1926,33 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   if (b < f.nb[4]) portbits_blk(f.M, f.D, f.portok, f.portbits, b);  // for the egress class rows
 }
 
+// Launch C also carries PM builds' sparse pod-peer rows (they need only launch A's selector table
+// and precede the class rows): the light class election keeps them off launch B, whose IP rows and
+// membership would otherwise run at the pod rows' register budget (occupancy 8 -> 5-7).
 struct FrontC {
-  uint32_t nb[2];
+  uint32_t nb[3];
   MemberArgs ma[2];
   uint32_t* class_of[2];
+  // sparse pod-peer rows (pod_rows_sparse_blk)
+  uint32_t Rp, P, W, pr_grp;
+  const uint32_t* plist;
+  const DPeer* peers;
+  SelView sv;
+  const uint32_t *pod_ns, *pod_nsls, *pod_ls;
+  const DWordNS* nsw;  // per word, then per chunk: namespace ranges
+  uint64_t* PM;
+  uint32_t *rng, *cnz;
 };
 __global__ __launch_bounds__(256) void k_front_c(FrontC f) {
-  const uint32_t b = blockIdx.x;
-  if (b < f.nb[0]) classify_blk(f.ma[0], f.class_of[0], b, f.nb[0]);
-  else classify_blk(f.ma[1], f.class_of[1], b - f.nb[0], f.nb[1]);
+  uint32_t b = blockIdx.x;
+  if (b < f.nb[0]) return classify_blk(f.ma[0], f.class_of[0], b, f.nb[0]);
+  b -= f.nb[0];
+  if (b < f.nb[1]) return classify_blk(f.ma[1], f.class_of[1], b, f.nb[1]);
+  b -= f.nb[1];
+#ifdef CYC_DIAG_NO_PODROWS  // timing diagnostic only (rows stay empty: results are wrong)
+  return;
+#endif
+  pod_rows_sparse_blk(f.Rp, f.P, f.W, f.plist, f.peers, f.sv, f.pod_ns, f.pod_nsls, f.pod_ls, f.nsw, f.PM, f.rng, f.cnz, f.pr_grp, b);
 }
 
 struct FrontRows {
@@ -1755,6 +2004,7 @@ struct EmitArgs {
   const uint32_t* order[2];   // pods in [row_lo,row_hi) clustered by the plane's class
   const uint32_t *pod_id[2], *class_of[2];
   const uint64_t* A[2];
+  const uint32_t* arow[2];    // in-place class rows (RowArgs::arow): the class row is a row of out
   uint64_t* out[2];
   uint64_t row_words;         // K * W
   uint32_t chunk;             // k_emit_flat: rows per block
@@ -1775,6 +2025,15 @@ __device__ __forceinline__ void emit_row_of(const EmitArgs& a, uint32_t r, uint3
   }
 }
 
+// Source of plane pl's row for pod p: its class row; null when the row is itself its class's row
+// (in-place class rows: nothing to copy).
+__device__ __forceinline__ const uint64_t* emit_src(const EmitArgs& a, uint32_t pl, uint32_t p) {
+  const uint32_t c = a.class_of[pl][a.pod_id[pl][p]];
+  if (!a.arow[pl]) return a.A[pl] + uint64_t(c) * a.row_words;
+  const uint32_t r = a.arow[pl][c];
+  return r == p - a.row_lo ? nullptr : a.out[pl] + uint64_t(r) * a.row_words;
+}
+
 // Block b's slice of the status plane copy (every emit kernel calls this first).
 __device__ __forceinline__ void emit_status(const EmitArgs& a) {
   if (!a.st_bytes) return;
@@ -1792,7 +2051,8 @@ __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
   if (r >= min(2 * a.n_rows, (x + 1) * a.per_xcd)) return;
   uint32_t pl, p;
   emit_row_of(a, r, pl, p);
-  const uint64_t* src = a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words;
+  const uint64_t* src = emit_src(a, pl, p);
+  if (!src) return;
   uint64_t* dst = a.out[pl] + uint64_t(p - a.row_lo) * a.row_words;
   for (uint64_t i = threadIdx.x; i < a.row_words; i += blockDim.x) dst[i] = src[i];
 }
@@ -1811,12 +2071,27 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   const uint32_t r0 = x * a.per_xcd + (b >> 3) * a.chunk;
   const uint32_t r_end = min(n, (x + 1) * a.per_xcd);
   if (r0 >= r_end) return;
-  const uint32_t nr = min(a.chunk, r_end - r0);
+  __shared__ uint32_t s_cnt[4];
+  uint32_t nr = min(a.chunk, r_end - r0);
+  // the block's rows that need a copy (in-place class rows are skipped), compacted in row order
+  const u64x2* src = nullptr;
+  u64x2* dst = nullptr;
   if (threadIdx.x < nr) {
     uint32_t pl, p;
     emit_row_of(a, r0 + threadIdx.x, pl, p);
-    s_src[threadIdx.x] = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
-    s_dst[threadIdx.x] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
+    src = reinterpret_cast<const u64x2*>(emit_src(a, pl, p));
+    dst = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
+  }
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t keep = __ballot(src != nullptr);
+  if (lane == 0) s_cnt[wv] = __popcll(keep);
+  __syncthreads();
+  uint32_t off = __popcll(keep & ((1ull << lane) - 1));
+  for (uint32_t x = 0; x < wv; x++) off += s_cnt[x];
+  nr = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  if (src) {
+    s_src[off] = src;
+    s_dst[off] = dst;
   }
   __syncthreads();
   const uint32_t n2 = uint32_t(a.row_words / 2), tot = nr * n2;
@@ -1848,7 +2123,8 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   if (r >= min(n, (x + 1) * a.per_xcd)) return;
   uint32_t pl, p;
   emit_row_of(a, r, pl, p);
-  const u64x2* si = reinterpret_cast<const u64x2*>(a.A[pl] + uint64_t(a.class_of[pl][a.pod_id[pl][p]]) * a.row_words);
+  const u64x2* si = reinterpret_cast<const u64x2*>(emit_src(a, pl, p));
+  if (!si) return;  // in-place class row: already written
   u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
   const uint32_t n2 = uint32_t(a.row_words / 2);
   for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS * UNROLL) {
@@ -2164,12 +2440,15 @@ struct cyc_ctx {
   DevBuf pod_peers_u;  // identity-set (IDOB) rows: the needed pod peers, one per distinct
                        // (namespace matcher, pod selector) of a direction (peer_ido maps every peer)
   DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
+  DevBuf plvt;      // LVT per pod (SelView::PLVT)
+  DevBuf ns_words;  // DWordNS per 64-pod word, then per 64-word chunk (sparse pod rows)
   bool dense_sel = false;  // k_selectors_dense (LVT fits)
   uint32_t Rp = 0, Ri = 0;
   uint32_t rp_off[3] = {0, 0, 0}, ri_off[3] = {0, 0, 0};  // per-direction sub-lists (ingress, egress)
   uint32_t rpu_off[3] = {0, 0, 0};  // sub-lists of pod_peers_u: one pod peer per distinct matcher
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
   DevBuf act[2], sel_list;
+  DevBuf arow[2];  // per identity: its first pod's row in the run's row range (in-place class rows)
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
   double act_targets[2] = {0, 0};  // mean namespace targets per active identity (range plan)
   // Diagnostic path selectors (cyc_set_option; results never change, the GPU tests force each path):
@@ -2192,6 +2471,12 @@ struct cyc_ctx {
                         // (config #2 0.077 -> 0.069 ms/step, profiles/r02_step_events_ab.txt)
   int pl_wave = 1;      // "pl_wave": PM-build class rows a wave per 64-word chunk where they fit (1),
                         // or a thread per (slot chunk, word) item (0)
+  int class_inplace = -1; // "class_inplace": fused-front class rows written straight into the output
+                          // planes (the first member pod's row), the emit copying only the others (1);
+                          // -1 = auto (inplace_ok)
+  int pr_group = -1;   // "pr_group": sparse pod-peer rows, pod peers per block (1..64; -1 = auto)
+  int sel_lazy = -1;    // "sel_lazy": selectors evaluated where used (1) or as the dense SELRES table
+                        // first (0); -1 = lazy on the fused front of PM builds
   int front_fused = 1;  // "front_fused": the front as block-range-fused launches on one stream
                         // (enq_front_fused), 0 = the two-branch DAG
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
@@ -2392,6 +2677,11 @@ static void prepare_device(cyc_ctx* c) {
       for (DReq& q : dr) q.key = (q.op != REQ_INVALID && q.key < kx.size() && kx[q.key] >= 0) ? uint32_t(kx[q.key]) : nk;
       upload(c->lvt, lvt);
       upload(c->dreqs, dr);
+      // the same table per pod (sparse pod-peer rows evaluate pod selectors on a wave of pods)
+      std::vector<uint32_t> plvt(uint64_t(nk + 1) * pb.P);
+      for (uint32_t kk = 0; kk <= nk; kk++)
+        for (uint32_t q = 0; q < pb.P; q++) plvt[uint64_t(kk) * pb.P + q] = lvt[uint64_t(kk) * pb.L + pb.pod_ls[q]];
+      upload(c->plvt, plvt);
     }
   }
   c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
@@ -2447,6 +2737,17 @@ static void prepare_device(cyc_ctx* c) {
         wi[pb.W + ch] = d;
       }
       upload(c->ip_words, wi);
+      // namespace range of every word's and chunk's pods (pod_rows_sparse_blk)
+      std::vector<DWordNS> nw(pb.W + NC, DWordNS{0xFFFFFFFFu, 0u, 0u, 0u});
+      for (uint32_t q = 0; q < pb.P; q++) {
+        for (DWordNS* x : {&nw[q / 64], &nw[pb.W + q / 4096]}) {
+          if (x->lo == 0xFFFFFFFFu) x->nsls = pb.pod_nsls[q];
+          else if (x->lo != pb.pod_ns[q] || x->hi != pb.pod_ns[q]) x->nsls = 0xFFFFFFFFu;
+          x->lo = std::min(x->lo, pb.pod_ns[q]);
+          x->hi = std::max(x->hi, pb.pod_ns[q]);
+        }
+      }
+      upload(c->ns_words, nw);
     }
     c->ido.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * c->ids[1].ns.size(), 16));
     c->idob.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * ((c->ids[1].ns.size() + 63) / 64) * 8, 16));
@@ -2502,6 +2803,40 @@ static uint32_t* ip_cnz(cyc_ctx* c) { return c->ip_rng.as<uint32_t>() + 4 * c->p
 
 static unsigned grid1(uint64_t n, unsigned block) { return unsigned(std::min<uint64_t>((n + block - 1) / block, 1u << 20)); }
 
+static bool front_fused_ok(const cyc_ctx* c);
+static bool ido_mode(const cyc_ctx* c);
+// Selectors evaluated where used (sel_at through LVT), not as the dense SELRES table: the fused
+// front of PM builds (its pod-peer rows and membership are the only selector users, and PM builds
+// are the ones whose label sets number ~ the pods).  The DAG path computes SELRES regardless.
+// PM builds' fused front: sparse pod-peer rows (pod_rows_sparse_blk, launch C) once the rows are
+// large (>= 2M pod-peer words: config #3u), else full rows a wave per (pod peer, word) in launch B,
+// which has the parallelism small problems need (config #2: 125k peer words, B + C 33 vs 52 us).
+// pr_group > 0 forces the sparse rows.
+static bool pod_sparse(const cyc_ctx* c) {
+  if (ido_mode(c)) return false;
+  const uint64_t Rp = c->rp_off[2] - c->rp_off[0];
+  return c->pr_group > 0 || Rp * c->pb.W >= (2ull << 20);
+}
+static bool lazy_sel(const cyc_ctx* c) {
+  if (!c->dense_sel || c->pb.may_err || c->sel_lazy == 0 || ido_mode(c) || !front_fused_ok(c)) return false;
+  if (!pod_sparse(c)) return false;  // the full pod-peer rows read the dense selector table
+  // auto: lazy once the dense table would take ~0.1 ms (>= 64M pairs; config #3u: 0.75G pairs,
+  // 1.1 ms; config #2 stays dense — its multi-requirement selectors cost more evaluated per use)
+  return c->sel_lazy == 1 || uint64_t(c->n_sel) * c->pb.L >= (64ull << 20);
+}
+static SelView sel_view(cyc_ctx* c) {
+  SelView v{};
+  v.selres = lazy_sel(c) ? nullptr : c->selres.as<uint8_t>();
+  v.L = c->pb.L;
+  v.sel_off = c->sel_off.as<uint32_t>();
+  v.req_vals = c->req_vals.as<uint32_t>();
+  v.LVT = c->lvt.as<uint32_t>();
+  v.dreqs = c->dreqs.as<DReq>();
+  v.PLVT = c->plvt.as<uint32_t>();
+  v.P = c->pb.P;
+  return v;
+}
+
 static MemberArgs member_args(cyc_ctx* c, int d) {
   Problem& pb = c->pb;
   DirDev& dd = c->dir[d];
@@ -2516,7 +2851,7 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   a.tns_lo = dd.tns_lo.as<uint32_t>();
   a.tns_hi = dd.tns_hi.as<uint32_t>();
   a.tgt = dd.tgt.as<DTarget>();
-  a.selres = c->selres.as<uint8_t>();
+  a.sv = sel_view(c);
   a.list_off = dd.list_off.as<uint32_t>();
   a.list = dd.list.as<uint32_t>();
   a.cnt = dd.cnt.as<uint32_t>();
@@ -2568,6 +2903,11 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
       }
     }
     std::sort(act.begin(), act.end());
+    {  // each active identity's first pod in the range: its plane row holds the class row in place
+      std::vector<uint32_t> ar(I.ns.size(), 0xFFFFFFFFu);
+      for (int64_t p = hi - 1; p >= lo; p--) ar[I.of_pod[size_t(p)]] = uint32_t(p - lo);
+      upload(c->arow[d], ar);
+    }
     std::vector<uint8_t> ns_needed(pb.strings.size(), 0);
     for (uint32_t i : act) ns_needed[I.ns[i]] = 1;
     for (const DTarget& t : pb.tgt[d])
@@ -2882,7 +3222,7 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // d_status (may be null): the status plane, copied by the emit's blocks.  Returns false if no
 // emit was launched (no rows in the range; the caller then copies the status plane itself).
 static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, int64_t lo, int64_t hi,
-                     uint8_t* d_status) {
+                     uint8_t* d_status, bool inplace = false) {
   Problem& pb = c->pb;
   const uint32_t K = pb.K, W = pb.W;
   if (hi <= lo || !K || !W) return false;
@@ -2901,6 +3241,7 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
     ea.pod_id[pl] = c->dir[pl].pod_id.as<uint32_t>();
     ea.class_of[pl] = c->dir[pl].class_of.as<uint32_t>();
     ea.A[pl] = c->dir[pl].A.as<uint64_t>();
+    ea.arow[pl] = inplace ? c->arow[pl].as<uint32_t>() : nullptr;
   }
   ea.out[0] = out_in;
   ea.out[1] = out_eg;
@@ -2951,7 +3292,20 @@ static bool front_fused_ok(const cyc_ctx* c) {
   return !(Rp && E) || (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= pb.P);
 }
 
-static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nullptr, hipEvent_t ev_rows = nullptr) {
+// In-place class rows: the fused front with both output planes given.
+// Auto (-1): when the rows' identities are >= 1/16 of the rows (PM builds: config #4 emit -8 %,
+// #3u -7 %); with few identities the rows saved are few while the class rows, scattered over the
+// planes, write slower (config #3: 2 % of the rows, net +1 %: profiles/r02_class_inplace_ab.txt).
+static bool inplace_ok(const cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg) {
+  if (!c->class_inplace || !d_in || !d_eg || !front_fused_ok(c)) return false;
+  const uint64_t rows = uint64_t(std::max<int64_t>(c->order_hi - c->order_lo, 1));
+  return c->class_inplace == 1 || uint64_t(c->n_act[0] + c->n_act[1]) * 16 >= 2 * rows;
+}
+
+// out_in / out_eg non-null: the class rows go straight into those planes (in-place class rows; the
+// emit must then be enqueued with inplace = true).
+static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nullptr, hipEvent_t ev_rows = nullptr,
+                            uint64_t* out_in = nullptr, uint64_t* out_eg = nullptr) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size()), E = c->dir[1].n, EW = (E + 63) / 64;
@@ -2963,7 +3317,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   // A: IP word spans | port table | slot words | selectors
   FrontA fa{};
   fa.fill_p = c->ip_rng.as<uint32_t>();
-  fa.fill_n = c->Ri ? pb.peers.size() * 4 : 0;  // the word spans and chunk masks (cnz needs no reset)
+  // the word spans and chunk masks of the IP rows and of PM builds' sparse pod rows (cnz needs no reset)
+  fa.fill_n = (c->Ri || (!ido_mode(c) && c->Rp)) ? pb.peers.size() * 4 : 0;
   fa.nb[0] = blocks((fa.fill_n + 255) / 256);
   fa.M = M;
   fa.D = D;
@@ -2989,7 +3344,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fa.LVT = c->lvt.as<uint32_t>();
   fa.selres = c->selres.as<uint8_t>();
   fa.sel_list = c->sel_list.as<uint32_t>();
-  fa.nb[3] = uint64_t(c->n_sel) * pb.L ? blocks(uint64_t(c->n_sel) * ((pb.L + 256 * SEL_LPT - 1) / (256 * SEL_LPT))) : 0u;
+  fa.nb[3] = uint64_t(c->n_sel) * pb.L && !lazy_sel(c) ? blocks(uint64_t(c->n_sel) * ((pb.L + 256 * SEL_LPT - 1) / (256 * SEL_LPT))) : 0u;
   // B: IP rows | pod-peer identity sets (both directions' adjacent sub-lists) | membership x 2
   FrontB fb{};
   const uint32_t i0 = c->ri_off[0], Ri = c->ri_off[2] - i0;
@@ -3019,14 +3374,34 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.idob = c->idob.as<uint64_t>() + uint64_t(u0) * EW;
   fb.nb[1] = (Rp && E) ? blocks((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4) : 0u;
   const bool ido = ido_mode(c);
-  if (!ido) {  // PM builds: pod-peer rows per pod, a wave per (pod peer, 64-pod word)
+  FrontC fc{};
+  if (!ido && !pod_sparse(c)) {  // PM builds, few pod-peer words: full rows, a wave per (pod peer, word)
     fb.pod_direct = 1;
     fb.Rp = Rp;
     fb.plist = c->pod_peers.as<uint32_t>() + c->rp_off[0];
     fb.pod_eid = c->dir[1].pod_id.as<uint32_t>();
     fb.nb[1] = (Rp && E) ? blocks((uint64_t(Rp) * W + 3) / 4) : 0u;
+  } else if (!ido) {  // PM builds: sparse pod-peer rows in launch C (k_front_c)
+    fb.nb[1] = 0;
+    fc.Rp = Rp;
+    fc.P = P;
+    fc.W = W;
+    fc.plist = c->pod_peers.as<uint32_t>() + c->rp_off[0];
+    fc.peers = c->peers.as<DPeer>();
+    fc.pod_ns = c->pod_ns.as<uint32_t>();
+    fc.pod_nsls = c->pod_nsls.as<uint32_t>();
+    fc.pod_ls = c->pod_ls.as<uint32_t>();
+    fc.nsw = c->ns_words.as<DWordNS>();
+    fc.sv = sel_view(c);
+    fc.PM = c->PM.as<uint64_t>();
+    fc.rng = c->ip_rng.as<uint32_t>();
+    fc.cnz = ip_cnz(c);
+    // a wave per chunk over groups of 8 peers once that fills the chip (>= 64k peer chunks:
+    // config #3u 2.6 vs 3.2 ms), else the 4 waves of a block share each chunk (config #2)
+    const uint64_t cb = ((W + 63) / 64 + 3) / 4;
+    fc.pr_grp = c->pr_group > 0 ? uint32_t(c->pr_group) : (uint64_t(Rp) * ((W + 63) / 64) >= 65536 ? 8u : 1u);
+    fc.nb[2] = (Rp && E) ? blocks((uint64_t(Rp) + fc.pr_grp - 1) / fc.pr_grp * cb) : 0u;
   }
-  FrontC fc{};
   FrontRows fd{}, fe{};
   size_t lds = 0;
   for (int d = 0; d < 2; d++) {
@@ -3039,8 +3414,13 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fc.nb[d] = na ? blocks((uint64_t(na) + 255) / 256) : 0u;
     if (!na) continue;
     fd.ra[d] = row_args(c, d);  // its blocks empty the direction's hash table for the next run
+    if (out_in && out_eg) {
+      fd.ra[d].A = d == 0 ? out_in : out_eg;
+      fd.ra[d].arow = c->arow[d].as<uint32_t>();
+    }
     if (!ido) {  // PM builds: launch D (k_front_d_pm) is the class rows from flattened peer lists
       fd.nb[d] = pl_blocks(c, d);
+      fd.ra[d].pod_sparse = pod_sparse(c);  // pod rows from pod_rows_sparse_blk (launch C)
       continue;
     }
     fe.ra[d] = fd.ra[d];
@@ -3063,7 +3443,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (!fits) return false;
   if (ga) k_front_a<<<unsigned(ga), 256, 0, st>>>(fa);
   if (gb) k_front_b<<<unsigned(gb), 256, 0, st>>>(fb);
-  if (fc.nb[0] + fc.nb[1]) k_front_c<<<fc.nb[0] + fc.nb[1], 256, 0, st>>>(fc);
+  if (fc.nb[0] + fc.nb[1] + fc.nb[2]) k_front_c<<<fc.nb[0] + fc.nb[1] + fc.nb[2], 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
     if (fd.nb[0] + fd.nb[1] && pl_wave_ok(c)) k_front_d_pm<true><<<fd.nb[0] + fd.nb[1], PL_THREADS, 0, st>>>(fd);
@@ -3085,7 +3465,9 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
                              int64_t hi) {
   Problem& pb = c->pb;
   HIPCHK(hipEventRecord(c->ev[0], st));
-  if (!(front_fused_ok(c) && enq_front_fused(c, st, c->ev[1], c->ev[2]))) {
+  const bool ip = inplace_ok(c, d_in, d_eg);
+  const bool fused = front_fused_ok(c) && enq_front_fused(c, st, c->ev[1], c->ev[2], ip ? d_in : nullptr, ip ? d_eg : nullptr);
+  if (!fused) {
     enq_common(c, st);
     for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st);
     for (int d = 0; d < 2; d++) enq_member(c, d, st);
@@ -3093,7 +3475,7 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
     for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
     HIPCHK(hipEventRecord(c->ev[2], st));
   }
-  const bool status_done = enq_emit(c, st, d_in, d_eg, lo, hi, d_status);
+  const bool status_done = enq_emit(c, st, d_in, d_eg, lo, hi, d_status, ip && fused);
   HIPCHK(hipEventRecord(c->ev[3], st));
   if (!status_done && d_status && uint64_t(pb.P) * pb.K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
@@ -3106,8 +3488,9 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
 static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStream_t st3, uint64_t* d_in, uint64_t* d_eg,
                              uint8_t* d_status, int64_t lo, int64_t hi) {
   Problem& pb = c->pb;
-  if (front_fused_ok(c) && enq_front_fused(c, st)) {
-    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status)) return;
+  const bool ip = inplace_ok(c, d_in, d_eg);
+  if (front_fused_ok(c) && enq_front_fused(c, st, nullptr, nullptr, ip ? d_in : nullptr, ip ? d_eg : nullptr)) {
+    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status, ip)) return;
   } else {
     HIPCHK(hipEventRecord(c->fork_ev, st));
     HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
@@ -3709,6 +4092,9 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "class_rpb") range(1, 64), c->class_rpb_opt = value;
     else if (n == "ip_group") range(1, 64), c->ip_group = uint32_t(value);
     else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
+    else if (n == "sel_lazy") range(-1, 1), c->sel_lazy = int(value);
+    else if (n == "pr_group") range(-1, 64), c->pr_group = int(value == 0 ? -1 : value);
+    else if (n == "class_inplace") range(-1, 1), c->class_inplace = int(value);
     else if (n == "step_events") range(0, 1), c->step_events = int(value);
     else return fail(c, CYC_ERR_ARG, "unknown option " + n);
     drop_graph(c);
@@ -3726,6 +4112,13 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "ip_group") *value = c->ip_group;
   else if (n == "pl_wave") *value = c->pl_wave;
+  else if (n == "sel_lazy") *value = c->sel_lazy;
+  else if (n == "pr_group") *value = c->pr_group;
+  else if (n == "class_inplace") *value = c->class_inplace;
+  else if (n == "class_inplace_active") {
+    if (!c->prepared || c->order_lo < 0) return fail(c, CYC_ERR_ARG, "class_inplace_active: run a probe first");
+    *value = inplace_ok(c, reinterpret_cast<const uint64_t*>(16), reinterpret_cast<const uint64_t*>(16)) ? 1 : 0;
+  }
   else if (n == "step_events") *value = c->step_events;
   else if (n == "pl_wave_active") {
     if (!c->prepared) return fail(c, CYC_ERR_ARG, "pl_wave_active: call cyc_probe_prepare first");

@@ -183,6 +183,16 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  *                 events cyc_last_timings reads (they idle the GPU ~9 us between steps)
  *   "pl_wave"     1 (default) / 0: materialised-row class rows a wave per 64-word chunk where they
  *                 fit (<= 4 job slots and descriptors), or a thread per (slot chunk, word) item
+ *   "pr_group"    -1 (default: auto) / 1..64: the fused front's sparse pod-peer rows (PM builds) with
+ *                 a block per pod peer (1) or a wave per 64-word chunk over groups of that many peers
+ *   "class_inplace" -1 (default: auto) / 0 / 1: on the fused front, each class's rows are written
+ *                 straight into the output planes at its first member pod's row and the emit copies
+ *                 them to the class's other pods (1), or they go to a buffer of their own the emit
+ *                 copies from (0); auto = 1 when the rows' identities are >= 1/16 of the rows
+ *                 ("class_inplace_active" reports the choice of the last run's row range)
+ *   "sel_lazy"    -1 (default: auto) / 0 / 1: on the fused front of PM builds, label selectors are
+ *                 evaluated where membership and pod-peer rows use them (1) instead of as the dense
+ *                 selector x label-set table first (0); auto = 1 once that table has >= 64M pairs
  * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
  * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
  * uses (0 or 1). */

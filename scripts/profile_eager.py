@@ -2,6 +2,7 @@
 (per-kernel durations without the two-branch graph overlap).
 
     rocprofv3 --kernel-trace --stats -d OUT -o run -- python scripts/profile_eager.py config3 20 [NAME=VALUE ...]
+(CYC_SHARD=r/N: rank r's row shard of an N-way run.)
 """
 import json
 import os
@@ -20,14 +21,21 @@ data = synth.CONFIGS[name]()
 eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
 sh = eng.prepare(data["probes"])
 P, K, W = sh["pods"], sh["slots"], sh["words"]
-d_in = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
-d_eg = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
+# CYC_SHARD=r/N: rank r's row shard of an N-way run (shard.row_range), as bench.py --gpus N runs it
+lo, hi = 0, P
+if os.environ.get("CYC_SHARD"):
+    from cyclonus_amd.shard import row_range
+
+    r_, n_ = (int(x) for x in os.environ["CYC_SHARD"].split("/"))
+    lo, hi = row_range(P, n_, r_)
+d_in = torch.empty((hi - lo, K, W), dtype=torch.int64, device="cuda")
+d_eg = torch.empty((hi - lo, K, W), dtype=torch.int64, device="cuda")
 d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 eng.set_option("graphs", 0)
 for k, v in opts:
     eng.set_option(k, int(v))
 for _ in range(n):
-    eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), st)
+    eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), st, lo, hi)
 torch.cuda.synchronize()
 print(json.dumps({"config": name, "steps": n, "shape": sh, "timings_last": eng.timings(), "classes": eng.classes()}))

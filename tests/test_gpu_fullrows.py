@@ -69,3 +69,8 @@ def test_config3_full_rows():
 
 def test_config4_full_rows():
     _check("config4", {}, [(1, 0), (4, 3)])
+
+
+def test_config3u_full_rows():
+    """Class explosion: config #3's shape with every pod identity distinct (synth.config3u)."""
+    _check("config3u", {}, [(1, 0)])

@@ -237,6 +237,7 @@ def test_graph_and_eager_paths_agree(gpu):
             eng.set_option("member_wave", mw)
             eng.set_option("pod_rows", pod_rows)
             eng.set_option("ip_group", grp)
+            eng.set_option("class_inplace", int(graphs != 2))  # class rows in the planes or in their own buffer
             d_in = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_eg = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_st = torch.zeros((P, K), dtype=torch.uint8, device="cuda")
@@ -310,7 +311,8 @@ def test_ip_interval_words(gpu, seed):
 
 def test_pm_class_rows_wave_and_items(gpu):
     """PM-build class rows (pod_words = 0) a wave per 64-word chunk (pl_wave = 1: <= 4 slots and
-    descriptors) and a thread per item (pl_wave = 0) against the oracle: IP-interval problems (IP
+    descriptors) and a thread per item (pl_wave = 0), over sparse pod-peer rows built by either block
+    shape with lazy or dense selectors, against the oracle: IP-interval problems (IP
     rows with skipped and straddling chunks) and random problems, which include classes with more
     list entries than the LDS part holds only at sizes the oracle cannot check — those run through
     tests/test_gpu_fullrows.py."""
@@ -330,6 +332,14 @@ def test_pm_class_rows_wave_and_items(gpu):
             eng.set_option("pl_wave", wave)
             assert_same(want, eng.run_host(), f"problem {n} pl_wave={wave}")
         eng.set_option("pl_wave", 1)
+        # sparse pod-peer rows a block per peer or a wave per chunk over peer groups, selectors
+        # evaluated where used or as the dense table first
+        for grp, lazy in ((1, 1), (8, 0), (3, 1), (64, -1)):
+            eng.set_option("pr_group", grp)
+            eng.set_option("sel_lazy", lazy)
+            assert_same(want, eng.run_host(), f"problem {n} pr_group={grp} sel_lazy={lazy}")
+        eng.set_option("pr_group", -1)
+        eng.set_option("sel_lazy", -1)
         seen_wave += eng.get_option("pl_wave_active")
     assert seen_wave >= 10
 
@@ -526,7 +536,8 @@ def test_launch_modes_and_knobs(gpu):
     assert eng.get_option("front_fused_active") == int(fused)
     assert eng.get_option("launch") == (2 if fused else 1)
     for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("ip_group", 3), ("graphs", 1), ("graphs", -1),
-                    ("step_events", 1), ("step_events", 0)):
+                    ("step_events", 1), ("step_events", 0), ("pr_group", 5), ("pr_group", -1), ("sel_lazy", 1),
+                    ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1)):
         eng.set_option(name, v)
         assert eng.get_option(name) == v
         assert_same(want, eng.run_host(), f"{name}={v}")
@@ -546,7 +557,8 @@ def test_launch_modes_and_knobs(gpu):
     assert_same(want, eng.run_host(), "DAG graph")
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
-    for name, v in (("class_rpb", 0), ("class_rpb", 65), ("graphs", 3), ("emit_variant", 1), ("nope", 0)):
+    for name, v in (("class_rpb", 0), ("class_rpb", 65), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
+                    ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
     # a build that may panic keeps the graph path (the panic walk needs the ordered peer rows)
