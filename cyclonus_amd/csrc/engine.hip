@@ -1106,7 +1106,7 @@ constexpr uint32_t IDO_LDS_BYTES = 48 * 1024;  // staged identity sets per class
 // one ballot per peer -> IDOB (no-panic runs only).
 constexpr uint32_t PB_GROUP = 8;
 __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
-                                                   const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres, uint32_t L,
+                                                   const DPeer* __restrict__ peers, const SelView& sv,
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                    const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t bid_, uint32_t nblk_) {
   const uint32_t wv = bid_ * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1122,7 +1122,10 @@ __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t 
     const uint32_t p = g * PB_GROUP + x;
     if (p >= Rp) break;
     const DPeer pr = peers[pod_peers[p]];
-    const bool m = live && pod_peer_outcome(pr, selres, L, ns, nsls, ls) == 1;
+    bool m = live;  // podpeermatcher.go:21-28 (no panic on this path: outcomes are 0 / 1)
+    if (m && pr.nskind == 0) m = ns == pr.nsval;
+    else if (m && pr.nskind == 2) m = sel_at(sv, pr.nsval, nsls) == 1;
+    if (m && pr.podsel != CYC_ALL) m = sel_at(sv, pr.podsel, ls) == 1;
     const uint64_t b = __ballot(m);
     if (lane == x) mine = b;
   }
@@ -1132,7 +1135,12 @@ __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t 
 __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
                                                    const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres, uint32_t L,
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
-                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob) { peer_bits_blk(Rp, E, EW, pod_peers, peers, selres, L, id_ns, id_nsls, id_ls, idob, blockIdx.x, gridDim.x); }
+                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob) {
+  SelView sv{};
+  sv.selres = selres;
+  sv.L = L;
+  peer_bits_blk(Rp, E, EW, pod_peers, peers, sv, id_ns, id_nsls, id_ls, idob, blockIdx.x, gridDim.x);
+}
 
 // Per class representative and NB index (ingress: job slot, egress: job descriptor): the set of
 // egress identities its targets' pod / all / ports-for-all peers allow on that port (target.go:29-36
@@ -1881,6 +1889,7 @@ struct FrontB {
   uint32_t ip_grp;      // IP rows: peers per wave
   uint32_t pod_direct;  // PM builds with few pod-peer words: segment 1 = full pod-peer rows per pod
                         // (pod_rows_direct_blk), else identity sets (IDO)
+  SelView sv;           // IDO identity sets: selector outcomes (SELRES or evaluated where used)
   uint32_t Rp;
   const uint32_t *plist, *pod_eid;
   uint32_t M, D;
@@ -1911,7 +1920,7 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
     if (f.pod_direct)
       return pod_rows_direct_blk<false>(f.Rp, f.P, f.W, f.plist, f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls, f.id_ls,
                                         f.PM, nullptr, b, f.nb[1]);
-    return peer_bits_blk(f.Ru, f.E, f.EW, f.pod_peers_u, f.peers, f.selres, f.L, f.id_ns, f.id_nsls, f.id_ls, f.idob, b, f.nb[1]);
+    return peer_bits_blk(f.Ru, f.E, f.EW, f.pod_peers_u, f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob, b, f.nb[1]);
   }
   b -= f.nb[1];
 #pragma unroll
@@ -1926,14 +1935,52 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   if (b < f.nb[4]) portbits_blk(f.M, f.D, f.portok, f.portbits, b);  // for the egress class rows
 }
 
+// Pod-peer rows from posting lists: a pod selector that is ONE requirement `k = v` or `k in (v0,
+// v1)` (matchLabels, the common shape) matches exactly the pods listed under (k, v) in the host's
+// label postings, so its row is built from those few pods instead of testing every pod: block =
+// one such peer; the row is assembled in LDS PR_POST_WORDS words at a time (each pod of the
+// postings whose namespace the peer's namespace matcher accepts sets its bit with an LDS atomic
+// OR), then stored chunk-dense with span and chunk masks (pod_chunk_store).  Cost ~ postings +
+// nonzero chunks, not pods.
+constexpr uint32_t PR_POST_WORDS = 1024;  // 16 chunks of the row per LDS pass (8 KB)
+__device__ __forceinline__ void pod_rows_post_blk(uint32_t P, uint32_t W, const uint32_t* __restrict__ plist,
+                                                  const DPeer* __restrict__ peers, const SelView& sv,
+                                                  const uint4* __restrict__ req_post, const uint32_t* __restrict__ post_pods,
+                                                  const uint32_t* __restrict__ pod_ns, const uint32_t* __restrict__ pod_nsls,
+                                                  uint64_t* __restrict__ PM, uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz,
+                                                  uint32_t bid_) {
+  __shared__ unsigned long long s_row[PR_POST_WORDS];
+  const uint32_t j = plist[bid_];
+  const DPeer pr = peers[j];
+  const uint4 pp = req_post[sv.sel_off[pr.podsel]];  // (offset, count) of value 0, then of value 1
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, chunks = (W + 63) / 64;
+  for (uint32_t w0 = 0; w0 < W; w0 += PR_POST_WORDS) {
+    for (uint32_t x = threadIdx.x; x < PR_POST_WORDS; x += blockDim.x) s_row[x] = 0;
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < pp.y + pp.w; e += blockDim.x) {
+      const uint32_t q = post_pods[e < pp.y ? pp.x + e : pp.z + (e - pp.y)];
+      const uint32_t w = q >> 6;
+      if (w < w0 || w >= w0 + PR_POST_WORDS) continue;
+      bool ok = pr.nskind == 1;  // podpeermatcher.go:21-28: the namespace matcher
+      if (pr.nskind == 0) ok = pod_ns[q] == pr.nsval;
+      else if (pr.nskind == 2) ok = sel_at(sv, pr.nsval, pod_nsls[q]) == 1;
+      if (ok) atomicOr(&s_row[w - w0], 1ull << (q & 63));
+    }
+    __syncthreads();
+    for (uint32_t c = w0 / 64 + wave; c < min(chunks, (w0 + PR_POST_WORDS) / 64); c += blockDim.x >> 6)
+      pod_chunk_store(j, c, W, lane, c * 64 + lane < W ? s_row[c * 64 + lane - w0] : 0ull, PM, rng, cnz);
+    __syncthreads();  // s_row is cleared for the next pass
+  }
+}
+
 // Launch C also carries PM builds' sparse pod-peer rows (they need only launch A's selector table
 // and precede the class rows): the light class election keeps them off launch B, whose IP rows and
 // membership would otherwise run at the pod rows' register budget (occupancy 8 -> 5-7).
 struct FrontC {
-  uint32_t nb[3];
+  uint32_t nb[4];
   MemberArgs ma[2];
   uint32_t* class_of[2];
-  // sparse pod-peer rows (pod_rows_sparse_blk)
+  // sparse pod-peer rows (pod_rows_sparse_blk over plist, then pod_rows_post_blk over plist_post)
   uint32_t Rp, P, W, pr_grp;
   const uint32_t* plist;
   const DPeer* peers;
@@ -1942,6 +1989,9 @@ struct FrontC {
   const DWordNS* nsw;  // per word, then per chunk: namespace ranges
   uint64_t* PM;
   uint32_t *rng, *cnz;
+  const uint32_t* plist_post;  // pod peers whose rows come from label postings (pod_rows_post_blk)
+  const uint4* req_post;
+  const uint32_t* post_pods;
 };
 __global__ __launch_bounds__(256) void k_front_c(FrontC f) {
   uint32_t b = blockIdx.x;
@@ -1952,7 +2002,11 @@ __global__ __launch_bounds__(256) void k_front_c(FrontC f) {
 #ifdef CYC_DIAG_NO_PODROWS  // timing diagnostic only (rows stay empty: results are wrong)
   return;
 #endif
-  pod_rows_sparse_blk(f.Rp, f.P, f.W, f.plist, f.peers, f.sv, f.pod_ns, f.pod_nsls, f.pod_ls, f.nsw, f.PM, f.rng, f.cnz, f.pr_grp, b);
+  if (b < f.nb[2])
+    return pod_rows_sparse_blk(f.Rp, f.P, f.W, f.plist, f.peers, f.sv, f.pod_ns, f.pod_nsls, f.pod_ls, f.nsw, f.PM, f.rng, f.cnz,
+                               f.pr_grp, b);
+  b -= f.nb[2];
+  pod_rows_post_blk(f.P, f.W, f.plist_post, f.peers, f.sv, f.req_post, f.post_pods, f.pod_ns, f.pod_nsls, f.PM, f.rng, f.cnz, b);
 }
 
 struct FrontRows {
@@ -2441,6 +2495,10 @@ struct cyc_ctx {
                        // (namespace matcher, pod selector) of a direction (peer_ido maps every peer)
   DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
   DevBuf plvt;      // LVT per pod (SelView::PLVT)
+  DevBuf req_post, post_pods;  // label postings: per requirement (offset, count) x 2 values; pod lists
+  std::vector<uint8_t> req_post_ok;  // the requirement's pods are its postings (EQ, IN of <= 2 values)
+  DevBuf pp_scan, pp_post;     // sparse pod rows: pod peers scanned per word / built from postings
+  uint32_t n_scan = 0, n_post = 0;
   DevBuf ns_words;  // DWordNS per 64-pod word, then per 64-word chunk (sparse pod rows)
   bool dense_sel = false;  // k_selectors_dense (LVT fits)
   uint32_t Rp = 0, Ri = 0;
@@ -2682,6 +2740,38 @@ static void prepare_device(cyc_ctx* c) {
       for (uint32_t kk = 0; kk <= nk; kk++)
         for (uint32_t q = 0; q < pb.P; q++) plvt[uint64_t(kk) * pb.P + q] = lvt[uint64_t(kk) * pb.L + pb.pod_ls[q]];
       upload(c->plvt, plvt);
+      // label postings: the pods under each (dense key, value) of their own labels, and per EQ / IN
+      // (<= 2 values) requirement the postings of its values (pod_rows_post_blk)
+      std::vector<std::pair<uint64_t, uint32_t>> kv;
+      for (uint32_t q = 0; q < pb.P; q++) {
+        const uint32_t l = pb.pod_ls[q];
+        for (uint32_t x = pb.ls_off[l]; x < pb.ls_off[l + 1]; x++) kv.push_back({(uint64_t(kx[pb.ls_key[x]]) << 32) | pb.ls_val[x], q});
+      }
+      std::sort(kv.begin(), kv.end());
+      std::vector<uint32_t> pods(kv.size());
+      for (size_t i = 0; i < kv.size(); i++) pods[i] = kv[i].second;
+      auto range = [&](uint32_t key, uint32_t v) {
+        const uint64_t k = (uint64_t(key) << 32) | v;
+        auto lo = std::lower_bound(kv.begin(), kv.end(), std::make_pair(k, 0u));
+        auto hi = std::lower_bound(kv.begin(), kv.end(), std::make_pair(k + 1, 0u));
+        return std::make_pair(uint32_t(lo - kv.begin()), uint32_t(hi - lo));
+      };
+      std::vector<uint4> rp(dr.size(), uint4{0, 0, 0, 0});
+      c->req_post_ok.assign(dr.size(), 0);
+      for (size_t r = 0; r < dr.size(); r++) {
+        const DReq& q = dr[r];
+        if (q.key >= nk || !(q.op == REQ_EQ || (q.op == REQ_IN && q.vcnt >= 1 && q.vcnt <= 2))) continue;
+        const auto a = range(q.key, pb.req_vals[q.voff]);
+        rp[r] = uint4{a.first, a.second, 0, 0};
+        if (q.op == REQ_IN && q.vcnt == 2 && pb.req_vals[q.voff + 1] != pb.req_vals[q.voff]) {
+          const auto b = range(q.key, pb.req_vals[q.voff + 1]);
+          rp[r].z = b.first;
+          rp[r].w = b.second;
+        }
+        c->req_post_ok[r] = 1;
+      }
+      upload(c->req_post, rp);
+      upload(c->post_pods, pods);
     }
   }
   c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
@@ -2818,11 +2908,13 @@ static bool pod_sparse(const cyc_ctx* c) {
   return c->pr_group > 0 || Rp * c->pb.W >= (2ull << 20);
 }
 static bool lazy_sel(const cyc_ctx* c) {
-  if (!c->dense_sel || c->pb.may_err || c->sel_lazy == 0 || ido_mode(c) || !front_fused_ok(c)) return false;
-  if (!pod_sparse(c)) return false;  // the full pod-peer rows read the dense selector table
+  if (!c->dense_sel || c->pb.may_err || c->sel_lazy == 0 || !front_fused_ok(c)) return false;
+  if (!ido_mode(c) && !pod_sparse(c)) return false;  // the full pod-peer rows read the dense selector table
   // auto: lazy once the dense table would take ~0.1 ms (>= 64M pairs; config #3u: 0.75G pairs,
   // 1.1 ms; config #2 stays dense — its multi-requirement selectors cost more evaluated per use)
-  return c->sel_lazy == 1 || uint64_t(c->n_sel) * c->pb.L >= (64ull << 20);
+  // IDO builds always: their identity sets and membership evaluate fewer pairs than the table
+  // holds (config #3: A + B 118 -> 111 us; its N = 8 shard 35 -> 31 us, profiles/r02_sel_lazy_ab.txt)
+  return c->sel_lazy == 1 || ido_mode(c) || uint64_t(c->n_sel) * c->pb.L >= (64ull << 20);
 }
 static SelView sel_view(cyc_ctx* c) {
   SelView v{};
@@ -2943,6 +3035,20 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   for (uint32_t i = 0; i < pb.S; i++)
     if (sel_needed[i]) sl.push_back(i);
   c->n_sel = uint32_t(sl.size());
+  {  // sparse pod rows: peers whose pod selector is one posting requirement are built from postings
+    std::vector<uint32_t> scan, post;
+    for (uint32_t j : c->plan.pod_peers) {
+      if (!peer_needed[j]) continue;
+      const DPeer& pr = pb.peers[j];
+      const bool one = pr.podsel != CYC_ALL && pb.sel_off[pr.podsel + 1] - pb.sel_off[pr.podsel] == 1;
+      if (one && c->dense_sel && !c->req_post_ok.empty() && c->req_post_ok[pb.sel_off[pr.podsel]]) post.push_back(j);
+      else scan.push_back(j);
+    }
+    c->n_scan = uint32_t(scan.size());
+    c->n_post = uint32_t(post.size());
+    upload(c->pp_scan, scan);
+    upload(c->pp_post, post);
+  }
   upload(c->sel_list, sl);
   std::vector<uint32_t> pp, ip;
   std::vector<DIPTest> tests;
@@ -3372,6 +3478,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.id_nsls = c->id_nsls.as<uint32_t>();
   fb.id_ls = c->dir[1].id_ls.as<uint32_t>();
   fb.idob = c->idob.as<uint64_t>() + uint64_t(u0) * EW;
+  fb.sv = sel_view(c);
   fb.nb[1] = (Rp && E) ? blocks((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4) : 0u;
   const bool ido = ido_mode(c);
   FrontC fc{};
@@ -3383,10 +3490,13 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fb.nb[1] = (Rp && E) ? blocks((uint64_t(Rp) * W + 3) / 4) : 0u;
   } else if (!ido) {  // PM builds: sparse pod-peer rows in launch C (k_front_c)
     fb.nb[1] = 0;
-    fc.Rp = Rp;
+    fc.Rp = c->n_scan;
     fc.P = P;
     fc.W = W;
-    fc.plist = c->pod_peers.as<uint32_t>() + c->rp_off[0];
+    fc.plist = c->pp_scan.as<uint32_t>();
+    fc.plist_post = c->pp_post.as<uint32_t>();
+    fc.req_post = c->req_post.as<uint4>();
+    fc.post_pods = c->post_pods.as<uint32_t>();
     fc.peers = c->peers.as<DPeer>();
     fc.pod_ns = c->pod_ns.as<uint32_t>();
     fc.pod_nsls = c->pod_nsls.as<uint32_t>();
@@ -3399,8 +3509,9 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     // a wave per chunk over groups of 8 peers once that fills the chip (>= 64k peer chunks:
     // config #3u 2.6 vs 3.2 ms), else the 4 waves of a block share each chunk (config #2)
     const uint64_t cb = ((W + 63) / 64 + 3) / 4;
-    fc.pr_grp = c->pr_group > 0 ? uint32_t(c->pr_group) : (uint64_t(Rp) * ((W + 63) / 64) >= 65536 ? 8u : 1u);
-    fc.nb[2] = (Rp && E) ? blocks((uint64_t(Rp) + fc.pr_grp - 1) / fc.pr_grp * cb) : 0u;
+    fc.pr_grp = c->pr_group > 0 ? uint32_t(c->pr_group) : (uint64_t(fc.Rp) * ((W + 63) / 64) >= 65536 ? 8u : 1u);
+    fc.nb[2] = (fc.Rp && E) ? blocks((uint64_t(fc.Rp) + fc.pr_grp - 1) / fc.pr_grp * cb) : 0u;
+    fc.nb[3] = E ? c->n_post : 0u;  // a block per posting-built peer
   }
   FrontRows fd{}, fe{};
   size_t lds = 0;
@@ -3443,7 +3554,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (!fits) return false;
   if (ga) k_front_a<<<unsigned(ga), 256, 0, st>>>(fa);
   if (gb) k_front_b<<<unsigned(gb), 256, 0, st>>>(fb);
-  if (fc.nb[0] + fc.nb[1] + fc.nb[2]) k_front_c<<<fc.nb[0] + fc.nb[1] + fc.nb[2], 256, 0, st>>>(fc);
+  if (fc.nb[0] + fc.nb[1] + fc.nb[2] + fc.nb[3]) k_front_c<<<fc.nb[0] + fc.nb[1] + fc.nb[2] + fc.nb[3], 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
     if (fd.nb[0] + fd.nb[1] && pl_wave_ok(c)) k_front_d_pm<true><<<fd.nb[0] + fd.nb[1], PL_THREADS, 0, st>>>(fd);

@@ -190,9 +190,10 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  *                 them to the class's other pods (1), or they go to a buffer of their own the emit
  *                 copies from (0); auto = 1 when the rows' identities are >= 1/16 of the rows
  *                 ("class_inplace_active" reports the choice of the last run's row range)
- *   "sel_lazy"    -1 (default: auto) / 0 / 1: on the fused front of PM builds, label selectors are
- *                 evaluated where membership and pod-peer rows use them (1) instead of as the dense
- *                 selector x label-set table first (0); auto = 1 once that table has >= 64M pairs
+ *   "sel_lazy"    -1 (default: auto) / 0 / 1: on the fused front, label selectors are evaluated where
+ *                 membership and pod-peer rows / identity sets use them (1) instead of as the dense
+ *                 selector x label-set table first (0); auto = 1 for identity-set builds and once
+ *                 that table has >= 64M pairs
  * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
  * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
  * uses (0 or 1). */
