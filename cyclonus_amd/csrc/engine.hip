@@ -1146,11 +1146,18 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
 // egress identities its targets' pod / all / ports-for-all peers allow on that port (target.go:29-36
 // is an OR over peers; without a panic its order only matters for early exit).  One wave per
 // (representative, NB index), lanes over 64-identity words.
+// The class's peers are first flattened, in target order, into a per-wave LDS list (targets 64 at
+// a time, a wave prefix sum over their peer counts), so the walk loads CI_BATCH peers' fields and
+// identity-set words at once — one chain of dependent loads per batch instead of per peer (the
+// walk dominates this launch on row shards, where few classes leave the chip mostly idle).
+// Classes with more than CI_LDS peers walk the targets directly.
+constexpr uint32_t CI_LDS = 128, CI_BATCH = 4;
 template <bool EGRESS, int G>
 __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
+  __shared__ uint32_t s_j[4][CI_LDS];
   ht_clear_slice(a, bid_, nblk_);
   // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
-  const uint32_t wv = bid_ * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t wi = threadIdx.x >> 6, wv = bid_ * 4 + wi, lane = threadIdx.x & 63;
   const uint32_t nbc = (a.NB + G - 1) / G;
   const uint32_t r = wv / nbc, nb0 = (wv % nbc) * G;
   if (r >= *a.rep_cnt + 1u) return;
@@ -1167,26 +1174,77 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
   }
   const uint32_t n = a.cnt[i];
   const uint32_t* lst = a.list + a.list_off[i];
+  uint32_t* sj = s_j[wi];
+  uint32_t m = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += 64) {
+    uint32_t poff = 0, pc = 0;
+    if (t0 + lane < n) {
+      const DTarget tg = a.tgt[lst[t0 + lane]];
+      poff = tg.poff;
+      pc = tg.pcnt;
+    }
+    uint32_t x = pc;  // inclusive prefix sum over the wave
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    const uint32_t base = m + x - pc;
+    for (uint32_t k = 0; k < pc && base + k < CI_LDS; k++) sj[base + k] = poff + k;
+    m += __shfl(x, 63);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the list is read back by other lanes
+  const bool flat = m <= CI_LDS;
   for (uint32_t ew0 = 0; ew0 < a.EW; ew0 += 64) {
     const uint32_t ew = ew0 + lane;
     uint64_t b[G];
 #pragma unroll
     for (uint32_t x = 0; x < uint32_t(G); x++) b[x] = (n == 0 && du[x] >= 0) ? ~0ull : 0ull;  // no target: allowed (policy.go:158-160)
-    for (uint32_t tj = 0; tj < n; tj++) {
-      const DTarget tg = a.tgt[lst[tj]];
-      for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
-        const DPeer pr = a.peers[j];
-        if (pr.kind == 3) continue;  // IP peers: per pod word, in the class rows
-        const uint8_t* pok = a.portok + uint64_t(pr.port) * a.D;
-        if (pr.kind == 0) {  // AllPeersMatcher
+    if (flat) {
+      // no panic on this path: the OR over peers is order-free (AllPeersMatcher: every valid cell)
+      for (uint32_t x0 = 0; x0 < m; x0 += CI_BATCH) {
+        uint32_t kind[CI_BATCH], port[CI_BATCH], pid[CI_BATCH];
 #pragma unroll
-          for (uint32_t x = 0; x < uint32_t(G); x++) b[x] = du[x] >= 0 ? ~0ull : 0ull;
-          break;
+        for (uint32_t u = 0; u < CI_BATCH; u++) {
+          kind[u] = 3;
+          port[u] = 0;
+          pid[u] = 0;
+          if (x0 + u < m) {
+            const uint32_t j = __builtin_amdgcn_readfirstlane(sj[x0 + u]);
+            kind[u] = a.peers[j].kind;
+            port[u] = a.peers[j].port;
+            pid[u] = a.peer_ido[j];
+          }
         }
-        const uint64_t v = pr.kind == 1 ? ~0ull : (ew < a.EW ? a.IDOB[uint64_t(a.peer_ido[j]) * a.EW + ew] : 0ull);
+        uint64_t v[CI_BATCH];
 #pragma unroll
-        for (uint32_t x = 0; x < uint32_t(G); x++)
-          if (du[x] >= 0 && pok[du[x]]) b[x] |= v;  // PortsForAllPeers / pod peer on an allowed port
+        for (uint32_t u = 0; u < CI_BATCH; u++)
+          v[u] = kind[u] == 0 || kind[u] == 1 ? ~0ull : (kind[u] == 2 && ew < a.EW ? a.IDOB[uint64_t(pid[u]) * a.EW + ew] : 0ull);
+#pragma unroll
+        for (uint32_t u = 0; u < CI_BATCH; u++) {
+          if (kind[u] == 3) continue;  // IP peers: per pod word, in the class rows
+          const uint8_t* pok = a.portok + uint64_t(port[u]) * a.D;
+#pragma unroll
+          for (uint32_t x = 0; x < uint32_t(G); x++)
+            if (du[x] >= 0 && (kind[u] == 0 || pok[du[x]])) b[x] |= v[u];
+        }
+      }
+    } else {
+      for (uint32_t tj = 0; tj < n; tj++) {
+        const DTarget tg = a.tgt[lst[tj]];
+        for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
+          const DPeer pr = a.peers[j];
+          if (pr.kind == 3) continue;  // IP peers: per pod word, in the class rows
+          const uint8_t* pok = a.portok + uint64_t(pr.port) * a.D;
+          if (pr.kind == 0) {  // AllPeersMatcher
+#pragma unroll
+            for (uint32_t x = 0; x < uint32_t(G); x++) b[x] = du[x] >= 0 ? ~0ull : 0ull;
+            break;
+          }
+          const uint64_t vv = pr.kind == 1 ? ~0ull : (ew < a.EW ? a.IDOB[uint64_t(a.peer_ido[j]) * a.EW + ew] : 0ull);
+#pragma unroll
+          for (uint32_t x = 0; x < uint32_t(G); x++)
+            if (du[x] >= 0 && pok[du[x]]) b[x] |= vv;  // PortsForAllPeers / pod peer on an allowed port
+        }
       }
     }
     if (ew < a.EW) {
@@ -1195,19 +1253,40 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
         if (nb0 + x < a.NB) a.B[(uint64_t(i) * a.NB + nb0 + x) * a.EW + ew] = b[x];
     }
   }
-  if (nb0 == 0 && lane == 0) {
-    // the class's IP peers (whatever the port) with nonzero rows, walked per pod word by the class rows
-    uint4* il = a.ip_list + a.ip_off[i];
-    uint32_t m = 0;
+  if (nb0 != 0) return;
+  // the class's IP peers (whatever the port) with nonzero rows, walked per pod word by the class rows
+  uint4* il = a.ip_list + a.ip_off[i];
+  if (flat) {  // lanes over the list, compacted by ballot; none when an AllPeersMatcher allows all
+    uint32_t mm = 0;
+    bool all = false;
+    for (uint32_t e0 = 0; e0 < m; e0 += 64) {
+      const uint32_t e = e0 + lane;
+      uint32_t j = 0, kind = 3, r0 = 0xFFFFFFFFu;
+      if (e < m) {
+        j = sj[e];
+        kind = a.peers[j].kind;
+        if (kind == 3) r0 = a.ip_rng[4 * j];
+      }
+      all |= __ballot(e < m && kind == 0) != 0;
+      const bool keep = e < m && kind == 3 && r0 != 0xFFFFFFFFu;
+      const uint64_t bm = __ballot(keep);
+      if (keep && !all) il[mm + __popcll(bm & ((1ull << lane) - 1))] = make_uint4(j, a.peers[j].port, r0, ~a.ip_rng[4 * j + 1]);
+      mm += __popcll(bm);
+    }
+    if (lane == 0) a.ip_cnt[i] = all ? 0u : mm;
+    return;
+  }
+  if (lane == 0) {
+    uint32_t mm = 0;
     for (uint32_t tj = 0; tj < n; tj++) {
       const DTarget tg = a.tgt[lst[tj]];
       for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
         const DPeer pr = a.peers[j];
         if (pr.kind == 0) break;  // AllPeers: the identity sets already allow everything
-        if (pr.kind == 3 && a.ip_rng[4 * j] != 0xFFFFFFFFu) il[m++] = make_uint4(j, pr.port, a.ip_rng[4 * j], ~a.ip_rng[4 * j + 1]);
+        if (pr.kind == 3 && a.ip_rng[4 * j] != 0xFFFFFFFFu) il[mm++] = make_uint4(j, pr.port, a.ip_rng[4 * j], ~a.ip_rng[4 * j + 1]);
       }
     }
-    a.ip_cnt[i] = m;
+    a.ip_cnt[i] = mm;
   }
 }
 template <bool EGRESS, int G>
