@@ -180,7 +180,10 @@ struct SelView {
   const DReq* dreqs;
   const uint32_t* PLVT;   // LVT's columns per pod: PLVT[kx][q] = LVT[kx][label set of pod q]
   uint32_t P;
+  const uint4* one;       // per selector: (op | values << 8, dense key, value 0, value 1) when it is ONE
+                          // requirement of <= 2 values; x = SEL_ALL (no requirement) / SEL_WALK (other)
 };
+constexpr uint32_t SEL_ALL = 0xFFFFFFFEu, SEL_WALK = 0xFFFFFFFFu;
 // (tab, n) = (LVT, L) with l a label set, or (PLVT, P) with l a pod: the key's value column
 __device__ __forceinline__ uint32_t sel_eval(const SelView& v, const uint32_t* __restrict__ tab, uint32_t n, uint32_t s, uint32_t l) {
   for (uint32_t r = v.sel_off[s]; r < v.sel_off[s + 1]; r++) {
@@ -206,8 +209,27 @@ __device__ __forceinline__ uint32_t sel_eval(const SelView& v, const uint32_t* _
   }
   return 1;
 }
+// labelselector.go:66-86 for one requirement, x = the pod's value of the key (~0: absent), with at
+// most two values (v0, v1; vc of them)
+__device__ __forceinline__ bool req_holds(uint32_t op, uint32_t x, uint32_t v0, uint32_t v1, uint32_t vc) {
+  const bool present = x != 0xFFFFFFFFu;
+  const bool in = (vc > 0 && x == v0) || (vc > 1 && x == v1);
+  switch (op) {
+    case REQ_EQ: return present && x == v0;
+    case REQ_EQ_EMPTY: return !present || x == v0;
+    case REQ_IN: return present && in;
+    case REQ_NOTIN: return present && !in;
+    case REQ_EXISTS: return present;
+    default: return !present;  // REQ_DNE
+  }
+}
+
 __device__ __forceinline__ uint32_t sel_at(const SelView& v, uint32_t s, uint32_t l) {
   if (v.selres) return v.selres[uint64_t(s) * v.L + l];
+  // one requirement: one table load, no walk (so several evaluations' loads can be in flight)
+  const uint4 d = v.one[s];
+  if (d.x == SEL_ALL) return 1;
+  if (d.x != SEL_WALK) return req_holds(d.x & 0xFFu, v.LVT[uint64_t(d.y) * v.L + l], d.z, d.w, d.x >> 8) ? 1u : 0u;
   return sel_eval(v, v.LVT, v.L, s, l);
 }
 // Pod selector s on pod q's own labels through PLVT: one coalesced load per requirement for a wave
@@ -355,21 +377,6 @@ struct DWordNS {
 #define CYC_PR_WB 8
 #endif
 constexpr uint32_t PR_WB = CYC_PR_WB;  // words evaluated at once per wave
-
-// labelselector.go:66-86 for one requirement, x = the pod's value of the key (~0: absent), with at
-// most two values (v0, v1; vc of them)
-__device__ __forceinline__ bool req_holds(uint32_t op, uint32_t x, uint32_t v0, uint32_t v1, uint32_t vc) {
-  const bool present = x != 0xFFFFFFFFu;
-  const bool in = (vc > 0 && x == v0) || (vc > 1 && x == v1);
-  switch (op) {
-    case REQ_EQ: return present && x == v0;
-    case REQ_EQ_EMPTY: return !present || x == v0;
-    case REQ_IN: return present && in;
-    case REQ_NOTIN: return present && !in;
-    case REQ_EXISTS: return present;
-    default: return !present;  // REQ_DNE
-  }
-}
 
 // Word masks of pod peer pr over chunk `chunk` (this lane's word w): the namespace outcome per word
 // first, then a pod per lane for the words it leaves open — only those of rank part, part + parts,
@@ -2574,6 +2581,7 @@ struct cyc_ctx {
                        // (namespace matcher, pod selector) of a direction (peer_ido maps every peer)
   DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
   DevBuf plvt;      // LVT per pod (SelView::PLVT)
+  DevBuf sel_one;   // SelView::one
   DevBuf req_post, post_pods;  // label postings: per requirement (offset, count) x 2 values; pod lists
   std::vector<uint8_t> req_post_ok;  // the requirement's pods are its postings (EQ, IN of <= 2 values)
   DevBuf pp_scan, pp_post;     // sparse pod rows: pod peers scanned per word / built from postings
@@ -2814,6 +2822,22 @@ static void prepare_device(cyc_ctx* c) {
       for (DReq& q : dr) q.key = (q.op != REQ_INVALID && q.key < kx.size() && kx[q.key] >= 0) ? uint32_t(kx[q.key]) : nk;
       upload(c->lvt, lvt);
       upload(c->dreqs, dr);
+      {  // one-requirement selectors in a single record each (SelView::one)
+        std::vector<uint4> one(std::max<size_t>(pb.S, 1), uint4{SEL_WALK, 0, 0, 0});
+        for (uint32_t sid = 0; sid < pb.S; sid++) {
+          const uint32_t r0 = pb.sel_off[sid], nr = pb.sel_off[sid + 1] - r0;
+          if (nr == 0) {
+            one[sid].x = SEL_ALL;
+            continue;
+          }
+          const DReq& q = dr[r0];
+          if (nr != 1 || q.op == REQ_INVALID || q.vcnt > 2) continue;
+          const bool has_v = q.op == REQ_EQ || q.op == REQ_EQ_EMPTY || q.op == REQ_IN || q.op == REQ_NOTIN;
+          const uint32_t vc = has_v ? (q.op == REQ_EQ || q.op == REQ_EQ_EMPTY ? 1u : q.vcnt) : 0u;
+          one[sid] = uint4{q.op | (vc << 8), q.key, vc > 0 ? pb.req_vals[q.voff] : 0u, vc > 1 ? pb.req_vals[q.voff + 1] : 0u};
+        }
+        upload(c->sel_one, one);
+      }
       // the same table per pod (sparse pod-peer rows evaluate pod selectors on a wave of pods)
       std::vector<uint32_t> plvt(uint64_t(nk + 1) * pb.P);
       for (uint32_t kk = 0; kk <= nk; kk++)
@@ -3005,6 +3029,7 @@ static SelView sel_view(cyc_ctx* c) {
   v.dreqs = c->dreqs.as<DReq>();
   v.PLVT = c->plvt.as<uint32_t>();
   v.P = c->pb.P;
+  v.one = c->sel_one.as<uint4>();
   return v;
 }
 
