@@ -1746,8 +1746,11 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
         if (pr.kind == 0) {
           sh.all = 1;  // AllPeersMatcher
         } else {
-          en = make_uint4(pr.kind == 1 ? PL_ONES : j, pr.port, 0u, a.W - 1);
-          if (pr.kind == 3 || (pr.kind == 2 && a.pod_sparse)) {  // bit 31 of z: a sparse row (only the cnz-marked words were written)
+          // PortsForAllPeers, and a pod peer of every pod in every namespace (podpeermatcher.go with
+          // AllNamespaceMatcher + AllPodMatcher): all-ones rows, never loaded (nor built, sparse rows)
+          const bool ones = pr.kind == 1 || (pr.kind == 2 && pr.nskind == 1 && pr.podsel == CYC_ALL);
+          en = make_uint4(ones ? PL_ONES : j, pr.port, 0u, a.W - 1);
+          if (!ones && (pr.kind == 3 || (pr.kind == 2 && a.pod_sparse))) {  // bit 31 of z: a sparse row (only the cnz-marked words were written)
             en.z = a.ip_rng[4 * j] | PL_IP;
             en.w = ~a.ip_rng[4 * j + 1];
             if (a.ip_rng[4 * j] == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
@@ -3063,9 +3066,12 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   return a;
 }
 
-// PM-build class rows (k_class_rows_pl, PL_THREADS per block): blocks per direction, striding over
-// the representatives; about two blocks in flight per CU slot
-static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c->n_act[d], 2048u * 256u / PL_THREADS); }
+// PM-build class rows (k_class_rows_pl): threads per block — PL_THREADS, or 256 for rows of >= 16
+// chunks (the wave-per-chunk rows then split a class's chunks over 4 waves: config #3u -5 %,
+// config #4's 13 chunks +9 %: profiles/r02_pl_threads_ab.txt) — and blocks per direction, striding
+// over the representatives, about two blocks in flight per CU slot
+static uint32_t pl_threads(const cyc_ctx* c) { return (c->pb.W + 63) / 64 >= 16 ? 256u : PL_THREADS; }
+static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c->n_act[d], 2048u * 256u / pl_threads(c)); }
 
 // Range plan for rows [lo,hi): (1) the rows ordered so pods sharing class rows are adjacent
 // (L2 / Infinity-Cache reuse in k_emit); (2) the identities those rows use, per direction —
@@ -3144,6 +3150,7 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
     for (uint32_t j : c->plan.pod_peers) {
       if (!peer_needed[j]) continue;
       const DPeer& pr = pb.peers[j];
+      if (pr.nskind == NS_ALL && pr.podsel == CYC_ALL) continue;  // all-ones row: the class rows need none
       const bool one = pr.podsel != CYC_ALL && pb.sel_off[pr.podsel + 1] - pb.sel_off[pr.podsel] == 1;
       if (one && c->dense_sel && !c->req_post_ok.empty() && c->req_post_ok[pb.sel_off[pr.podsel]]) post.push_back(j);
       else scan.push_back(j);
@@ -3421,10 +3428,10 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     else k_class_rows_ido<true, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
   } else {  // per-class flattened peer lists (the IP word spans are final here)
     const bool wave = pl_wave_ok(c);
-    if (d == 0 && wave) k_class_rows_pl<false, true><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
-    else if (d == 0) k_class_rows_pl<false, false><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
-    else if (wave) k_class_rows_pl<true, true><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
-    else k_class_rows_pl<true, false><<<pl_blocks(c, d), PL_THREADS, 0, st>>>(ra);
+    if (d == 0 && wave) k_class_rows_pl<false, true><<<pl_blocks(c, d), pl_threads(c), 0, st>>>(ra);
+    else if (d == 0) k_class_rows_pl<false, false><<<pl_blocks(c, d), pl_threads(c), 0, st>>>(ra);
+    else if (wave) k_class_rows_pl<true, true><<<pl_blocks(c, d), pl_threads(c), 0, st>>>(ra);
+    else k_class_rows_pl<true, false><<<pl_blocks(c, d), pl_threads(c), 0, st>>>(ra);
   }
 }
 
@@ -3661,8 +3668,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (fc.nb[0] + fc.nb[1] + fc.nb[2] + fc.nb[3]) k_front_c<<<fc.nb[0] + fc.nb[1] + fc.nb[2] + fc.nb[3], 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
-    if (fd.nb[0] + fd.nb[1] && pl_wave_ok(c)) k_front_d_pm<true><<<fd.nb[0] + fd.nb[1], PL_THREADS, 0, st>>>(fd);
-    else if (fd.nb[0] + fd.nb[1]) k_front_d_pm<false><<<fd.nb[0] + fd.nb[1], PL_THREADS, 0, st>>>(fd);
+    if (fd.nb[0] + fd.nb[1] && pl_wave_ok(c)) k_front_d_pm<true><<<fd.nb[0] + fd.nb[1], pl_threads(c), 0, st>>>(fd);
+    else if (fd.nb[0] + fd.nb[1]) k_front_d_pm<false><<<fd.nb[0] + fd.nb[1], pl_threads(c), 0, st>>>(fd);
     if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
     return true;
   }
