@@ -334,12 +334,14 @@ def test_pm_class_rows_wave_and_items(gpu):
         eng.set_option("pl_wave", 1)
         # sparse pod-peer rows a block per peer or a wave per chunk over peer groups, selectors
         # evaluated where used or as the dense table first
-        for grp, lazy in ((1, 1), (8, 0), (3, 1), (64, -1)):
+        for grp, lazy, wave in ((1, 1, 1), (8, 0, 1), (3, 1, 0), (64, -1, 1), (2, 0, 0)):
             eng.set_option("pr_group", grp)
             eng.set_option("sel_lazy", lazy)
-            assert_same(want, eng.run_host(), f"problem {n} pr_group={grp} sel_lazy={lazy}")
+            eng.set_option("pl_wave", wave)  # sparse rows read per word (spans + chunk flags) or per chunk
+            assert_same(want, eng.run_host(), f"problem {n} pr_group={grp} sel_lazy={lazy} pl_wave={wave}")
         eng.set_option("pr_group", -1)
         eng.set_option("sel_lazy", -1)
+        eng.set_option("pl_wave", 1)
         seen_wave += eng.get_option("pl_wave_active")
     assert seen_wave >= 10
 
