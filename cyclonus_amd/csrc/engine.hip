@@ -709,7 +709,7 @@ __device__ __forceinline__ uint64_t cnz_mask(const uint32_t* __restrict__ cnz, u
 // word): the group's tests and their except records are staged into LDS once (one coalesced load
 // per block, instead of a chain of dependent scalar loads per peer and except), and each wave loads
 // its words' [min, max] records once for the whole group.
-constexpr uint32_t IP_GROUP = 8, IP_GROUP_MAX = 64, IP_EX_LDS = 256;
+constexpr uint32_t IP_GROUP = 16, IP_GROUP_MAX = 64, IP_EX_LDS = 256;  // 16: profiles/r02_ip_group_ab.txt
 __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
