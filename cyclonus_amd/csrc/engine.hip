@@ -1111,7 +1111,10 @@ constexpr uint32_t IDO_LDS_BYTES = 48 * 1024;  // staged identity sets per class
 // peers): the identities' (namespace, namespace labels, labels) are loaded once and the group's
 // outcomes (podpeermatcher.go:21-28: namespace then pod matcher) are independent selres gathers;
 // one ballot per peer -> IDOB (no-panic runs only).
-constexpr uint32_t PB_GROUP = 8;
+#ifndef CYC_PB_GROUP
+#define CYC_PB_GROUP 16  // pod peers per identity-set wave (8: +4 % launch B, profiles/r02_pb_group_ab.txt)
+#endif
+constexpr uint32_t PB_GROUP = CYC_PB_GROUP;
 __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
                                                    const DPeer* __restrict__ peers, const SelView& sv,
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
