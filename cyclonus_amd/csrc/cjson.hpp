@@ -32,22 +32,35 @@ struct Node {
   const Node* find(std::string_view k) const {
     if (t != Obj) return nullptr;
     const Node* hit = nullptr;
-    for (auto& kv : o) {
-      if (kv.first.size() != k.size()) continue;
-      size_t i = 0;
-      for (; i < k.size(); i++) {
-        char x = kv.first[i], y = k[i];
-        if (x >= 'A' && x <= 'Z') x += 32;
-        if (y >= 'A' && y <= 'Z') y += 32;
-        if (x != y) break;
-      }
-      if (i == k.size()) hit = &kv.second;
-    }
+    for (auto& kv : o)
+      if (key_eq(kv.first, k)) hit = &kv.second;
     return hit;
   }
+  // Pointer, slice, map and interface fields: JSON null sets them to nil, so the last matching
+  // key decides and a null there means absent.
   const Node* val(std::string_view k) const {  // non-null member or nullptr
     const Node* n = find(k);
     return (n && n->t != Null) ? n : nullptr;
+  }
+  // Scalar (string, number, bool) and struct-valued fields: encoding/json leaves them unchanged
+  // for a JSON null, so the last NON-null matching key decides ({"Namespace":"a","namespace":null}
+  // decodes to "a").
+  const Node* sval(std::string_view k) const {
+    if (t != Obj) return nullptr;
+    const Node* hit = nullptr;
+    for (auto& kv : o)
+      if (kv.second.t != Null && key_eq(kv.first, k)) hit = &kv.second;
+    return hit;
+  }
+  static bool key_eq(std::string_view a, std::string_view k) {  // exact or ASCII case-insensitive
+    if (a.size() != k.size()) return false;
+    for (size_t i = 0; i < k.size(); i++) {
+      char x = a[i], y = k[i];
+      if (x >= 'A' && x <= 'Z') x += 32;
+      if (y >= 'A' && y <= 'Z') y += 32;
+      if (x != y) return false;
+    }
+    return true;
   }
   const std::string& str() const {
     if (t != Str) throw std::runtime_error("json: expected a string");

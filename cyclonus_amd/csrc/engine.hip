@@ -242,6 +242,15 @@ __device__ __forceinline__ void fill_u32_blk(uint32_t* p, uint64_t n, uint32_t v
 }
 __global__ void k_fill_u32(uint32_t* p, uint64_t n, uint32_t v) { fill_u32_blk(p, n, v, blockIdx.x, gridDim.x); }
 
+// PLVT[kx][q] = LVT[kx][label set of pod q] (SelView::PLVT), one word per thread (grid-stride)
+__global__ __launch_bounds__(256) void k_plvt(const uint32_t* __restrict__ LVT, const uint32_t* __restrict__ pod_ls, uint32_t L,
+                                              uint32_t P, uint64_t n, uint32_t* __restrict__ PLVT) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t kx = i / P, q = i - kx * P;
+    PLVT[i] = LVT[kx * L + pod_ls[q]];
+  }
+}
+
 // IPNet.Contains after To4 collapse (ipaddress.go:10-20): families must agree.
 __device__ __forceinline__ bool cidr_contains(const DCidr& c, const DIP& ip) {
   if (c.fam != ip.fam) return false;
@@ -434,9 +443,13 @@ __device__ __forceinline__ uint64_t pod_chunk_words(const DPeer& pr, const SelVi
       live[u] = wl[u] < 64 && q[u] < P;
       // the pod's namespace (exact matcher) or namespace label set (selector), when needed
       nsv[u] = live[u] && pr.nskind != 1 ? (pr.nskind == 0 ? pod_ns[q[u]] : pod_nsls[q[u]]) : 0u;
-      // the selector's key value of the pod (one requirement), or the pod's label set (dense table)
+      // the selector's key value of the pod (one requirement), or the pod's label set (dense table,
+      // or no PLVT: the selector is then evaluated on the label set)
       xv[u] = 0;
-      if (live[u] && pr.podsel != CYC_ALL) xv[u] = one ? sv.PLVT[uint64_t(r_key) * P + q[u]] : sv.selres ? pod_ls[q[u]] : 0u;
+      if (live[u] && pr.podsel != CYC_ALL) {
+        if (one) xv[u] = sv.PLVT ? sv.PLVT[uint64_t(r_key) * P + q[u]] : sv.LVT[uint64_t(r_key) * sv.L + pod_ls[q[u]]];
+        else if (sv.selres || !sv.PLVT) xv[u] = pod_ls[q[u]];
+      }
     }
 #pragma unroll
     for (uint32_t u = 0; u < PR_WB; u++) {
@@ -446,7 +459,8 @@ __device__ __forceinline__ uint64_t pod_chunk_words(const DPeer& pr, const SelVi
       bool b = pr.podsel == CYC_ALL;
       if (!b && live[u])
         b = one ? req_holds(r_op, xv[u], r_v0, r_v1, r_vc)
-                : (sv.selres ? sv.selres[uint64_t(pr.podsel) * sv.L + xv[u]] : sel_at_pod(sv, pr.podsel, q[u])) == 1;
+                : (sv.selres ? sv.selres[uint64_t(pr.podsel) * sv.L + xv[u]]
+                   : sv.PLVT ? sel_at_pod(sv, pr.podsel, q[u]) : sel_at(sv, pr.podsel, xv[u])) == 1;
       const uint64_t m = __ballot(live[u] && a && b);
       if (lane == wl[u]) mine = m;
     }
@@ -1454,9 +1468,6 @@ __device__ __forceinline__ uint64_t pl_word(const RowArgs& a, const uint4& e, ui
   if (e.x == PL_ONES) return ~0ull;
   const uint32_t lo = e.z & ~PL_IP;
   if (e.x == PL_SKIP || w < lo || w > e.w) return 0ull;
-#ifdef CYC_DIAG_NO_PM
-  return uint64_t(e.x) * 0x9E3779B97F4A7C15ull ^ w;
-#endif
   const uint64_t v = a.PM[uint64_t(e.x) * a.W + w];
   return (e.z & PL_IP) ? v & cnz_mask(a.ip_cnz, a.W, e.x, w) : v;
 }
@@ -1564,6 +1575,9 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
       if (!undecided) break;
     }
   } else if (!allow_all) {  // mixed descriptors, no bit rows (ingress K > 32), lists past the LDS part
+    // ingress with K <= 32: an entry's .y is its slot bits for this representative (class_rows_pl_blk),
+    // not a port matcher id; every other entry carries the port matcher
+    const bool slot_bits = !EGRESS && a.K <= 32;
     for (uint32_t x = 0; x < m; x++) {
       const uint4 e = x < PL_LDS ? sh.e[x] : spill[x];
 #pragma unroll
@@ -1571,8 +1585,13 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
         const uint64_t pm = pl_word(a, e, w[q]);
         if (!pm) continue;
 #pragma unroll
-        for (int kk = 0; kk < KC; kk++)
-          allow[q][kk] |= pm & port_mask<EGRESS>(a, a.portok + uint64_t(e.y) * a.D, du[q][kk], k0[q] + kk, w[q]);
+        for (int kk = 0; kk < KC; kk++) {
+          if (slot_bits) {
+            if (du[q][kk] >= 0 && ((e.y >> (k0[q] + kk)) & 1u)) allow[q][kk] |= pm;
+          } else {
+            allow[q][kk] |= pm & port_mask<EGRESS>(a, a.portok + uint64_t(e.y) * a.D, du[q][kk], k0[q] + kk, w[q]);
+          }
+        }
       }
     }
   }
@@ -1581,10 +1600,6 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
       const uint32_t k = k0[q] + kk;
-#ifdef CYC_DIAG_NO_STORE
-      if (k < a.K && (allow[q][kk] & valid[q][kk]) == 0x123456789ull) a.A[(uint64_t(i) * a.K + k) * a.W + w[q]] = 1;
-      continue;
-#endif
       if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.W + w[q]] = allow[q][kk] & valid[q][kk];
     }
 }
@@ -1712,15 +1727,7 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
     if (threadIdx.x == 0) sh.all = 0;
     uint32_t m = 0;
-#ifdef CYC_DIAG_NO_LIST
-    if (nt) {
-      if (threadIdx.x == 0) sh.all = 0;
-      __syncthreads();
-    }
-    for (uint32_t t0 = 0; t0 < 0; t0 += PL_TGT) {
-#else
     for (uint32_t t0 = 0; t0 < nt; t0 += PL_TGT) {  // targets in chunks: offsets, counts, prefix sums
-#endif
       const uint32_t ntc = min(PL_TGT, nt - t0);
       for (uint32_t t = threadIdx.x; t < ntc; t += blockDim.x) {
         const DTarget tg = a.tgt[lst[t0 + t]];
@@ -1801,9 +1808,6 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     const bool allow_all = nt == 0 || sh.all;
     const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
     // the class's (slot chunk, word) items, PL_ITEMS per thread at once (their loads overlap)
-#ifdef CYC_DIAG_NO_ITEMS
-    if (m < 100000) continue;
-#endif
     if (WAVE) {
       pl_wave_chunks<EGRESS>(a, sh, spill, i, m, allow_all, lastmask);
     } else {
@@ -2091,9 +2095,6 @@ __global__ __launch_bounds__(256) void k_front_c(FrontC f) {
   b -= f.nb[0];
   if (b < f.nb[1]) return classify_blk(f.ma[1], f.class_of[1], b, f.nb[1]);
   b -= f.nb[1];
-#ifdef CYC_DIAG_NO_PODROWS  // timing diagnostic only (rows stay empty: results are wrong)
-  return;
-#endif
   if (b < f.nb[2])
     return pod_rows_sparse_blk(f.Rp, f.P, f.W, f.plist, f.peers, f.sv, f.pod_ns, f.pod_nsls, f.pod_ls, f.nsw, f.PM, f.rng, f.cnz,
                                f.pr_grp, b);
@@ -2515,6 +2516,29 @@ struct HipErr {
   std::string msg;
 };
 
+// Makes `device` current for the scope of an entry point and restores the caller's current device
+// afterwards: a binding calling in from a thread whose current device is another GPU (e.g. PyTorch
+// on cuda:1 with a context on device 0) keeps its own current device.
+struct DeviceGuard {
+  int prev = -1;
+  bool set = false;
+  explicit DeviceGuard(int device, bool strict = true) {
+    hipError_t e = hipGetDevice(&prev);
+    if (e == hipSuccess && prev == device) return;
+    e = hipSetDevice(device);
+    if (e != hipSuccess) {
+      if (strict) throw HipErr{std::string("hipSetDevice: ") + hipGetErrorString(e)};
+      return;
+    }
+    set = prev >= 0;
+  }
+  ~DeviceGuard() {
+    if (set) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -2586,7 +2610,10 @@ struct cyc_ctx {
   DevBuf pod_peers_u;  // identity-set (IDOB) rows: the needed pod peers, one per distinct
                        // (namespace matcher, pod selector) of a direction (peer_ido maps every peer)
   DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
-  DevBuf plvt;      // LVT per pod (SelView::PLVT)
+  DevBuf plvt;      // LVT per pod (SelView::PLVT), built by ensure_plvt when it fits PLVT_MAX_BYTES
+  uint32_t n_lkeys = 0;     // dense label keys (LVT rows - 1)
+  bool plvt_ready = false;
+  int64_t plvt_max_mb = 1024;  // "plvt_max_mb": largest PLVT built (0: never, the LVT gathers instead)
   DevBuf sel_one;   // SelView::one
   DevBuf req_post, post_pods;  // label postings: per requirement (offset, count) x 2 values; pod lists
   std::vector<uint8_t> req_post_ok;  // the requirement's pods are its postings (EQ, IN of <= 2 values)
@@ -2654,6 +2681,7 @@ struct cyc_ctx {
   double last_ms[3] = {0, 0, 0};
   bool timed = false;  // the last run recorded the step timing events
   bool ran = false;    // a run has been enqueued
+  hipEvent_t run_done = nullptr;  // recorded on the run's stream after every run (cyc_last_classes)
 };
 
 int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t idx);
@@ -2844,11 +2872,11 @@ static void prepare_device(cyc_ctx* c) {
         }
         upload(c->sel_one, one);
       }
-      // the same table per pod (sparse pod-peer rows evaluate pod selectors on a wave of pods)
-      std::vector<uint32_t> plvt(uint64_t(nk + 1) * pb.P);
-      for (uint32_t kk = 0; kk <= nk; kk++)
-        for (uint32_t q = 0; q < pb.P; q++) plvt[uint64_t(kk) * pb.P + q] = lvt[uint64_t(kk) * pb.L + pb.pod_ls[q]];
-      upload(c->plvt, plvt);
+      // the same table per pod (PLVT, sparse pod-peer rows) is gathered on the device when a run
+      // first needs it (ensure_plvt): IDO builds never read it, and it is (keys + 1) x P words
+      c->n_lkeys = nk;
+      c->plvt.alloc(0);
+      c->plvt_ready = false;
       // label postings: the pods under each (dense key, value) of their own labels, and per EQ / IN
       // (<= 2 values) requirement the postings of its values (pod_rows_post_blk)
       std::vector<std::pair<uint64_t, uint32_t>> kv;
@@ -3016,6 +3044,20 @@ static bool pod_sparse(const cyc_ctx* c) {
   const uint64_t Rp = c->rp_off[2] - c->rp_off[0];
   return c->pr_group > 0 || Rp * c->pb.W >= (2ull << 20);
 }
+// PLVT (each pod's value of every dense label key) for the sparse pod-peer rows: gathered on the
+// device from LVT once per prepare, on the run's stream ahead of the step, when a run needs it
+// and it fits PLVT_MAX_BYTES; otherwise the rows read LVT through each pod's label set (SelView
+// with PLVT null), one more dependent load per pod.
+static void ensure_plvt(cyc_ctx* c, hipStream_t st) {
+  if (c->plvt_ready || !c->dense_sel || !pod_sparse(c)) return;
+  const uint64_t n = uint64_t(c->n_lkeys + 1) * c->pb.P;
+  if (!n || n * 4 > (uint64_t(c->plvt_max_mb) << 20)) return;
+  c->plvt.alloc(n * 4);
+  k_plvt<<<grid1(n, 256), 256, 0, st>>>(c->lvt.as<uint32_t>(), c->pod_ls.as<uint32_t>(), c->pb.L, c->pb.P, n,
+                                        c->plvt.as<uint32_t>());
+  HIPCHK(hipGetLastError());
+  c->plvt_ready = true;
+}
 static bool lazy_sel(const cyc_ctx* c) {
   if (!c->dense_sel || c->pb.may_err || c->sel_lazy == 0 || !front_fused_ok(c)) return false;
   if (!ido_mode(c) && !pod_sparse(c)) return false;  // the full pod-peer rows read the dense selector table
@@ -3033,7 +3075,7 @@ static SelView sel_view(cyc_ctx* c) {
   v.req_vals = c->req_vals.as<uint32_t>();
   v.LVT = c->lvt.as<uint32_t>();
   v.dreqs = c->dreqs.as<DReq>();
-  v.PLVT = c->plvt.as<uint32_t>();
+  v.PLVT = c->plvt_ready ? c->plvt.as<uint32_t>() : nullptr;  // null: pod -> label set -> LVT gathers
   v.P = c->pb.P;
   v.one = c->sel_one.as<uint4>();
   return v;
@@ -3781,14 +3823,21 @@ static void ensure_cap_streams(cyc_ctx* c) {
   HIPCHK(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
 }
 
+// allow_capture = false: never capture a graph for this run (cyc_table_run's planes are new on
+// every call, so a captured graph would be re-instantiated each time): graphs = 1 runs as 2.
 static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
-                        int64_t hi) {
+                        int64_t hi, bool allow_capture = true) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W;
   if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
   if (c->order_lo != lo || c->order_hi != hi) drop_graph(c);  // range plan buffers are re-made
   ensure_range(c, lo, hi);
-  const int graphs = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);
+  if (!c->plvt_ready && front_fused_ok(c) && pod_sparse(c)) {
+    drop_graph(c);  // a graph captured without the per-pod table would keep the slower gathers
+    ensure_plvt(c, st);
+  }
+  int graphs = c->use_graphs >= 0 ? c->use_graphs : (front_fused_ok(c) ? 2 : 1);
+  if (graphs == 1 && !allow_capture) graphs = 2;
   if (graphs == 2 && !pb.may_err) {
     // the graph's DAG, enqueued directly: the caller's stream forks to two internal streams and
     // joins them back before the emit (events), without hipGraphLaunch's per-replay latency
@@ -3826,6 +3875,7 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     c->timed_graph = false;
   }
   c->ran = true;
+  HIPCHK(hipEventRecord(c->run_done, st));
 
   // 8. panic path: the first panicking job in job order, as the reference would hit it.  Configs
   // run in order (one RunProbeForConfig each); within one, the job expansion (may panic on a pod
@@ -3998,7 +4048,7 @@ int cyc_ctx_create(int device_id, cyc_ctx** out) {
 void cyc_ctx_destroy(cyc_ctx* c) {
   if (!c) return;
   if (c->stream) {
-    (void)hipSetDevice(c->device);
+    DeviceGuard dg(c->device, false);
     drop_graph(c);
     reap_graphs(c, true);  // waits for each retired exec's last launch only
     destroy_events(c);
@@ -4009,6 +4059,7 @@ void cyc_ctx_destroy(cyc_ctx* c) {
     if (c->ports_ev) (void)hipEventDestroy(c->ports_ev);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    if (c->run_done) (void)hipEventDestroy(c->run_done);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -4061,10 +4112,11 @@ int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* s
   if (!c || !js) return CYC_ERR_ARG;
   if (!c->have_policy || !c->have_res) return fail(c, CYC_ERR_ARG, "load a policy and resources first");
   return guarded(c, [&] {
-    HIPCHK(hipSetDevice(c->device));
+    DeviceGuard dg(c->device);
     if (!c->stream) {
       HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+      HIPCHK(hipEventCreateWithFlags(&c->run_done, hipEventDisableTiming));
     }
     auto probes = load_probes(json::parse(js, len));
     c->pb = build_problem(c->policy, c->res, probes);
@@ -4099,7 +4151,7 @@ int cyc_probe_run(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg, uint
   if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
   if ((!d_in || !d_eg) && hi > lo) return fail(c, CYC_ERR_ARG, "null output plane");
   return guarded(c, [&] {
-    HIPCHK(hipSetDevice(c->device));
+    DeviceGuard dg(c->device);
     hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the HIP default (null) stream
     return run_pipeline(c, st, d_in, d_eg, d_status, lo, hi);
   });
@@ -4109,7 +4161,7 @@ int cyc_probe_run_host(cyc_ctx* c, uint64_t* h_in, uint64_t* h_eg, uint8_t* h_st
   if (!c) return CYC_ERR_ARG;
   if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
   return guarded(c, [&] {
-    HIPCHK(hipSetDevice(c->device));
+    DeviceGuard dg(c->device);
     uint64_t rows = uint64_t(std::max<int64_t>(hi - lo, 0));
     uint64_t words = rows * c->pb.K * c->pb.W;
     DevBuf din, deg, dst;
@@ -4157,7 +4209,7 @@ int cyc_table_run(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) {
   *out = nullptr;
   if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
   return guarded(c, [&]() -> int {
-    HIPCHK(hipSetDevice(c->device));
+    DeviceGuard dg(c->device);
     cyc_table* t = nullptr;
     int rc = table_new(c, lo, hi, &t);
     if (rc != CYC_OK) return rc;
@@ -4169,7 +4221,8 @@ int cyc_table_run(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) {
     t->in = t->own_in.as<uint64_t>();
     t->eg = t->own_eg.as<uint64_t>();
     t->status = t->own_st.as<uint8_t>();
-    rc = run_pipeline(c, c->stream, t->own_in.as<uint64_t>(), t->own_eg.as<uint64_t>(), t->own_st.as<uint8_t>(), lo, hi);
+    rc = run_pipeline(c, c->stream, t->own_in.as<uint64_t>(), t->own_eg.as<uint64_t>(), t->own_st.as<uint8_t>(), lo, hi,
+                      false);
     HIPCHK(hipStreamSynchronize(c->stream));
     if (rc != CYC_OK) return rc;
     *out = hold.release();
@@ -4221,7 +4274,7 @@ int cyc_table_cells(cyc_table* t, int64_t s_lo, int64_t s_hi, int64_t d_lo, int6
   const uint64_t n = uint64_t(s_hi - s_lo) * uint64_t(d_hi - d_lo) * uint64_t(k_hi - k_lo);
   if (!n) return (int)CYC_OK;
   try {
-    HIPCHK(hipSetDevice(t->device));
+    DeviceGuard dg(t->device);
     if (!t->stream) HIPCHK(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
     DevBuf o[3];
     uint8_t* host[3] = {ingress, egress, combined};
@@ -4261,7 +4314,7 @@ int cyc_table_cells(cyc_table* t, int64_t s_lo, int64_t s_hi, int64_t d_lo, int6
 
 void cyc_table_destroy(cyc_table* t) {
   if (!t) return;
-  (void)hipSetDevice(t->device);
+  DeviceGuard dg(t->device, false);
   if (t->stream) {
     (void)hipStreamSynchronize(t->stream);
     (void)hipStreamDestroy(t->stream);
@@ -4273,6 +4326,7 @@ int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
   if (!c || !ms) return CYC_ERR_ARG;
   if (!c->timed) return fail(c, CYC_ERR_ARG, c->ran ? "the last run recorded no timing events (step_events = 0)" : "no run yet");
   return guarded(c, [&] {
+    DeviceGuard dg(c->device);
     HIPCHK(hipEventSynchronize(c->ev[3]));
     float a = 0, b = 0, r = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[3]));
@@ -4290,8 +4344,8 @@ int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
   if (!c || !out || n < 2) return CYC_ERR_ARG;
   if (!c->ran) return fail(c, CYC_ERR_ARG, "no run yet");
   return guarded(c, [&]() -> int {
-    HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipDeviceSynchronize());
+    DeviceGuard dg(c->device);
+    HIPCHK(hipEventSynchronize(c->run_done));  // the last run's stream, not the whole device
     for (int d = 0; d < 2; d++) {
       uint32_t v = 0xFFFFFFFFu;
       if (c->dir[d].n && c->n_act[d]) HIPCHK(hipMemcpy(&v, c->dir[d].rep_cnt(), 4, hipMemcpyDeviceToHost));
@@ -4303,7 +4357,8 @@ int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
 
 int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return CYC_ERR_ARG;
-  if (c->stream) (void)hipSetDevice(c->device);  // drop_graph may destroy this context's execs
+  std::unique_ptr<DeviceGuard> dg;
+  if (c->stream) dg.reset(new DeviceGuard(c->device, false));  // drop_graph may destroy this context's execs
   const std::string n(name);
   auto range = [&](int64_t lo, int64_t hi) {
     if (value < lo || value > hi) throw Panic{CYC_ERR_ARG, n + " must be in " + std::to_string(lo) + ".." + std::to_string(hi)};
@@ -4321,6 +4376,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "pr_group") range(-1, 64), c->pr_group = int(value == 0 ? -1 : value);
     else if (n == "class_inplace") range(-1, 1), c->class_inplace = int(value);
     else if (n == "step_events") range(0, 1), c->step_events = int(value);
+    else if (n == "plvt_max_mb") {
+      range(0, 1 << 20);
+      c->plvt_max_mb = value;
+      c->plvt_ready = false;  // rebuilt (or not) by the next run
+      c->plvt.alloc(0);
+    }
     else return fail(c, CYC_ERR_ARG, "unknown option " + n);
     drop_graph(c);
     return (int)CYC_OK;
@@ -4345,6 +4406,8 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
     *value = inplace_ok(c, reinterpret_cast<const uint64_t*>(16), reinterpret_cast<const uint64_t*>(16)) ? 1 : 0;
   }
   else if (n == "step_events") *value = c->step_events;
+  else if (n == "plvt_max_mb") *value = c->plvt_max_mb;
+  else if (n == "plvt_active") *value = c->plvt_ready ? 1 : 0;
   else if (n == "pl_wave_active") {
     if (!c->prepared) return fail(c, CYC_ERR_ARG, "pl_wave_active: call cyc_probe_prepare first");
     *value = !ido_mode(c) && pl_wave_ok(c) ? 1 : 0;
@@ -4361,7 +4424,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
 // targets in primary-key order, t for an allowing target and -t-1 for a denying one.
 static int run_query(cyc_ctx* c, const std::vector<QueryTraffic>& ts, uint8_t* out,
                      std::vector<std::vector<int64_t>>* tlist, bool members_only = false) {
-  HIPCHK(hipSetDevice(c->device));
+  DeviceGuard dg(c->device);
   std::vector<uint32_t> ext, tdesc;
   Problem q = build_query_problem(c->policy, ts, ext, tdesc);
   DevBuf ls_off, ls_key, ls_val, sel_off, reqs, req_vals, pod_ns, pod_ls, pod_nsls, pod_ip, cidrs, ipbs, ipb_ex, pms, pents,

@@ -75,8 +75,8 @@ static Selector decode_selector(const Node& n) {
   if (auto me = n.val("matchExpressions"); me && me->is_arr())
     for (auto& e : me->a) {
       Requirement r;
-      if (auto k = e.val("key")) r.key = k->str();
-      if (auto op = e.val("operator")) r.op = op->str();
+      if (auto k = e.sval("key")) r.key = k->str();
+      if (auto op = e.sval("operator")) r.op = op->str();
       if (auto vs = e.val("values"); vs && vs->is_arr())
         for (auto& v : vs->a) r.values.push_back(v.str());
       s.exprs.push_back(std::move(r));
@@ -223,7 +223,7 @@ struct Compiler {
       p.port = port;
       if (auto ib = from.val("ipBlock")) {  // selectors next to an ipBlock are ignored (:116-121)
         p.kind = PK_IP;
-        if (auto c = ib->val("cidr")) p.cidr = c->str();
+        if (auto c = ib->sval("cidr")) p.cidr = c->str();
         if (auto ex = ib->val("except"); ex && ex->is_arr()) {
           p.except_nil = false;
           for (auto& e : ex->a) p.except.push_back(e.str());
@@ -398,19 +398,19 @@ PolicyIR build_network_policies(const Node& netpols, bool simplify) {
   Compiler c;
   std::map<std::string, Target> dict[2];
   for_each_netpol(netpols, [&](const Node& pol) {
-    const Node* md = pol.val("metadata");
-    const Node* spec = pol.val("spec");
+    const Node* md = pol.sval("metadata");
+    const Node* spec = pol.sval("spec");
     std::string name, ns;
     if (md) {
-      if (auto n = md->val("name")) name = n->str();
-      if (auto n = md->val("namespace")) ns = n->str();
+      if (auto n = md->sval("name")) name = n->str();
+      if (auto n = md->sval("namespace")) ns = n->str();
     }
     if (ns.empty()) ns = "default";  // builder.go:28-33
     const Node* types = spec ? spec->val("policyTypes") : nullptr;
     if (!types || !types->is_arr() || types->a.empty())
       throw Panic{CYC_ERR_INVALID_POLICY, "invalid network policy: need at least 1 type"};  // :38-40
     Selector sel;
-    if (auto ps = spec->val("podSelector")) sel = decode_selector(*ps);
+    if (auto ps = spec->sval("podSelector")) sel = decode_selector(*ps);
     bool have[2] = {false, false};
     Target built[2];
     for (auto& t : types->a) {  // BuildTarget :35-61 (a repeated type rebuilds the same target)
@@ -545,7 +545,7 @@ PolicyIR load_policy_ir(const Node& root) {
         m.ports_nil = false;
         for (auto& p : ps->a) {
           PortEntry e;
-          if (auto pr = p.val("Protocol")) e.proto = pr->str();
+          if (auto pr = p.sval("Protocol")) e.proto = pr->str();
           if (auto po = p.val("Port")) {
             e.has_port = true;
             e.port = decode_intstr(*po);
@@ -557,9 +557,9 @@ PolicyIR load_policy_ir(const Node& root) {
         std::vector<PortRange> v;
         for (auto& r : rs->a) {
           PortRange pr;
-          if (auto x = r.val("From")) pr.from = int32_t(x->i64());
-          if (auto x = r.val("To")) pr.to = int32_t(x->i64());
-          if (auto x = r.val("Protocol")) pr.proto = x->str();
+          if (auto x = r.sval("From")) pr.from = int32_t(x->i64());
+          if (auto x = r.sval("To")) pr.to = int32_t(x->i64());
+          if (auto x = r.sval("Protocol")) pr.proto = x->str();
           v.push_back(pr);
         }
         ir.range_arrays.push_back(v);
@@ -575,7 +575,7 @@ PolicyIR load_policy_ir(const Node& root) {
     for (auto& kv : dict->o) {
       const Node& tn = kv.second;
       Target t;
-      if (auto ns = tn.val("Namespace")) t.ns = ns->str();
+      if (auto ns = tn.sval("Namespace")) t.ns = ns->str();
       if (auto ps = tn.val("PodSelector")) t.sel = decode_selector(*ps);
       t.pk = target_pk(t.ns, t.sel);
       if (auto sr = tn.val("SourceRules"); sr && sr->is_arr())
@@ -596,7 +596,7 @@ PolicyIR load_policy_ir(const Node& root) {
             p.port = load_port(pn.val("Port"));
           } else if (ty == "IPBlock") {
             p.kind = PK_IP;
-            if (auto c = pn.val("CIDR")) p.cidr = c->str();
+            if (auto c = pn.sval("CIDR")) p.cidr = c->str();
             if (auto ex = pn.val("Except"); ex && ex->is_arr()) {
               p.except_nil = false;
               for (auto& e : ex->a) p.except.push_back(e.str());
@@ -608,7 +608,7 @@ PolicyIR load_policy_ir(const Node& root) {
             const std::string nty = ns ? type_of(*ns) : std::string("all namespaces");
             if (nty == "specific namespace") {
               p.ns_kind = NS_EXACT;
-              if (auto x = ns->val("Namespace")) p.ns = x->str();
+              if (auto x = ns->sval("Namespace")) p.ns = x->str();
             } else if (nty == "matching namespace by label") {
               p.ns_kind = NS_LABEL;
               if (auto x = ns->val("Selector")) p.ns_sel = decode_selector(*x);
@@ -656,17 +656,17 @@ Resources load_resources(const Node& n) {
     r.pods.reserve(pods->a.size());
     for (auto& p : pods->a) {
       Pod pod;
-      if (auto x = p.val("Namespace")) pod.ns = x->str();
-      if (auto x = p.val("Name")) pod.name = x->str();
-      if (auto x = p.val("IP")) pod.ip = x->str();
+      if (auto x = p.sval("Namespace")) pod.ns = x->str();
+      if (auto x = p.sval("Name")) pod.name = x->str();
+      if (auto x = p.sval("IP")) pod.ip = x->str();
       decode_labels(p.val("Labels"), pod.labels_nil, pod.labels);
       if (auto cs = p.val("Containers"); cs && cs->is_arr())
         for (auto& c : cs->a) {
           Container ct;
-          if (auto x = c.val("Name")) ct.name = x->str();
-          if (auto x = c.val("Port")) ct.port = int32_t(x->i64());
-          if (auto x = c.val("Protocol")) ct.proto = x->str();
-          if (auto x = c.val("PortName")) ct.port_name = x->str();
+          if (auto x = c.sval("Name")) ct.name = x->str();
+          if (auto x = c.sval("Port")) ct.port = int32_t(x->i64());
+          if (auto x = c.sval("Protocol")) ct.proto = x->str();
+          if (auto x = c.sval("PortName")) ct.port_name = x->str();
           pod.conts.push_back(ct);
         }
       r.pods.push_back(std::move(pod));
@@ -679,12 +679,12 @@ std::vector<ProbeConfig> load_probes(const Node& n) {
   std::vector<ProbeConfig> out;
   auto one = [&](const Node& p) {
     ProbeConfig c;
-    if (auto a = p.val("AllAvailable"); a && a->t == Node::Bool && a->b) {
+    if (auto a = p.sval("AllAvailable"); a && a->t == Node::Bool && a->b) {
       c.all_available = true;
     } else {
       const Node* src = p.val("PortProtocol") ? p.val("PortProtocol") : &p;
       if (auto x = src->val("Port")) c.port = decode_intstr(*x);
-      if (auto x = src->val("Protocol")) c.proto = x->str();
+      if (auto x = src->sval("Protocol")) c.proto = x->str();
     }
     out.push_back(c);
   };
@@ -1178,10 +1178,10 @@ std::vector<QueryTraffic> load_traffics(const Node& n) {
   auto end = [](const Node* p) {
     QueryEnd e;
     if (!p) return e;
-    if (auto ip = p->val("IP")) e.ip = ip->str();
+    if (auto ip = p->sval("IP")) e.ip = ip->str();
     if (auto in = p->val("Internal")) {
       e.external = false;
-      if (auto ns = in->val("Namespace")) e.ns = ns->str();
+      if (auto ns = in->sval("Namespace")) e.ns = ns->str();
       bool nil;
       decode_labels(in->val("PodLabels"), nil, e.labels);
       decode_labels(in->val("NamespaceLabels"), nil, e.ns_labels);

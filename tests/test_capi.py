@@ -51,6 +51,18 @@ def test_json_depth_limit_and_last_key_wins():
     ir = e.build_policies(pol).policy_ir()
     ns = [t["Namespace"] for t in ir["Ingress"].values()]
     assert ns == ["b"], ir
+    # a JSON null leaves a scalar (or struct-valued) field unchanged: the last non-null key decides
+    # ({"namespace":"a","Namespace":null} is "a"); into a pointer / slice field null means nil
+    pol = [{"metadata": {"name": "p", "namespace": "a", "Namespace": None},
+            "spec": {"podSelector": {"matchLabels": {"x": "1"}}, "policyTypes": ["Ingress"], "PodSelector": None,
+                     "ingress": [{"from": [{"ipBlock": {"cidr": "10.0.0.0/8", "CIDR": None}}]}]}}]
+    ir = e.build_policies(pol).policy_ir()
+    (t,) = ir["Ingress"].values()
+    assert t["Namespace"] == "a" and t["PodSelector"]["matchLabels"] == {"x": "1"}, ir
+    assert t["Peers"][0]["CIDR"] == "10.0.0.0/8", ir
+    pol[0]["spec"]["ingress"][0]["From"] = None  # []NetworkPolicyPeer: null = nil, i.e. all peers
+    t2 = list(e.build_policies(pol).policy_ir()["Ingress"].values())[0]
+    assert t2["Peers"] != t["Peers"], (t, t2)
 
 
 def test_malformed_inputs_fail_cleanly():

@@ -318,6 +318,7 @@ def test_pm_class_rows_wave_and_items(gpu):
     tests/test_gpu_fullrows.py."""
     eng = Engine(0)
     seen_wave = 0
+    seen_plvt = [0, 0]  # runs without / with the per-pod label table
     problems = [_ip_interval_problem(s, n_pods=300 + 97 * s) for s in range(3)]
     problems += [random_problem(95_000 + s, n_pods=120) for s in range(40)]
     for n, (pols, res, probes) in enumerate(problems):
@@ -334,16 +335,22 @@ def test_pm_class_rows_wave_and_items(gpu):
         eng.set_option("pl_wave", 1)
         # sparse pod-peer rows a block per peer or a wave per chunk over peer groups, selectors
         # evaluated where used or as the dense table first
-        for grp, lazy, wave in ((1, 1, 1), (8, 0, 1), (3, 1, 0), (64, -1, 1), (2, 0, 0)):
+        # (per-pod label table PLVT, or pod -> label set -> LVT gathers when it is not built)
+        for grp, lazy, wave, plvt in ((1, 1, 1, 1024), (8, 0, 1, 0), (3, 1, 0, 0), (64, -1, 1, 1024), (2, 0, 0, 0),
+                                      (1, 1, 0, 0)):
             eng.set_option("pr_group", grp)
             eng.set_option("sel_lazy", lazy)
             eng.set_option("pl_wave", wave)  # sparse rows read per word (spans + chunk flags) or per chunk
-            assert_same(want, eng.run_host(), f"problem {n} pr_group={grp} sel_lazy={lazy} pl_wave={wave}")
+            eng.set_option("plvt_max_mb", plvt)
+            assert_same(want, eng.run_host(), f"problem {n} pr_group={grp} sel_lazy={lazy} pl_wave={wave} plvt={plvt}")
+            seen_plvt[eng.get_option("plvt_active")] += plvt == 0 or eng.get_option("plvt_active") == 1
+        eng.set_option("plvt_max_mb", 1024)
         eng.set_option("pr_group", -1)
         eng.set_option("sel_lazy", -1)
         eng.set_option("pl_wave", 1)
         seen_wave += eng.get_option("pl_wave_active")
     assert seen_wave >= 10
+    assert min(seen_plvt) >= 10, seen_plvt
 
 
 def _deployment_problem(seed, min_run=22):
@@ -604,3 +611,57 @@ def test_batch_cross_block_panic_isolated(gpu):
             want = Panicked(str(e))
         assert_same(want, Panicked(g.msg) if isinstance(g, CyclonusPanic) else g, blk["resources"]["Pods"][0]["Name"])
     assert isinstance(got[2], CyclonusPanic) and not isinstance(got[0], CyclonusPanic)
+
+
+def _long_class_problem(seed, n_peers=300, n_pods=260):
+    """One ingress target (and one egress target) whose peer list is longer than the class-row
+    kernel's LDS part (> 256 entries) on a PM build with 5-32 job slots: the entries past the LDS
+    part are read back from the spill list, each carrying its slot bits (they were read
+    as a port matcher id).  Peers are pod selectors of one label value each (so none merge under
+    Simplify), IPBlocks and ports-only rules, on numbered, named and ranged ports."""
+    rng = np.random.default_rng(seed)
+    ports = [(80, "TCP"), (81, "TCP"), (53, "UDP"), (443, "TCP"), (9000, "SCTP"), (8080, "TCP")]
+    pods = []
+    for q in range(n_pods):
+        conts = [{"Name": f"c{j}", "Port": p, "Protocol": pr, "PortName": f"serve-{p}-{pr.lower()}"}
+                 for j, (p, pr) in enumerate(ports)]
+        pods.append({"Namespace": "x" if q % 5 else "y", "Name": f"p{q}", "Labels": {"i": str(q % n_peers), "g": str(q % 3)},
+                     "IP": f"10.0.{q // 200}.{q % 200}", "Containers": conts})
+    res = {"Namespaces": {"x": {"ns": "x"}, "y": {"ns": "y"}}, "Pods": pods}
+    peers = []
+    for n in range(n_peers):
+        kind = rng.random()
+        if kind < 0.8:
+            peer = {"podSelector": {"matchLabels": {"i": str(n)}}}
+            if rng.random() < 0.3:
+                peer["namespaceSelector"] = {}
+        else:
+            peer = {"ipBlock": {"cidr": f"10.0.{int(rng.integers(0, 2))}.{int(rng.integers(0, 25)) * 8}/29"}}
+        peers.append(peer)
+    rules = []
+    for x in range(0, n_peers, 20):
+        p, pr = ports[int(rng.integers(0, len(ports)))]
+        port = [{"port": p, "protocol": pr}, {"port": f"serve-{p}-{pr.lower()}", "protocol": pr},
+                {"port": 80, "endPort": 444, "protocol": "TCP"}][int(rng.integers(0, 3))]
+        rules.append({"from": peers[x:x + 20], "ports": [port]})
+    pols = [{"metadata": {"name": "long", "namespace": "x"},
+             "spec": {"podSelector": {"matchLabels": {"g": "1"}}, "policyTypes": ["Ingress", "Egress"],
+                      "ingress": rules, "egress": [{"to": r["from"], "ports": r["ports"]} for r in rules]}}]
+    return pols, res, [{"AllAvailable": True}]
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_long_class_lists_pm_items(gpu, seed):
+    pols, res, probes = _long_class_problem(seed)
+    for simplify in (True, False):
+        want = Oracle(pols, res, simplify).probe(probes)
+        eng = Engine(0).build_policies(pols, simplify).load_resources(res)
+        sh = eng.prepare(probes)
+        assert 5 <= sh["slots"] <= 32, sh
+        eng.set_option("pod_words", 0)  # PM build: flattened peer lists in the class rows
+        for wave in (0, 1):  # pl_wave does not apply with 6 slots: both settings take the item walk
+            eng.set_option("pl_wave", wave)
+            assert eng.get_option("pl_wave_active") == 0
+            for fused in (1, 0):
+                eng.set_option("front_fused", fused)
+                assert_same(want, eng.run_host(), f"seed {seed} simplify {simplify} pl_wave {wave} fused {fused}")
