@@ -6,9 +6,11 @@
 A step is one full pass of the hot path over the synthetic workload with every input table
 already resident in HBM: selector evaluation, peer rows, port tables, target membership and
 class election, class rows, and the emit of both packed verdict planes (ingress keyed by
-destination, egress keyed by source) for this rank's rows.  N > 1 shards target-pod rows across
-ranks (one process per GPU, torch.distributed over RCCL for the barrier / max-time reduce only;
-there is no collective on the data path).  Rank 0 prints one JSON line.
+destination, egress keyed by source) for this rank's rows.  N > 1 shards the pods across ranks
+(one process per GPU, torch.distributed over RCCL for the barrier / max-time reduce only; there is
+no collective on the data path): --partition source (north_star: rank r owns source pods, i.e.
+every cell Table.Get(from = s, *) of its sources) or target (rank r owns the target rows of both
+planes).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -102,6 +104,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-assemble", action="store_true", help="skip the N>1 all-gather timing")
+    ap.add_argument("--partition", default="source", choices=["source", "target"],
+                    help="row partition across ranks (include/cyclonus_hip.h cyc_rows; the same at N=1)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="cyc_set_option tuning knob (diagnostics; results never change)")
     args = ap.parse_args()
@@ -110,7 +114,7 @@ def main():
     import torch
 
     from cyclonus_amd.engine import Engine
-    from cyclonus_amd.shard import row_range
+    from cyclonus_amd.shard import shard_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -133,27 +137,42 @@ def main():
             dist.barrier()
 
     data = load_workload(args.config)
+    # the drop-in's host cost (analyze --mode probe, pkg/cli/analyze.go:121, 232-243): policy build
+    # (BuildNetworkPolicies + Simplify), Resources load and cyc_probe_prepare (interning, job
+    # expansion, table upload) — paid once per probe model, outside `value`
+    pols_json, res_json = json.dumps(data["policies"]), json.dumps(data["resources"])
+    t_prep = time.perf_counter()
     eng = Engine(device)
     for o in args.opt:
         k, v = o.split("=")
         eng.set_option(k, int(v))
-    eng.build_policies(json.dumps(data["policies"]))
-    eng.load_resources(json.dumps(data["resources"]))
+    eng.build_policies(pols_json)
+    t_built = time.perf_counter()
+    eng.load_resources(res_json)
+    t_loaded = time.perf_counter()
     shape = eng.prepare(data["probes"])
+    torch.cuda.synchronize()
+    t_prepared = time.perf_counter()
+    prepare_s = {"policy_build_s": t_built - t_prep, "resources_load_s": t_loaded - t_built,
+                 "probe_prepare_s": t_prepared - t_loaded, "total_s": t_prepared - t_prep}
     P, K, W = shape["pods"], shape["slots"], shape["words"]
-    lo, hi = row_range(P, world, rank)
+    part = args.partition
+    lo, hi = shard_range(P, world, rank, part)
     rows = hi - lo
 
-    # shards differ by at most one row: every rank allocates the largest, so the optional
-    # all-gather (assembled table) moves the planes as they are
-    maxrows = max(b - a for a, b in (row_range(P, world, r) for r in range(world)))
-    d_in = torch.empty((max(maxrows, 1), K, W), dtype=torch.int64, device="cuda")
-    d_eg = torch.empty((max(maxrows, 1), K, W), dtype=torch.int64, device="cuda")
+    # shards differ by at most one row (target) / one 64-pod word (source): every rank allocates the
+    # largest, so the optional all-gather (assembled table) moves the planes as they are
+    lays = [eng.layout(*shard_range(P, world, r, part), part) for r in range(world)]
+    ri, wi, re_, we, w0 = lays[rank]
+    max_in = max(x[0] * x[1] for x in lays)
+    max_eg = max(x[2] * x[3] for x in lays)
+    d_in = torch.empty((max(max_in, 1) * K,), dtype=torch.int64, device="cuda")
+    d_eg = torch.empty((max(max_eg, 1) * K,), dtype=torch.int64, device="cuda")
     d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():
-        eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), stream, lo, hi)
+        eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), stream, lo, hi, part)
 
     for _ in range(args.warmup):
         step()
@@ -176,11 +195,12 @@ def main():
     assembled = None
     if dist is not None and not args.no_assemble:
         try:
-            out_in = torch.empty((world * maxrows, K, W), dtype=torch.int64, device="cuda" if backend == "nccl" else "cpu")
-            out_eg = torch.empty_like(out_in)
+            dev = "cuda" if backend == "nccl" else "cpu"
+            out_in = torch.empty((world * d_in.numel(),), dtype=torch.int64, device=dev)
+            out_eg = torch.empty((world * d_eg.numel(),), dtype=torch.int64, device=dev)
             src_in, src_eg = (d_in, d_eg) if backend == "nccl" else (d_in.cpu(), d_eg.cpu())
 
-            def gather():
+            def gather():  # one all-gather per plane of the padded shards (the relayout to [P][K][W] excluded)
                 for src, out in ((src_in, out_in), (src_eg, out_eg)):
                     if backend == "nccl":
                         dist.all_gather_into_tensor(out, src)
@@ -200,9 +220,8 @@ def main():
                               device="cuda" if backend == "nccl" else "cpu")
             dist.all_reduce(ga, op=dist.ReduceOp.MAX)
             ga = float(ga.item())
-            assembled = {"all_gather_ms": ga * 1e3,
-                         "bytes_received_per_rank": 2 * (world - 1) * maxrows * K * W * 8,
-                         "xgmi_GBs_per_rank": 2 * (world - 1) * maxrows * K * W * 8 / ga / 1e9}
+            recv = (world - 1) * (d_in.numel() + d_eg.numel()) * 8
+            assembled = {"all_gather_ms": ga * 1e3, "bytes_received_per_rank": recv, "xgmi_GBs_per_rank": recv / ga / 1e9}
             del out_in, out_eg
         except Exception as e:  # the assembled figure is informational; never lose the bench line
             assembled = {"error": f"{type(e).__name__}: {e}"}
@@ -238,6 +257,31 @@ def main():
         fills.append(e0.elapsed_time(e1))
     fill_gbs = (d_in.numel() + d_eg.numel()) * 8 / (min(fills) * 1e-3) / 1e9
 
+    # reading the table back (not part of `value`): Table.Get(from, *) of 64 sources through the
+    # device-resident table (cyc_table_cells: Ingress / Egress / Combined bytes to the host), and the
+    # packed planes' device-to-host copy rate
+    readback = None
+    try:
+        torch.cuda.synchronize()
+        tab = eng.wrap_table(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), lo, hi, part)
+        s_hi = min(hi, lo + 64)
+        t0 = time.perf_counter()
+        tab.cells(lo, s_hi, 0, P, 0, K)
+        tc = time.perf_counter() - t0
+        n_rb = min(d_in.numel(), 1 << 27)
+        host = torch.empty(n_rb, dtype=torch.int64, pin_memory=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        host.copy_(d_in[:n_rb], non_blocking=True)
+        torch.cuda.synchronize()
+        tp = time.perf_counter() - t0
+        readback = {"table_cells_64_sources_s": tc, "cells": (s_hi - lo) * P * K * 3,
+                    "planes_d2h_GBs": n_rb * 8 / tp / 1e9}
+        tab.close()
+        del host
+    except Exception as e:  # informational
+        readback = {"error": f"{type(e).__name__}: {e}"}
+
     status = d_st.cpu().numpy()
     if "batch" in data:  # only the cells inside each batched problem are answers
         cells = data["batch"].cells(status)
@@ -251,27 +295,42 @@ def main():
     # rows x K x W x 8 B per plane = 2 bits per cell — less the rows that already hold their class
     # row (in-place class rows, cyc_set_option class_inplace: one row per class and plane is written
     # by the class-row kernel, the emit copies it to the class's other rows)
-    launches = 1
+    # a source shard's planes differ in row length (ingress: every destination over the shard's
+    # words; egress: its sources over all words) and are emitted by one launch each
+    launches = 1 if (ri, wi) == (re_, we) else 2
     inplace = eng.get_option("class_inplace_active") == 1
-    emit_rows = 2 * rows - (classes_in + classes_eg if inplace else 0)
-    emit_bytes = emit_rows * K * W * 8
-    emit_launch_ms = emit_ms
+    emit_rows = ri + re_ - (classes_in + classes_eg if inplace else 0)
+    emit_bytes = (ri - (classes_in if inplace else 0)) * K * wi * 8 + (re_ - (classes_eg if inplace else 0)) * K * we * 8
+    emit_launch_ms = emit_ms  # both launches when there are two (HIP events around the emit phase)
     achieved = emit_bytes / (emit_launch_ms * 1e-3) / 1e9
-    # the emit kernel the library picks by plane-row length (engine.hip enq_emit)
-    row_bytes = K * W * 8
-    emit_kernel = ("k_emit_words (8-byte copies)" if (K * W) % 2 else
-                   "k_emit_wide<512,U> (one single-pass block per row)" if row_bytes >= 65536 else
-                   "k_emit_wide<256,U> (one single-pass block per row)" if row_bytes >= 16384 else
-                   "k_emit_flat (multi-row blocks)")
+
+    def kernel_of(words):  # the emit kernel the library picks by plane-row length (engine.hip enq_emit_launch)
+        row_bytes = K * words * 8
+        return ("k_emit_words (8-byte copies)" if (K * words) % 2 else
+                "k_emit_wide<512,U> (one single-pass block per row)" if row_bytes >= 65536 else
+                "k_emit_wide<256,U> (one single-pass block per row)" if row_bytes >= 16384 else
+                "k_emit_flat (multi-row blocks)")
+    emit_kernel = kernel_of(we) if launches == 1 else f"ingress {kernel_of(wi)}; egress {kernel_of(we)}"
 
     # HBM traffic of k_emit from the committed PMC passes for this same workload (rocprofv3
     # --pmc FETCH_SIZE / WRITE_SIZE, corrected per MI355X_MICROARCH.md; scripts/pmc_summary.py)
     # (the newest round's file); MFMA use from the same file's --pmc SQ_*MFMA* pass
+    # Only a profile of THIS library build is quoted: the PMC file records the sha256 of the library
+    # it profiled (scripts/pmc_summary.py --build-info); another build's counters give traffic null.
     traffic, traffic_src, mfma = None, None, None
     pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc_{args.config}.json")))
     if pmcs and world == 1:
+        from cyclonus_amd import _lib
+        from cyclonus_amd.build import lib_sha256
+
         pmc = json.load(open(pmcs[-1]))
-        traffic, traffic_src = pmc.get("emit_hbm_bytes_per_launch"), os.path.relpath(pmcs[-1], ROOT)
+        traffic_src = os.path.relpath(pmcs[-1], ROOT)
+        loaded = lib_sha256(_lib.SO_PATH)
+        if (pmc.get("build") or {}).get("lib_sha256") == loaded:
+            traffic = pmc.get("emit_hbm_bytes_per_launch")
+        else:
+            traffic_src = (f"{traffic_src} profiled library "
+                           f"{(pmc.get('build') or {}).get('lib_sha256', 'unrecorded')[:12]}, loaded {loaded[:12]}: not quoted")
         if pmc.get("mfma"):
             m = pmc["mfma"]
             mfma = {"insts_per_step": m["mfma_insts_per_step"], "busy_cycles_per_step": m["mfma_busy_cycles_per_step"],
@@ -305,7 +364,8 @@ def main():
                 "identities_eg": shape["classes_eg"],
                 "classes_in": classes_in,
                 "classes_eg": classes_eg,
-                "parallelism": f"target-row shards x{world}",
+                "parallelism": f"{part}-row shards x{world}",
+                "partition": part,
                 "rows_per_rank": rows,
             },
             "roofline": {
@@ -326,6 +386,8 @@ def main():
                 "mfma": mfma,
             },
             "launch": launch_desc,
+            "prepare_s": prepare_s,
+            "readback": readback,
             "pipeline_ms": {"total": pipe_ms, "emit": emit_ms, "class_rows": rows_ms, "front": pipe_ms - emit_ms - rows_ms},
         }
         if assembled is not None:

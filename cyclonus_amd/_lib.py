@@ -50,7 +50,16 @@ EXPORTS = [
     "cyc_table_shape",
     "cyc_table_error",
     "cyc_table_destroy",
+    "cyc_rows_layout",
+    "cyc_probe_run_rows",
+    "cyc_probe_run_host_rows",
+    "cyc_table_run_rows",
+    "cyc_table_wrap_rows",
 ]
+
+# cyc_rows (row partitions for one-process-per-GPU runs)
+ROWS_TARGET, ROWS_SOURCE = 0, 1
+PARTITIONS = {"target": ROWS_TARGET, "source": ROWS_SOURCE}
 
 
 class CyclonusError(RuntimeError):
@@ -115,6 +124,11 @@ def lib():
         L.cyc_table_error.restype = cp
         L.cyc_table_destroy.argtypes = [vp]
         L.cyc_table_destroy.restype = None
+        L.cyc_rows_layout.argtypes = [vp, i, i64, i64, ctypes.POINTER(i64), i]
+        L.cyc_probe_run_rows.argtypes = [vp, vp, vp, vp, vp, i, i64, i64]
+        L.cyc_probe_run_host_rows.argtypes = [vp, vp, vp, vp, i, i64, i64]
+        L.cyc_table_run_rows.argtypes = [vp, i, i64, i64, ctypes.POINTER(vp)]
+        L.cyc_table_wrap_rows.argtypes = [vp, vp, vp, vp, i, i64, i64, ctypes.POINTER(vp)]
         _lib = L
     return _lib
 

@@ -106,8 +106,40 @@ def build(verbose: bool = True, force: bool = False) -> str:
         objs.append(obj)
     if force or _newer(OUT, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs])
+    write_build_info()
     build_driver(force)
     return OUT
+
+
+BUILD_INFO = os.path.join(BUILD, "build_info.json")
+
+
+def lib_sha256(path: str = OUT) -> str:
+    import hashlib
+
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def write_build_info():
+    """Provenance of the built library (travels to the GPU box with it): the git head it was built
+    from (and whether the tree differed from it) and the library's sha256.  Profiles record it, and
+    bench.py quotes a profile's counters only for the same library."""
+    import json
+
+    info = {"lib_sha256": lib_sha256(OUT)}
+    try:
+        info["git_head"] = subprocess.run(["git", "-C", ROOT, "rev-parse", "HEAD"], capture_output=True, text=True,
+                                          check=True).stdout.strip()
+        info["git_dirty"] = bool(subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no"],
+                                                capture_output=True, text=True, check=True).stdout.strip())
+    except Exception:  # no git (e.g. on the GPU box): keep what the build host wrote
+        if os.path.exists(BUILD_INFO):
+            old = json.load(open(BUILD_INFO))
+            if old.get("lib_sha256") == info["lib_sha256"]:
+                return
+    with open(BUILD_INFO, "w") as f:
+        json.dump(info, f)
 
 
 if __name__ == "__main__":

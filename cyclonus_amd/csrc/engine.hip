@@ -310,11 +310,11 @@ template <bool ERR>
 __global__ __launch_bounds__(256) void k_pod_rows(uint32_t Rp, uint32_t E, uint32_t W, const uint32_t* __restrict__ pod_peers,
                                                   const uint8_t* __restrict__ ido, const uint32_t* __restrict__ word_off,
                                                   const uint32_t* __restrict__ run_e, const uint64_t* __restrict__ run_mask,
-                                                  uint64_t* __restrict__ PM, uint64_t* __restrict__ ER) {
-  uint32_t chunks = (W + 255) / 256;
+                                                  uint64_t* __restrict__ PM, uint64_t* __restrict__ ER, uint32_t w0, uint32_t nw) {
+  uint32_t chunks = (nw + 255) / 256;
   uint32_t p = blockIdx.x / chunks;
-  uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
-  if (p >= Rp || w >= W) return;
+  uint32_t w = w0 + (blockIdx.x % chunks) * 256 + threadIdx.x;
+  if (p >= Rp || w >= w0 + nw) return;
   const uint8_t* row = ido + uint64_t(p) * E;
   uint64_t m = 0, e = 0;
   for (uint32_t x = word_off[w]; x < word_off[w + 1]; x++) {
@@ -332,6 +332,7 @@ __global__ __launch_bounds__(256) void k_pod_rows(uint32_t Rp, uint32_t E, uint3
 // lane = pod, one ballot per word.  Used when identities are about as many as pods (every pod
 // labelled apart, e.g. a `pod: <name>` label): then the identity-space outcomes cost as much as
 // this and the run expansion above loops over up to 64 runs per word.
+// Words [w0, w0 + nw) of each row (a source shard's ingress peers: its word window).
 template <bool ERR>
 __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uint32_t W,
                                                          const uint32_t* __restrict__ pod_peers,
@@ -339,9 +340,10 @@ __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uin
                                                          uint32_t L, const uint32_t* __restrict__ pod_eid,
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                          const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
-                                                         uint64_t* __restrict__ ER, uint32_t bid_, uint32_t nblk_) {
+                                                         uint64_t* __restrict__ ER, uint32_t bid_, uint32_t nblk_, uint32_t w0,
+                                                         uint32_t nw) {
   const uint32_t lane = threadIdx.x & 63, gw = bid_ * 4 + (threadIdx.x >> 6);
-  const uint32_t p = gw / W, w = gw - p * W;
+  const uint32_t p = gw / nw, w = w0 + (gw - p * nw);
   if (p >= Rp) return;
   const uint32_t j = pod_peers[p];
   const DPeer pr = peers[j];
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P
                                                          uint32_t L, const uint32_t* __restrict__ pod_eid,
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                          const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
-                                                         uint64_t* __restrict__ ER) { pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, PM, ER, blockIdx.x, gridDim.x); }
+                                                         uint64_t* __restrict__ ER, uint32_t w0, uint32_t nw) { pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, PM, ER, blockIdx.x, gridDim.x, w0, nw); }
 
 // Pod-peer rows of the fused front on PM builds (no panic possible), stored sparse, 64-word chunks
 // at a time with lane = pod word (block shapes: pod_rows_sparse_blk).  The namespace
@@ -495,15 +497,15 @@ __device__ __forceinline__ void pod_rows_sparse_blk(uint32_t Rp, uint32_t P, uin
                                                     const uint32_t* __restrict__ pod_nsls, const uint32_t* __restrict__ pod_ls,
                                                     const DWordNS* __restrict__ nsw, uint64_t* __restrict__ PM,
                                                     uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t grp,
-                                                    uint32_t bid_) {
+                                                    uint32_t bid_, uint32_t c0, uint32_t nch) {
   __shared__ uint64_t s_m[4][64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t chunks = (W + 63) / 64, cb = (chunks + 3) / 4;
+  const uint32_t chunks = (W + 63) / 64, cb = (nch + 3) / 4;  // chunks [c0, c0 + nch) of each row
   const uint32_t x0 = (bid_ / cb) * grp;
   if (x0 >= Rp) return;  // whole block
   if (grp > 1) {
-    const uint32_t chunk = __builtin_amdgcn_readfirstlane((bid_ % cb) * 4 + wave);
-    if (chunk >= chunks) return;
+    const uint32_t chunk = __builtin_amdgcn_readfirstlane(c0 + (bid_ % cb) * 4 + wave);
+    if (chunk >= c0 + nch) return;
     const DWordNS ck = nsw[W + chunk];
     for (uint32_t x = x0; x < min(Rp, x0 + grp); x++) {
       const uint32_t j = plist[x];
@@ -520,8 +522,8 @@ __device__ __forceinline__ void pod_rows_sparse_blk(uint32_t Rp, uint32_t P, uin
   const uint32_t j = plist[x0];
   const DPeer pr = peers[j];
   for (uint32_t ci = 0; ci < 4; ci++) {
-    const uint32_t chunk = (bid_ % cb) * 4 + ci;  // block-uniform
-    if (chunk >= chunks) break;
+    const uint32_t chunk = c0 + (bid_ % cb) * 4 + ci;  // block-uniform
+    if (chunk >= c0 + nch) break;
     const DWordNS ck = nsw[W + chunk];
     if (pr.nskind == 0 && (pr.nsval < ck.lo || pr.nsval > ck.hi)) {
       if (threadIdx.x == 0) cnz[uint64_t(j) * chunks + chunk] = 0;
@@ -545,15 +547,17 @@ struct DIPTest {
   DCidr cidr;
 };
 
+// Words [w0, w0 + nw) of the rows only (a source shard's ingress peers: the shard's word window).
 template <bool ERR>
 __global__ __launch_bounds__(256) void k_ip_rows(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                  const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
-                                                 uint64_t* __restrict__ PM, uint64_t* __restrict__ ER, uint32_t batch) {
+                                                 uint64_t* __restrict__ PM, uint64_t* __restrict__ ER, uint32_t batch,
+                                                 uint32_t w0, uint32_t nw) {
   __shared__ DIPTest s_t[IPB_BATCH];
   __shared__ DCidr s_ex[IPB_EX_LDS];
-  const uint32_t wchunks = (W + 3) / 4;
+  const uint32_t wchunks = (nw + 3) / 4;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t w = (blockIdx.x % wchunks) * 4 + wave;
+  const uint32_t w = w0 + (blockIdx.x % wchunks) * 4 + wave;
   const uint32_t r0 = (blockIdx.x / wchunks) * batch;
   const uint32_t nr = min(Ri - r0, batch);
   const uint32_t ex0 = tests[r0].exoff;
@@ -561,7 +565,7 @@ __global__ __launch_bounds__(256) void k_ip_rows(uint32_t Ri, uint32_t P, uint32
   for (uint32_t t = threadIdx.x; t < nr; t += blockDim.x) s_t[t] = tests[r0 + t];
   for (uint32_t t = threadIdx.x; t < min(nex, IPB_EX_LDS); t += blockDim.x) s_ex[t] = ip_ex[ex0 + t];
   __syncthreads();
-  if (w >= W) return;
+  if (w >= w0 + nw) return;
   const uint32_t q = w * 64 + lane;
   DIP ip{};
   if (q < P) ip = pod_ip[q];
@@ -724,25 +728,26 @@ __device__ __forceinline__ uint64_t cnz_mask(const uint32_t* __restrict__ cnz, u
 // per block, instead of a chain of dependent scalar loads per peer and except), and each wave loads
 // its words' [min, max] records once for the whole group.
 constexpr uint32_t IP_GROUP = 16, IP_GROUP_MAX = 64, IP_EX_LDS = 256;  // 16: profiles/r02_ip_group_ab.txt
+// Chunks [c0, c0 + nch) of the rows (a source shard's ingress peers: the chunks of its word window).
 __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
                                                       uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t bid_, uint32_t nblk_,
-                                                      uint32_t grp = IP_GROUP) {
+                                                      uint32_t grp, uint32_t c0, uint32_t nch) {
   __shared__ DIPTest s_t[IP_GROUP_MAX];
   __shared__ DCidr s_ex[IP_EX_LDS];
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t chunks = (W + 63) / 64, cb = (chunks + 3) / 4;
+  const uint32_t cb = (nch + 3) / 4;
   const uint32_t r0 = (bid_ / cb) * grp;
   if (r0 >= Ri) return;  // whole block
-  const uint32_t nr = min(Ri - r0, grp), chunk = (bid_ % cb) * 4 + (threadIdx.x >> 6);
+  const uint32_t nr = min(Ri - r0, grp), chunk = c0 + (bid_ % cb) * 4 + (threadIdx.x >> 6);
   const uint32_t ex0 = tests[r0].exoff, nex = tests[r0 + nr - 1].exoff + tests[r0 + nr - 1].excnt - ex0;
   const bool ex_lds = nex <= IP_EX_LDS;
   for (uint32_t x = threadIdx.x; x < nr; x += blockDim.x) s_t[x] = tests[r0 + x];
   if (ex_lds)
     for (uint32_t x = threadIdx.x; x < nex; x += blockDim.x) s_ex[x] = ip_ex[ex0 + x];
   __syncthreads();
-  if (chunk >= chunks) return;
+  if (chunk >= c0 + nch) return;
   const uint32_t w = chunk * 64 + lane;
   const bool valid = w < W;
   DWordIP wd{};
@@ -764,13 +769,14 @@ __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32
 __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
-                                                      uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t grp) {
-  ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, cnz, blockIdx.x, gridDim.x, grp);
+                                                      uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t grp,
+                                                      uint32_t c0, uint32_t nch) {
+  ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, cnz, blockIdx.x, gridDim.x, grp, c0, nch);
 }
 
-// Grid of k_ip_rows_fast / the IP-row range of k_front_b: peer groups x blocks of 4 word chunks.
-__host__ __device__ inline uint64_t ip_rows_blocks(uint32_t Ri, uint32_t W, uint32_t grp) {
-  return uint64_t((Ri + grp - 1) / grp) * (((W + 63) / 64 + 3) / 4);
+// Grid of k_ip_rows_fast / an IP-row range of k_front_b: peer groups x blocks of 4 of the nch chunks.
+__host__ __device__ inline uint64_t ip_rows_blocks(uint32_t Ri, uint32_t nch, uint32_t grp) {
+  return uint64_t((Ri + grp - 1) / grp) * ((nch + 3) / 4);
 }
 
 // PortMatcher.Allows(ResolvedPort, ResolvedPortName, Protocol) — portmatcher.go:10-92, 190-199.
@@ -1064,6 +1070,9 @@ struct RowArgs {
   const uint32_t* portbits;  // fused IDO egress: portok row m as bits over descriptors (D <= 32), else null
   uint32_t D;
   uint32_t n_ident, K, W, P;
+  // the word window of the class rows: words [w0, w0 + WA) of each row (a source shard's ingress
+  // rows: its sources' words; otherwise 0, W); A rows hold WA words, word w at w - w0
+  uint32_t w0, WA;
   const uint32_t* reps;     // class representatives (k_classify)
   const uint32_t* rep_cnt;  // count = value + 1
   uint32_t rep_blocks;      // block rows of the grid; they stride over the representatives
@@ -1416,7 +1425,7 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
   for (int kk = 0; kk < KC; kk++) {
     uint32_t k = k0 + kk;
     if (k < a.K) {
-      uint64_t idx = (uint64_t(i) * a.K + k) * a.W + w;
+      uint64_t idx = (uint64_t(i) * a.K + k) * a.WA + (w - a.w0);
       a.A[idx] = allow[kk] & valid[kk];
       if (ERR) a.AE[idx] = err[kk] & valid[kk];
     }
@@ -1430,10 +1439,10 @@ template <bool EGRESS>
 __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
   constexpr int KC = 8;
   ht_clear_slice(a, blockIdx.x, gridDim.x);
-  const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
+  const uint32_t chunks = (a.WA + 255) / 256, nkc = (a.K + KC - 1) / KC;
   const uint32_t kc = (blockIdx.x / chunks) % nkc;
-  const uint32_t w = (blockIdx.x % chunks) * 256 + threadIdx.x;
-  if (w >= a.W) return;
+  const uint32_t w = a.w0 + (blockIdx.x % chunks) * 256 + threadIdx.x;
+  if (w >= a.w0 + a.WA) return;
   const uint32_t r = blockIdx.x / (chunks * nkc);
   if (r < *a.rep_cnt + 1u) class_row_word<EGRESS, true, KC>(a, a.reps[r], kc, w);
 }
@@ -1499,8 +1508,8 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
   for (int q = 0; q < NI; q++) {
     const uint32_t it = it0 + q * blockDim.x;
     const bool live = it < items;
-    const uint32_t kc = live ? it / a.W : 0u;
-    w[q] = live ? it - kc * a.W : 0u;
+    const uint32_t kc = live ? it / a.WA : 0u;
+    w[q] = a.w0 + (live ? it - kc * a.WA : 0u);
     k0[q] = live ? kc * KC : a.K;  // a dead item has no slot
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
@@ -1600,7 +1609,7 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
       const uint32_t k = k0[q] + kk;
-      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.W + w[q]] = allow[q][kk] & valid[q][kk];
+      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.WA + (w[q] - a.w0)] = allow[q][kk] & valid[q][kk];
     }
 }
 
@@ -1640,12 +1649,13 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
                                                uint32_t m, bool allow_all, uint64_t lastmask) {
   static_assert(PL_LDS % 64 == 0, "a lane group of entries is all in LDS or all spilled");
   const uint32_t lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
-  const uint32_t chunks = (a.W + 63) / 64;  // <= 64 (pl_wave_ok)
+  // the chunks holding the window's words (<= 64 chunks in all: pl_wave_ok)
+  const uint32_t cend = (a.w0 + a.WA + 63) / 64;
   const PlLane g0 = pl_lane(a, sh.e, lane, m);  // entries 0..63, one per lane, for every chunk
-  for (uint32_t c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < chunks; c += nwaves) {
+  for (uint32_t c = a.w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cend; c += nwaves) {
     const uint32_t w = c * 64 + lane;
-    const bool live = w < a.W;
-    const uint32_t wl = live ? w : a.W - 1;  // dead lanes load a valid word and store nothing
+    const bool live = w >= a.w0 && w < a.w0 + a.WA;
+    const uint32_t wl = live ? w : a.w0;  // dead lanes load a valid word and store nothing
     uint64_t valid[PL_NB];
     int32_t du[PL_NB];
 #pragma unroll
@@ -1709,7 +1719,7 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
           if (d < a.D) r |= acc[d] & dm[uint64_t(d) * a.W];
         r &= valid[k];
       }
-      a.A[(arow_of(a, i) * a.K + k) * a.W + w] = r;
+      a.A[(arow_of(a, i) * a.K + k) * a.WA + (w - a.w0)] = r;
     }
   }
 }
@@ -1718,7 +1728,7 @@ template <bool EGRESS, bool WAVE>
 __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
   ht_clear_slice(a, bid_, nblk_);
-  const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC, items = nkc * a.W;
+  const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC, items = nkc * a.WA;
   const bool kbits = EGRESS ? a.portbits != nullptr : a.K <= 32;
   for (uint32_t r = bid_; r < n_reps; r += nblk_) {
     const uint32_t i = a.reps[r];
@@ -1842,7 +1852,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   extern __shared__ uint64_t sB[];
   // block = (a.rpb consecutive class representatives, KC job slots, 256 pod words): the word's
   // runs and slot words are loaded once for all its representatives
-  const uint32_t chunks = (a.W + 255) / 256, nkc = (a.K + KC - 1) / KC;
+  const uint32_t chunks = (a.WA + 255) / 256, nkc = (a.K + KC - 1) / KC;
   const uint32_t kc = (bid_ / chunks) % nkc;
   const uint32_t r0 = (bid_ / (chunks * nkc)) * a.rpb, n_reps = *a.rep_cnt + 1u;
   if (r0 >= n_reps) return;  // whole block
@@ -1850,8 +1860,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   const uint32_t nrow = EGRESS ? a.NB : min(uint32_t(KC), a.K - k0), rowsz = nrow * a.EW;
   // the word's own loads (runs, slot words) are issued before the staging barrier, so their
   // latency overlaps the staging loads instead of following them
-  const uint32_t w = (bid_ % chunks) * 256 + threadIdx.x;
-  const bool live = w < a.W;
+  const uint32_t w = a.w0 + (bid_ % chunks) * 256 + threadIdx.x;
+  const bool live = w < a.w0 + a.WA;
   WordRuns wr{};
   if (live) wr = a.runs[w];
   const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
@@ -1935,7 +1945,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
       const uint32_t k = k0 + kk;
-      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.W + w] = allow[kk] & valid[kk];
+      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.WA + (w - a.w0)] = allow[kk] & valid[kk];
     }
   }
 }
@@ -1980,19 +1990,26 @@ __global__ __launch_bounds__(256) void k_front_a(FrontA f) {
   if (b < f.nb[3]) selectors_dense_blk(f.S, f.L, f.sel_off, f.dreqs, f.req_vals, f.LVT, f.selres, f.sel_list, b, f.nb[3]);
 }
 
+// Peer rows are built over a word window per direction: a source shard's ingress peers only over
+// its sources' words (chunks [c0, c0 + nch)), everything else over all words.  Segment x of the IP
+// rows and of the per-pod pod-peer rows is one direction's sub-list (target-row runs put both
+// directions into segment 0: one window).
 struct FrontB {
-  uint32_t nb[5];
+  uint32_t nb[7];       // IP rows x2 | pod-peer rows x2 (or identity sets, segment 2) | membership in | eg | port bits
   uint32_t ip_grp;      // IP rows: peers per wave
-  uint32_t pod_direct;  // PM builds with few pod-peer words: segment 1 = full pod-peer rows per pod
-                        // (pod_rows_direct_blk), else identity sets (IDO)
+  uint32_t pod_direct;  // PM builds with few pod-peer words: segments 2-3 = full pod-peer rows per pod
+                        // (pod_rows_direct_blk), else segment 2 = identity sets (IDO)
   SelView sv;           // IDO identity sets: selector outcomes (SELRES or evaluated where used)
-  uint32_t Rp;
-  const uint32_t *plist, *pod_eid;
+  uint32_t Rp[2];
+  const uint32_t* plist[2];
+  uint32_t pw0[2], pnw[2];  // per-pod pod-peer rows: word window per segment
+  const uint32_t* pod_eid;
   uint32_t M, D;
   const uint8_t* portok;
   uint32_t* portbits;
-  uint32_t Ri, P, W;
-  const DIPTest* tests;
+  uint32_t Ri[2], P, W;
+  const DIPTest* tests[2];
+  uint32_t ic0[2], inch[2];  // IP rows: chunk window per segment
   const DCidr* ip_ex;
   const DIP* pod_ip;
   const DWordIP* words;
@@ -2010,25 +2027,33 @@ struct FrontB {
 };
 __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   uint32_t b = blockIdx.x;
-  if (b < f.nb[0]) return ip_rows_fast_blk(f.Ri, f.P, f.W, f.tests, f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, f.cnz, b, f.nb[0], f.ip_grp);
-  b -= f.nb[0];
-  if (b < f.nb[1]) {
-    if (f.pod_direct)
-      return pod_rows_direct_blk<false>(f.Rp, f.P, f.W, f.plist, f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls, f.id_ls,
-                                        f.PM, nullptr, b, f.nb[1]);
-    return peer_bits_blk(f.Ru, f.E, f.EW, f.pod_peers_u, f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob, b, f.nb[1]);
+#pragma unroll
+  for (int x = 0; x < 2; x++) {
+    if (b < f.nb[x])
+      return ip_rows_fast_blk(f.Ri[x], f.P, f.W, f.tests[x], f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, f.cnz, b, f.nb[x], f.ip_grp,
+                              f.ic0[x], f.inch[x]);
+    b -= f.nb[x];
   }
-  b -= f.nb[1];
+#pragma unroll
+  for (int x = 0; x < 2; x++) {
+    if (b < f.nb[2 + x]) {
+      if (f.pod_direct)
+        return pod_rows_direct_blk<false>(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls,
+                                          f.id_ls, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
+      return peer_bits_blk(f.Ru, f.E, f.EW, f.pod_peers_u, f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob, b, f.nb[2 + x]);
+    }
+    b -= f.nb[2 + x];
+  }
 #pragma unroll
   for (int d = 0; d < 2; d++) {
-    if (b < f.nb[2 + d]) {
-      if (f.member_wave[d]) member_wave_blk(f.ma[d], b, f.nb[2 + d]);
-      else member_blk(f.ma[d], b, f.nb[2 + d]);
+    if (b < f.nb[4 + d]) {
+      if (f.member_wave[d]) member_wave_blk(f.ma[d], b, f.nb[4 + d]);
+      else member_blk(f.ma[d], b, f.nb[4 + d]);
       return;
     }
-    b -= f.nb[2 + d];
+    b -= f.nb[4 + d];
   }
-  if (b < f.nb[4]) portbits_blk(f.M, f.D, f.portok, f.portbits, b);  // for the egress class rows
+  if (b < f.nb[6]) portbits_blk(f.M, f.D, f.portok, f.portbits, b);  // for the egress class rows
 }
 
 // Pod-peer rows from posting lists: a pod selector that is ONE requirement `k = v` or `k in (v0,
@@ -2044,13 +2069,14 @@ __device__ __forceinline__ void pod_rows_post_blk(uint32_t P, uint32_t W, const 
                                                   const uint4* __restrict__ req_post, const uint32_t* __restrict__ post_pods,
                                                   const uint32_t* __restrict__ pod_ns, const uint32_t* __restrict__ pod_nsls,
                                                   uint64_t* __restrict__ PM, uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz,
-                                                  uint32_t bid_) {
+                                                  uint32_t bid_, uint32_t c0, uint32_t nch) {
   __shared__ unsigned long long s_row[PR_POST_WORDS];
   const uint32_t j = plist[bid_];
   const DPeer pr = peers[j];
   const uint4 pp = req_post[sv.sel_off[pr.podsel]];  // (offset, count) of value 0, then of value 1
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, chunks = (W + 63) / 64;
-  for (uint32_t w0 = 0; w0 < W; w0 += PR_POST_WORDS) {
+  // chunks [c0, c0 + nch) of the row (a source shard's ingress peers: the chunks of its word window)
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, chunks = c0 + nch;
+  for (uint32_t w0 = c0 * 64; w0 < min(W, chunks * 64); w0 += PR_POST_WORDS) {
     for (uint32_t x = threadIdx.x; x < PR_POST_WORDS; x += blockDim.x) s_row[x] = 0;
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < pp.y + pp.w; e += blockDim.x) {
@@ -2073,19 +2099,21 @@ __device__ __forceinline__ void pod_rows_post_blk(uint32_t P, uint32_t W, const 
 // and precede the class rows): the light class election keeps them off launch B, whose IP rows and
 // membership would otherwise run at the pod rows' register budget (occupancy 8 -> 5-7).
 struct FrontC {
-  uint32_t nb[4];
+  uint32_t nb[6];  // class election in | eg | sparse pod-peer rows x2 | posting-built rows x2
   MemberArgs ma[2];
   uint32_t* class_of[2];
-  // sparse pod-peer rows (pod_rows_sparse_blk over plist, then pod_rows_post_blk over plist_post)
-  uint32_t Rp, P, W, pr_grp;
-  const uint32_t* plist;
+  // sparse pod-peer rows (pod_rows_sparse_blk over plist, then pod_rows_post_blk over plist_post),
+  // one segment per word window (ingress peers of a source shard / the rest)
+  uint32_t Rp[2], P, W, pr_grp;
+  const uint32_t* plist[2];
+  uint32_t c0[2], nch[2];
   const DPeer* peers;
   SelView sv;
   const uint32_t *pod_ns, *pod_nsls, *pod_ls;
   const DWordNS* nsw;  // per word, then per chunk: namespace ranges
   uint64_t* PM;
   uint32_t *rng, *cnz;
-  const uint32_t* plist_post;  // pod peers whose rows come from label postings (pod_rows_post_blk)
+  const uint32_t* plist_post[2];  // pod peers whose rows come from label postings (pod_rows_post_blk)
   const uint4* req_post;
   const uint32_t* post_pods;
 };
@@ -2095,11 +2123,20 @@ __global__ __launch_bounds__(256) void k_front_c(FrontC f) {
   b -= f.nb[0];
   if (b < f.nb[1]) return classify_blk(f.ma[1], f.class_of[1], b, f.nb[1]);
   b -= f.nb[1];
-  if (b < f.nb[2])
-    return pod_rows_sparse_blk(f.Rp, f.P, f.W, f.plist, f.peers, f.sv, f.pod_ns, f.pod_nsls, f.pod_ls, f.nsw, f.PM, f.rng, f.cnz,
-                               f.pr_grp, b);
-  b -= f.nb[2];
-  pod_rows_post_blk(f.P, f.W, f.plist_post, f.peers, f.sv, f.req_post, f.post_pods, f.pod_ns, f.pod_nsls, f.PM, f.rng, f.cnz, b);
+#pragma unroll
+  for (int x = 0; x < 2; x++) {
+    if (b < f.nb[2 + x])
+      return pod_rows_sparse_blk(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.sv, f.pod_ns, f.pod_nsls, f.pod_ls, f.nsw, f.PM, f.rng,
+                                 f.cnz, f.pr_grp, b, f.c0[x], f.nch[x]);
+    b -= f.nb[2 + x];
+  }
+#pragma unroll
+  for (int x = 0; x < 2; x++) {
+    if (b < f.nb[4 + x])
+      return pod_rows_post_blk(f.P, f.W, f.plist_post[x], f.peers, f.sv, f.req_post, f.post_pods, f.pod_ns, f.pod_nsls, f.PM, f.rng,
+                               f.cnz, b, f.c0[x], f.nch[x]);
+    b -= f.nb[4 + x];
+  }
 }
 
 struct FrontRows {
@@ -2145,20 +2182,21 @@ __global__ __launch_bounds__(256) CYC_E_WAVES void k_front_e(FrontRows f) {
 // plain / sc1 stores, address-linear fill-like segments, per-plane launches —
 // profiles/r01_emit_*.txt.)
 struct EmitArgs {
-  uint32_t n_rows;            // pods in [row_lo, row_hi) per plane
-  uint32_t row_lo;
-  uint32_t per_xcd;           // rows of the 2 * n_rows row list per XCD segment
+  uint32_t n_rows[2];         // plane rows of this launch (pods [row_lo, row_lo + n_rows)); 0 = plane not in it
+  uint32_t row_lo[2];
+  uint32_t per_xcd;           // rows of the n_rows[0] + n_rows[1] row list per XCD segment
   const uint32_t* order[2];   // pods in [row_lo,row_hi) clustered by the plane's class
   const uint32_t *pod_id[2], *class_of[2];
   const uint64_t* A[2];
   const uint32_t* arow[2];    // in-place class rows (RowArgs::arow): the class row is a row of out
   uint64_t* out[2];
-  uint64_t row_words;         // K * W
+  uint64_t row_words;         // words per plane row, the same for every row of a launch (K * W, or
+                              // K * window words for a source shard's ingress rows)
   uint32_t chunk;             // k_emit_flat: rows per block
   const uint8_t* st_src;      // job status plane [P][K] (the run's third output), copied by the
   uint8_t* st_dst;            // emit's blocks in slices: no separate copy node ends the step
   uint64_t st_bytes;
-  uint32_t interleave;        // the row list alternates ingress / egress rows
+  uint32_t interleave;        // the row list alternates ingress / egress rows (n_rows equal)
 };
 
 // Row r of the row list -> (plane, pod).
@@ -2167,8 +2205,8 @@ __device__ __forceinline__ void emit_row_of(const EmitArgs& a, uint32_t r, uint3
     pl = r & 1u;
     p = a.order[pl][r >> 1];
   } else {
-    pl = r >= a.n_rows ? 1u : 0u;
-    p = a.order[pl][r - pl * a.n_rows];
+    pl = r >= a.n_rows[0] ? 1u : 0u;
+    p = a.order[pl][r - pl * a.n_rows[0]];
   }
 }
 
@@ -2178,7 +2216,7 @@ __device__ __forceinline__ const uint64_t* emit_src(const EmitArgs& a, uint32_t 
   const uint32_t c = a.class_of[pl][a.pod_id[pl][p]];
   if (!a.arow[pl]) return a.A[pl] + uint64_t(c) * a.row_words;
   const uint32_t r = a.arow[pl][c];
-  return r == p - a.row_lo ? nullptr : a.out[pl] + uint64_t(r) * a.row_words;
+  return r == p - a.row_lo[pl] ? nullptr : a.out[pl] + uint64_t(r) * a.row_words;
 }
 
 // Block b's slice of the status plane copy (every emit kernel calls this first).
@@ -2195,12 +2233,12 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
   emit_status(a);
   const uint32_t b = blockIdx.x, x = b & 7, r = x * a.per_xcd + (b >> 3);
-  if (r >= min(2 * a.n_rows, (x + 1) * a.per_xcd)) return;
+  if (r >= min(a.n_rows[0] + a.n_rows[1], (x + 1) * a.per_xcd)) return;
   uint32_t pl, p;
   emit_row_of(a, r, pl, p);
   const uint64_t* src = emit_src(a, pl, p);
   if (!src) return;
-  uint64_t* dst = a.out[pl] + uint64_t(p - a.row_lo) * a.row_words;
+  uint64_t* dst = a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.row_words;
   for (uint64_t i = threadIdx.x; i < a.row_words; i += blockDim.x) dst[i] = src[i];
 }
 
@@ -2214,7 +2252,7 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   emit_status(a);
   __shared__ const u64x2* s_src[EMIT_FLAT_MAX_ROWS];
   __shared__ u64x2* s_dst[EMIT_FLAT_MAX_ROWS];
-  const uint32_t b = blockIdx.x, n = a.n_rows * 2, x = b & 7;
+  const uint32_t b = blockIdx.x, n = a.n_rows[0] + a.n_rows[1], x = b & 7;
   const uint32_t r0 = x * a.per_xcd + (b >> 3) * a.chunk;
   const uint32_t r_end = min(n, (x + 1) * a.per_xcd);
   if (r0 >= r_end) return;
@@ -2227,7 +2265,7 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
     uint32_t pl, p;
     emit_row_of(a, r0 + threadIdx.x, pl, p);
     src = reinterpret_cast<const u64x2*>(emit_src(a, pl, p));
-    dst = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
+    dst = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.row_words);
   }
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t keep = __ballot(src != nullptr);
@@ -2265,14 +2303,14 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
 template <int BS, int UNROLL>
 __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   emit_status(a);
-  const uint32_t b = blockIdx.x, n = a.n_rows * 2, x = b & 7;
+  const uint32_t b = blockIdx.x, n = a.n_rows[0] + a.n_rows[1], x = b & 7;
   const uint32_t r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
   if (r >= min(n, (x + 1) * a.per_xcd)) return;
   uint32_t pl, p;
   emit_row_of(a, r, pl, p);
   const u64x2* si = reinterpret_cast<const u64x2*>(emit_src(a, pl, p));
   if (!si) return;  // in-place class row: already written
-  u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo) * a.row_words);
+  u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.row_words);
   const uint32_t n2 = uint32_t(a.row_words / 2);
   for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS * UNROLL) {
     u64x2 v[UNROLL];
@@ -2289,6 +2327,8 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
 struct ErrArgs {
   uint32_t P, K, W, n_cfg;
   uint32_t row_lo, row_hi;
+  uint32_t src;                    // source-row run: rows [row_lo, row_hi) are sources for both directions
+  uint32_t w0, WA;                 // ingress class rows' word window (RowArgs)
   const uint8_t* slot_status;  // [P][K]
   const uint32_t *slot_cfg, *slot_idx;
   const uint32_t *pod_iid, *pod_eid, *class_in, *class_eg;
@@ -2307,8 +2347,9 @@ __global__ __launch_bounds__(256) void k_first_error(ErrArgs a) {
     const uint32_t s = uint32_t(b / chunks);
     const uint32_t d = uint32_t(b % chunks) * blockDim.x + threadIdx.x;
     if (d >= a.P) continue;
-    // only the directions whose rows this run computes (the whole table when [lo,hi) = [0,P))
-    const bool din = d >= a.row_lo && d < a.row_hi, sin = s >= a.row_lo && s < a.row_hi;
+    // only the directions whose rows this run computes (the whole table when [lo,hi) = [0,P)); a
+    // source-row run computes both directions of its sources' cells
+    const bool sin = s >= a.row_lo && s < a.row_hi, din = a.src ? sin : d >= a.row_lo && d < a.row_hi;
     if (!din && !sin) continue;
     const bool s_err = sin && a.err_eg[a.pod_eid[s]];
     const bool d_err = din && a.err_in[a.pod_iid[d]];
@@ -2318,7 +2359,7 @@ __global__ __launch_bounds__(256) void k_first_error(ErrArgs a) {
     for (uint32_t k = 0; k < a.K; k++) {
       if (a.slot_status[uint64_t(d) * a.K + k] != CYC_JOB_VALID) continue;
       bool e = d_err || s_err;
-      if (!e && din && a.AE_in) e = (a.AE_in[(uint64_t(ci) * a.K + k) * a.W + s / 64] >> (s % 64)) & 1;
+      if (!e && din && a.AE_in) e = (a.AE_in[(uint64_t(ci) * a.K + k) * a.WA + (s / 64 - a.w0)] >> (s % 64)) & 1;
       if (!e && sin && a.AE_eg) e = (a.AE_eg[(uint64_t(ce) * a.K + k) * a.W + d / 64] >> (d % 64)) & 1;
       if (!e) continue;
       const uint32_t kc = a.slot_cfg[k];
@@ -2467,6 +2508,7 @@ __global__ void k_query(QueryArgs a) {
 // get the fixed results of jobrunner.go:36-55; slots without a job are CYC_CONN_NO_JOB.
 struct CellArgs {
   uint32_t K, W, row_lo, row_hi;
+  uint32_t src, w0, WA;      // source-row table: ingress rows of every destination over words [w0, w0 + WA)
   const uint64_t *in, *eg;   // planes of rows [row_lo, row_hi) (layout: include/cyclonus_hip.h)
   const uint8_t* status;     // [P][K]
   uint32_t s_lo, d_lo, k_lo, nd, nk;
@@ -2482,7 +2524,8 @@ __global__ __launch_bounds__(256) void k_table_cells(CellArgs a) {
     uint8_t ci = CYC_CONN_NO_JOB, ce = CYC_CONN_NO_JOB, cc = CYC_CONN_NO_JOB;
     if (st == CYC_JOB_VALID) {
       // the host checked that the requested planes cover these rows
-      const bool ai = a.o_in || a.o_comb ? (a.in[(uint64_t(d - a.row_lo) * a.K + k) * a.W + s / 64] >> (s % 64)) & 1 : false;
+      const uint64_t iw = a.src ? (uint64_t(d) * a.K + k) * a.WA + (s / 64 - a.w0) : (uint64_t(d - a.row_lo) * a.K + k) * a.W + s / 64;
+      const bool ai = a.o_in || a.o_comb ? (a.in[iw] >> (s % 64)) & 1 : false;
       const bool ae = a.o_eg || a.o_comb ? (a.eg[(uint64_t(s - a.row_lo) * a.K + k) * a.W + d / 64] >> (d % 64)) & 1 : false;
       ci = ai ? CYC_CONN_ALLOWED : CYC_CONN_BLOCKED;
       ce = ae ? CYC_CONN_ALLOWED : CYC_CONN_BLOCKED;
@@ -2673,10 +2716,17 @@ struct cyc_ctx {
     hipEvent_t done;  // null: never launched
   };
   std::vector<Retired> retired;
-  const void* graph_key[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  const void* graph_key[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool timed_graph = false;
   DirDev dir[2];
   int64_t order_lo = -1, order_hi = -1;
+  bool order_src = false;  // the range plan partitions sources (CYC_ROWS_SOURCE), not target rows
+  // the current plan: plane rows per direction (ingress keyed by destination, egress by source) and
+  // the ingress word window (a source shard's sources: its peers' rows and class rows cover only
+  // those words); target-row plans: both directions [lo, hi), window [0, W)
+  int64_t rl[2] = {0, 0}, rh[2] = {0, 0};
+  uint32_t win_w0 = 0, win_wa = 0;
+  uint32_t scan_off[3] = {0, 0, 0}, post_off[3] = {0, 0, 0};  // pp_scan / pp_post: ingress peers, then egress
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   double last_ms[3] = {0, 0, 0};
   bool timed = false;  // the last run recorded the step timing events
@@ -2685,6 +2735,7 @@ struct cyc_ctx {
 };
 
 int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t idx);
+static bool rows_layout(const cyc_ctx* c, int part, int64_t lo, int64_t hi, int64_t v[5], std::string& why);
 
 static int fail(cyc_ctx* c, int code, const std::string& m) {
   if (c) c->err = m;
@@ -3023,6 +3074,7 @@ static void prepare_device(cyc_ctx* c) {
     }
   }
   c->order_lo = c->order_hi = -1;
+  c->order_src = false;
 }
 
 // nonzero-chunk flags of the IP peers' PM rows, after the word spans and chunk masks in the ip_rng buffer
@@ -3123,12 +3175,23 @@ static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c
 // only their classes are elected and their class rows computed; (3) the peers of the targets
 // in those identities' namespaces — only their PM rows are built.  A rank of an N-GPU run thus
 // does ~1/N of the front work too, not just 1/N of the emit.
-static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
-  if (c->order_lo == lo && c->order_hi == hi) return;
+// Source-row plans (src): rows [lo, hi) are SOURCES; the run computes every cell (s in [lo, hi), d,
+// k): egress rows of sources [lo, hi) (full rows) and the ingress rows of EVERY destination, but
+// only their words [lo / 64, ceil(hi / 64)) — the shard's sources as peers.  lo must be a multiple
+// of 64 and hi too unless it is P (checked by the caller), so the windows of a partition tile the words.
+static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
+  if (c->order_lo == lo && c->order_hi == hi && c->order_src == src) return;
   Problem& pb = c->pb;
+  c->rl[0] = src ? 0 : lo;
+  c->rh[0] = src ? int64_t(pb.P) : hi;
+  c->rl[1] = lo;
+  c->rh[1] = hi;
+  c->win_w0 = src ? uint32_t(lo / 64) : 0u;
+  c->win_wa = src ? uint32_t((hi + 63) / 64 - lo / 64) : pb.W;
+  if (src && hi <= lo) c->win_wa = 0;
   for (int d = 0; d < 2; d++) {  // emit row order: clustered by this direction's identity
-    std::vector<uint32_t> ord(size_t(hi - lo));
-    std::iota(ord.begin(), ord.end(), uint32_t(lo));
+    std::vector<uint32_t> ord(size_t(c->rh[d] - c->rl[d]));
+    std::iota(ord.begin(), ord.end(), uint32_t(c->rl[d]));
     const auto& i1 = c->ids[d].of_pod;
     const auto& i2 = c->ids[1 - d].of_pod;
     std::stable_sort(ord.begin(), ord.end(),
@@ -3142,7 +3205,8 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
     const Identities& I = c->ids[d];
     std::vector<uint8_t> used(I.ns.size(), 0);
     std::vector<uint32_t> act;
-    for (int64_t p = lo; p < hi; p++) {
+    const bool empty_window = d == 0 && c->win_wa == 0;  // a source shard without sources: no ingress words
+    for (int64_t p = c->rl[d]; p < c->rh[d] && !empty_window; p++) {
       uint32_t i = I.of_pod[size_t(p)];
       if (!used[i]) {
         used[i] = 1;
@@ -3152,7 +3216,7 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
     std::sort(act.begin(), act.end());
     {  // each active identity's first pod in the range: its plane row holds the class row in place
       std::vector<uint32_t> ar(I.ns.size(), 0xFFFFFFFFu);
-      for (int64_t p = hi - 1; p >= lo; p--) ar[I.of_pod[size_t(p)]] = uint32_t(p - lo);
+      for (int64_t p = c->rh[d] - 1; p >= c->rl[d]; p--) ar[I.of_pod[size_t(p)]] = uint32_t(p - c->rl[d]);
       upload(c->arow[d], ar);
     }
     std::vector<uint8_t> ns_needed(pb.strings.size(), 0);
@@ -3177,7 +3241,7 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   for (int d = 0; d < 2; d++) {  // targets of active namespaces (also those without peers)
     const Identities& I = c->ids[d];
     std::vector<uint8_t> ns_needed(pb.strings.size(), 0);
-    for (int64_t p = lo; p < hi; p++) ns_needed[I.ns[I.of_pod[size_t(p)]]] = 1;
+    for (int64_t p = c->rl[d]; p < c->rh[d]; p++) ns_needed[I.ns[I.of_pod[size_t(p)]]] = 1;
     for (const DTarget& t : pb.tgt[d])
       if (ns_needed[t.ns]) sel_needed[t.sel] = 1;
   }
@@ -3191,15 +3255,22 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
     if (sel_needed[i]) sl.push_back(i);
   c->n_sel = uint32_t(sl.size());
   {  // sparse pod rows: peers whose pod selector is one posting requirement are built from postings
+    // (ingress peers first, then egress: each sub-list has its direction's word window)
     std::vector<uint32_t> scan, post;
-    for (uint32_t j : c->plan.pod_peers) {
-      if (!peer_needed[j]) continue;
-      const DPeer& pr = pb.peers[j];
-      if (pr.nskind == NS_ALL && pr.podsel == CYC_ALL) continue;  // all-ones row: the class rows need none
-      const bool one = pr.podsel != CYC_ALL && pb.sel_off[pr.podsel + 1] - pb.sel_off[pr.podsel] == 1;
-      if (one && c->dense_sel && !c->req_post_ok.empty() && c->req_post_ok[pb.sel_off[pr.podsel]]) post.push_back(j);
-      else scan.push_back(j);
+    for (int d = 0; d < 2; d++) {
+      c->scan_off[d] = uint32_t(scan.size());
+      c->post_off[d] = uint32_t(post.size());
+      for (uint32_t j : c->plan.pod_peers) {
+        if (!peer_needed[j] || peer_dir[j] != d) continue;
+        const DPeer& pr = pb.peers[j];
+        if (pr.nskind == NS_ALL && pr.podsel == CYC_ALL) continue;  // all-ones row: the class rows need none
+        const bool one = pr.podsel != CYC_ALL && pb.sel_off[pr.podsel + 1] - pb.sel_off[pr.podsel] == 1;
+        if (one && c->dense_sel && !c->req_post_ok.empty() && c->req_post_ok[pb.sel_off[pr.podsel]]) post.push_back(j);
+        else scan.push_back(j);
+      }
     }
+    c->scan_off[2] = uint32_t(scan.size());
+    c->post_off[2] = uint32_t(post.size());
     c->n_scan = uint32_t(scan.size());
     c->n_post = uint32_t(post.size());
     upload(c->pp_scan, scan);
@@ -3248,7 +3319,23 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi) {
   upload(c->ip_ex, c->plan.ip_ex);
   c->order_lo = lo;
   c->order_hi = hi;
+  c->order_src = src;
 }
+
+// Word window of direction d's peer rows in the current plan: [w0, w0 + nw); as 64-word chunks
+// [c0, c0 + nch).
+static void peer_window(const cyc_ctx* c, int d, uint32_t& w0, uint32_t& nw) {
+  w0 = d == 0 ? c->win_w0 : 0u;
+  nw = d == 0 ? c->win_wa : c->pb.W;
+}
+static void peer_chunks(const cyc_ctx* c, int d, uint32_t& c0, uint32_t& nch) {
+  uint32_t w0, nw;
+  peer_window(c, d, w0, nw);
+  c0 = w0 / 64;
+  nch = nw ? (w0 + nw + 63) / 64 - c0 : 0u;
+}
+// the two directions' peer rows share one window (target-row plans): one launch segment for both
+static bool one_window(const cyc_ctx* c) { return c->win_w0 == 0 && c->win_wa == c->pb.W; }
 
 // Pipeline pieces.  Steps 1, 3, 4 are shared; steps 2 and 5-7 run per direction (ingress peers,
 // targets, class rows and plane are disjoint from egress ones), so the two directions can run
@@ -3300,8 +3387,16 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
   Problem& pb = c->pb;
   const uint32_t P = pb.P, W = pb.W;
   const uint32_t E = c->dir[1].n;
-  // d = 2: both directions in one launch (their peer sub-lists are adjacent)
+  // d = 2: both directions in one launch (their peer sub-lists are adjacent) when they share a window
+  if (d == 2 && !one_window(c)) {
+    enq_peer_rows(c, 0, st, which);
+    enq_peer_rows(c, 1, st, which);
+    return;
+  }
   const int dlo = d == 2 ? 0 : d, dhi = d == 2 ? 2 : d + 1;
+  uint32_t w0, nw, c0, nch;  // the rows' word window (a source shard's ingress peers: its sources' words)
+  peer_window(c, d == 2 ? 1 : d, w0, nw);
+  peer_chunks(c, d == 2 ? 1 : d, c0, nch);
   const uint32_t r0 = c->rp_off[dlo], Rp = (which & PEERS_POD) ? c->rp_off[dhi] - r0 : 0u;
   if (Rp && E && W && ido_mode(c)) {
     const uint32_t EW = (E + 63) / 64;
@@ -3310,48 +3405,48 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
         Ru, E, EW, c->pod_peers_u.as<uint32_t>() + u0, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
         c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(),
         c->idob.as<uint64_t>() + uint64_t(u0) * EW);
-  } else if (Rp && E && W && (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= P)) {
+  } else if (Rp && E && nw && (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= P)) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
-    const unsigned g = unsigned((uint64_t(Rp) * W + 3) / 4);
+    const unsigned g = unsigned((uint64_t(Rp) * nw + 3) / 4);
     const uint32_t* eid = c->dir[1].pod_id.as<uint32_t>();
     if (pb.may_err)
       k_pod_rows_direct<true><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
                                                  c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(),
-                                                 c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
+                                                 c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
     else
       k_pod_rows_direct<false><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
                                                   c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(),
-                                                  c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
-  } else if (Rp && E && W) {
+                                                  c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
+  } else if (Rp && E && nw) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
     uint8_t* ido = c->ido.as<uint8_t>() + uint64_t(r0) * E;
     k_peer_ident<<<grid1(uint64_t(Rp) * E, 256), 256, 0, st>>>(Rp, E, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(),
                                                                pb.L, c->dir[1].id_ns.as<uint32_t>(),
                                                                c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(), ido);
-    unsigned g = unsigned(uint64_t((W + 255) / 256) * Rp);
+    unsigned g = unsigned(uint64_t((nw + 255) / 256) * Rp);
     if (pb.may_err)
       k_pod_rows<true><<<g, 256, 0, st>>>(Rp, E, W, plist, ido, c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(),
-                                          c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
+                                          c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
     else
       k_pod_rows<false><<<g, 256, 0, st>>>(Rp, E, W, plist, ido, c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(),
-                                           c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>());
+                                           c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
   }
   const uint32_t i0 = c->ri_off[dlo], Ri = (which & PEERS_IP) ? c->ri_off[dhi] - i0 : 0u;
-  if (Ri && W) {
+  if (Ri && nw) {
     const DIPTest* tests = c->ip_tests.as<DIPTest>() + i0;
     if (pb.may_err) {
       // batch size: as many peers per block as keep >= ~2048 blocks in flight, at most IPB_BATCH
-      const uint64_t wch = (W + 3) / 4;
+      const uint64_t wch = (nw + 3) / 4;
       const uint64_t nb_want = (2048 + wch - 1) / wch;
       const uint32_t bat = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(IPB_BATCH, (Ri + nb_want - 1) / nb_want)));
       unsigned g = unsigned(wch * ((Ri + bat - 1) / bat));
       k_ip_rows<true><<<g, 256, 0, st>>>(Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->PM.as<uint64_t>(),
-                                         c->ER.as<uint64_t>(), bat);
+                                         c->ER.as<uint64_t>(), bat, w0, nw);
     } else {
       const uint32_t grp = c->ip_group;
-      k_ip_rows_fast<<<unsigned(ip_rows_blocks(Ri, W, grp)), 256, 0, st>>>(
+      k_ip_rows_fast<<<unsigned(ip_rows_blocks(Ri, nch, grp)), 256, 0, st>>>(
           Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>(),
-          c->ip_rng.as<uint32_t>(), ip_cnz(c), grp);
+          c->ip_rng.as<uint32_t>(), ip_cnz(c), grp, c0, nch);
     }
   }
 }
@@ -3407,6 +3502,7 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.K = K;
   ra.W = W;
   ra.P = P;
+  peer_window(c, d, ra.w0, ra.WA);  // the class rows cover their peers' word window
   ra.class_of = dd.class_of.as<uint32_t>();
   ra.cnt = dd.cnt.as<uint32_t>();
   ra.list_off = dd.list_off.as<uint32_t>();
@@ -3455,8 +3551,9 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   DirDev& dd = c->dir[d];
   if (!dd.n || !K || !W || !c->n_act[d]) return;
   RowArgs ra = row_args(c, d);
+  if (!ra.WA) return;
   if (pb.may_err) {  // the ordered walk with panic bits: one block row per identity, 8 slots per thread
-    const unsigned g = unsigned(uint64_t((W + 255) / 256) * ((K + 7) / 8) * ra.rep_blocks);
+    const unsigned g = unsigned(uint64_t((ra.WA + 255) / 256) * ((K + 7) / 8) * ra.rep_blocks);
     if (d == 0) k_class_rows<false><<<g, 256, 0, st>>>(ra);
     else k_class_rows<true><<<g, 256, 0, st>>>(ra);
   } else if (ido_mode(c)) {
@@ -3468,7 +3565,7 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     const uint32_t rows = d == 0 ? std::min<uint32_t>(4, K) : D;
     const size_t per = size_t(rows) * ra.EW * 8;
     ra.rpb = class_rpb(c, per);
-    const unsigned gi = unsigned(uint64_t((W + 255) / 256) * ((K + 3) / 4) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
+    const unsigned gi = unsigned(uint64_t((ra.WA + 255) / 256) * ((K + 3) / 4) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
     if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
     else k_class_rows_ido<true, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
   } else {  // per-class flattened peer lists (the IP word spans are final here)
@@ -3480,40 +3577,19 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   }
 }
 
-// 7. the emit: both planes (ingress rows to out_in, egress rows to out_eg) in one launch.
-// d_status (may be null): the status plane, copied by the emit's blocks.  Returns false if no
-// emit was launched (no rows in the range; the caller then copies the status plane itself).
-static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, int64_t lo, int64_t hi,
-                     uint8_t* d_status, bool inplace = false) {
-  Problem& pb = c->pb;
-  const uint32_t K = pb.K, W = pb.W;
-  if (hi <= lo || !K || !W) return false;
-  EmitArgs ea{};
-  ea.st_src = c->slot_status.as<uint8_t>();
-  ea.st_dst = d_status;
-  ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
-  ea.n_rows = uint32_t(hi - lo);
-  ea.row_lo = uint32_t(lo);
-  // alternate the planes' rows when each plane is >= 8 GB (config #3 on one GPU: emit 3.42 ->
-  // 3.11 ms on two of three boxes, -1 % on the third; 1-4 % slower for planes of <= 5 GB — 2, 4
-  // and 8 shards — profiles/r01_emit_interleave_sweep.txt)
-  ea.interleave = uint64_t(ea.n_rows) * K * W * 8 >= (8ull << 30) ? 1u : 0u;
-  for (uint32_t pl = 0; pl < 2; pl++) {
-    ea.order[pl] = c->order[pl].as<uint32_t>();
-    ea.pod_id[pl] = c->dir[pl].pod_id.as<uint32_t>();
-    ea.class_of[pl] = c->dir[pl].class_of.as<uint32_t>();
-    ea.A[pl] = c->dir[pl].A.as<uint64_t>();
-    ea.arow[pl] = inplace ? c->arow[pl].as<uint32_t>() : nullptr;
-  }
-  ea.out[0] = out_in;
-  ea.out[1] = out_eg;
-  ea.row_words = uint64_t(K) * W;
-  ea.per_xcd = (ea.n_rows * 2 + 7) / 8;
+// 7. the emit: both planes (ingress rows to out_in, egress rows to out_eg) in one launch — two
+// when their rows differ in length (a source shard: ingress rows of every destination over the
+// shard's word window, egress rows of its sources over all words).  d_status (may be null): the
+// status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
+// in the plan; the caller then copies the status plane itself).
+static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out_in, uint64_t* out_eg) {
+  EmitArgs ea = ea_in;
+  ea.per_xcd = (ea.n_rows[0] + ea.n_rows[1] + 7) / 8;
   const bool aligned = reinterpret_cast<uintptr_t>(out_in) % 16 == 0 && reinterpret_cast<uintptr_t>(out_eg) % 16 == 0;
   const unsigned g = ea.per_xcd * 8;  // one block per row slot of the 8 XCD segments
   if (ea.row_words % 2 || !aligned) {
     k_emit_words<<<g, 256, 0, st>>>(ea);
-    return true;
+    return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
   if (row_bytes >= 65536) {  // 512-thread single pass: smallest UNROLL covering the row (16 = two passes)
@@ -3536,6 +3612,50 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   } else {  // flat multi-row sweep over ~32 KB per block
     ea.chunk = uint32_t(std::min<uint64_t>(EMIT_FLAT_MAX_ROWS, std::max<uint64_t>(1, 32768 / row_bytes)));
     k_emit_flat<8><<<(ea.per_xcd + ea.chunk - 1) / ea.chunk * 8, 256, 0, st>>>(ea);
+  }
+}
+
+static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, uint8_t* d_status, bool inplace = false) {
+  Problem& pb = c->pb;
+  const uint32_t K = pb.K;
+  const uint64_t rw[2] = {uint64_t(K) * c->win_wa, uint64_t(K) * pb.W};  // words per plane row
+  uint32_t nr[2];
+  for (int d = 0; d < 2; d++) nr[d] = rw[d] ? uint32_t(c->rh[d] - c->rl[d]) : 0u;
+  if (!nr[0] && !nr[1]) return false;
+  EmitArgs ea{};
+  ea.st_src = c->slot_status.as<uint8_t>();
+  ea.st_dst = d_status;
+  ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
+  for (uint32_t pl = 0; pl < 2; pl++) {
+    ea.row_lo[pl] = uint32_t(c->rl[pl]);
+    ea.order[pl] = c->order[pl].as<uint32_t>();
+    ea.pod_id[pl] = c->dir[pl].pod_id.as<uint32_t>();
+    ea.class_of[pl] = c->dir[pl].class_of.as<uint32_t>();
+    ea.A[pl] = c->dir[pl].A.as<uint64_t>();
+    ea.arow[pl] = inplace ? c->arow[pl].as<uint32_t>() : nullptr;
+  }
+  ea.out[0] = out_in;
+  ea.out[1] = out_eg;
+  if (rw[0] == rw[1] && nr[0] == nr[1]) {  // target rows: both planes in one launch
+    ea.n_rows[0] = ea.n_rows[1] = nr[0];
+    ea.row_words = rw[0];
+    // alternate the planes' rows when each plane is >= 8 GB (config #3 on one GPU: emit 3.42 ->
+    // 3.11 ms on two of three boxes, -1 % on the third; 1-4 % slower for planes of <= 5 GB — 2, 4
+    // and 8 shards — profiles/r01_emit_interleave_sweep.txt)
+    ea.interleave = uint64_t(nr[0]) * rw[0] * 8 >= (8ull << 30) ? 1u : 0u;
+    enq_emit_launch(ea, st, out_in, out_eg);
+    return true;
+  }
+  bool first = true;
+  for (int pl = 0; pl < 2; pl++) {  // rows of different lengths: one launch per plane
+    if (!nr[pl]) continue;
+    EmitArgs e1 = ea;
+    e1.n_rows[0] = pl == 0 ? nr[0] : 0u;  // the row list is [plane 0 rows][plane 1 rows]
+    e1.n_rows[1] = pl == 1 ? nr[1] : 0u;
+    e1.row_words = rw[pl];
+    if (!first) e1.st_bytes = 0;
+    first = false;
+    enq_emit_launch(e1, st, pl == 0 ? out_in : reinterpret_cast<uint64_t*>(16), pl == 1 ? out_eg : reinterpret_cast<uint64_t*>(16));
   }
   return true;
 }
@@ -3560,7 +3680,7 @@ static bool front_fused_ok(const cyc_ctx* c) {
 // planes, write slower (config #3: 2 % of the rows, net +1 %: profiles/r02_class_inplace_ab.txt).
 static bool inplace_ok(const cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg) {
   if (!c->class_inplace || !d_in || !d_eg || !front_fused_ok(c)) return false;
-  const uint64_t rows = uint64_t(std::max<int64_t>(c->order_hi - c->order_lo, 1));
+  const uint64_t rows = uint64_t(std::max<int64_t>((c->rh[0] - c->rl[0] + c->rh[1] - c->rl[1]) / 2, 1));
   return c->class_inplace == 1 || uint64_t(c->n_act[0] + c->n_act[1]) * 16 >= 2 * rows;
 }
 
@@ -3608,12 +3728,12 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fa.sel_list = c->sel_list.as<uint32_t>();
   fa.nb[3] = uint64_t(c->n_sel) * pb.L && !lazy_sel(c) ? blocks(uint64_t(c->n_sel) * ((pb.L + 256 * SEL_LPT - 1) / (256 * SEL_LPT))) : 0u;
   // B: IP rows | pod-peer identity sets (both directions' adjacent sub-lists) | membership x 2
+  // Segments x = 0, 1 of the IP rows and per-pod pod rows: the directions' sub-lists with their own
+  // word windows (source shards), or both directions in segment 0 (one window)
+  const bool one_win = one_window(c);
   FrontB fb{};
-  const uint32_t i0 = c->ri_off[0], Ri = c->ri_off[2] - i0;
-  fb.Ri = Ri;
   fb.P = P;
   fb.W = W;
-  fb.tests = c->ip_tests.as<DIPTest>() + i0;
   fb.ip_ex = c->ip_ex.as<DCidr>();
   fb.pod_ip = c->pod_ip.as<DIP>();
   fb.words = c->ip_words.as<DWordIP>();
@@ -3621,7 +3741,14 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.rng = c->ip_rng.as<uint32_t>();
   fb.cnz = ip_cnz(c);
   fb.ip_grp = c->ip_group;
-  fb.nb[0] = Ri ? blocks(ip_rows_blocks(Ri, W, fb.ip_grp)) : 0u;
+  for (int x = 0; x < 2; x++) {
+    const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
+    const uint32_t i0 = c->ri_off[dlo];
+    fb.Ri[x] = one_win && x ? 0u : c->ri_off[dhi] - i0;
+    fb.tests[x] = c->ip_tests.as<DIPTest>() + i0;
+    peer_chunks(c, one_win ? 1 : x, fb.ic0[x], fb.inch[x]);
+    fb.nb[x] = fb.Ri[x] && fb.inch[x] ? blocks(ip_rows_blocks(fb.Ri[x], fb.inch[x], fb.ip_grp)) : 0u;
+  }
   const uint32_t Rp = c->rp_off[2] - c->rp_off[0], u0 = c->rpu_off[0], Ru = c->rpu_off[2] - u0;
   fb.Ru = Ru;
   fb.E = E;
@@ -3635,22 +3762,23 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.id_ls = c->dir[1].id_ls.as<uint32_t>();
   fb.idob = c->idob.as<uint64_t>() + uint64_t(u0) * EW;
   fb.sv = sel_view(c);
-  fb.nb[1] = (Rp && E) ? blocks((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4) : 0u;
+  fb.nb[2] = (Rp && E) ? blocks((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4) : 0u;  // identity sets
   const bool ido = ido_mode(c);
   FrontC fc{};
   if (!ido && !pod_sparse(c)) {  // PM builds, few pod-peer words: full rows, a wave per (pod peer, word)
     fb.pod_direct = 1;
-    fb.Rp = Rp;
-    fb.plist = c->pod_peers.as<uint32_t>() + c->rp_off[0];
     fb.pod_eid = c->dir[1].pod_id.as<uint32_t>();
-    fb.nb[1] = (Rp && E) ? blocks((uint64_t(Rp) * W + 3) / 4) : 0u;
+    for (int x = 0; x < 2; x++) {
+      const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
+      fb.Rp[x] = one_win && x ? 0u : c->rp_off[dhi] - c->rp_off[dlo];
+      fb.plist[x] = c->pod_peers.as<uint32_t>() + c->rp_off[dlo];
+      peer_window(c, one_win ? 1 : x, fb.pw0[x], fb.pnw[x]);
+      fb.nb[2 + x] = (fb.Rp[x] && E && fb.pnw[x]) ? blocks((uint64_t(fb.Rp[x]) * fb.pnw[x] + 3) / 4) : 0u;
+    }
   } else if (!ido) {  // PM builds: sparse pod-peer rows in launch C (k_front_c)
-    fb.nb[1] = 0;
-    fc.Rp = c->n_scan;
+    fb.nb[2] = 0;
     fc.P = P;
     fc.W = W;
-    fc.plist = c->pp_scan.as<uint32_t>();
-    fc.plist_post = c->pp_post.as<uint32_t>();
     fc.req_post = c->req_post.as<uint4>();
     fc.post_pods = c->post_pods.as<uint32_t>();
     fc.peers = c->peers.as<DPeer>();
@@ -3664,10 +3792,22 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fc.cnz = ip_cnz(c);
     // a wave per chunk over groups of 8 peers once that fills the chip (>= 64k peer chunks:
     // config #3u 2.6 vs 3.2 ms), else the 4 waves of a block share each chunk (config #2)
-    const uint64_t cb = ((W + 63) / 64 + 3) / 4;
-    fc.pr_grp = c->pr_group > 0 ? uint32_t(c->pr_group) : (uint64_t(fc.Rp) * ((W + 63) / 64) >= 65536 ? 8u : 1u);
-    fc.nb[2] = (fc.Rp && E) ? blocks((uint64_t(fc.Rp) + fc.pr_grp - 1) / fc.pr_grp * cb) : 0u;
-    fc.nb[3] = E ? c->n_post : 0u;  // a block per posting-built peer
+    uint64_t peer_chunks_all = 0;
+    for (int x = 0; x < 2; x++) {
+      const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
+      fc.Rp[x] = one_win && x ? 0u : c->scan_off[dhi] - c->scan_off[dlo];
+      fc.plist[x] = c->pp_scan.as<uint32_t>() + c->scan_off[dlo];
+      fc.plist_post[x] = c->pp_post.as<uint32_t>() + c->post_off[dlo];
+      peer_chunks(c, one_win ? 1 : x, fc.c0[x], fc.nch[x]);
+      peer_chunks_all += uint64_t(fc.Rp[x]) * fc.nch[x];
+    }
+    fc.pr_grp = c->pr_group > 0 ? uint32_t(c->pr_group) : (peer_chunks_all >= 65536 ? 8u : 1u);
+    for (int x = 0; x < 2; x++) {
+      const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
+      const uint64_t cb = (fc.nch[x] + 3) / 4;
+      fc.nb[2 + x] = (fc.Rp[x] && E && cb) ? blocks((uint64_t(fc.Rp[x]) + fc.pr_grp - 1) / fc.pr_grp * cb) : 0u;
+      fc.nb[4 + x] = E && fc.nch[x] && !(one_win && x) ? c->post_off[dhi] - c->post_off[dlo] : 0u;  // a block per posting-built peer
+    }
   }
   FrontRows fd{}, fe{};
   size_t lds = 0;
@@ -3677,7 +3817,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fc.ma[d] = fb.ma[d];
     fc.class_of[d] = c->dir[d].class_of.as<uint32_t>();
     fb.member_wave[d] = c->member_wave > 0 || (c->member_wave < 0 && na <= 4096 && c->act_targets[d] >= 4.0);
-    fb.nb[2 + d] = na ? blocks(fb.member_wave[d] ? (uint64_t(na) + 3) / 4 : (uint64_t(na) + 255) / 256) : 0u;
+    fb.nb[4 + d] = na ? blocks(fb.member_wave[d] ? (uint64_t(na) + 3) / 4 : (uint64_t(na) + 255) / 256) : 0u;
     fc.nb[d] = na ? blocks((uint64_t(na) + 255) / 256) : 0u;
     if (!na) continue;
     fd.ra[d] = row_args(c, d);  // its blocks empty the direction's hash table for the next run
@@ -3695,7 +3835,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + 3) / 4) + 3) / 4);
     const size_t per = size_t(d == 0 ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8;
     fe.ra[d].rpb = class_rpb(c, per);
-    fe.nb[d] = blocks(uint64_t((W + 255) / 256) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
+    fe.nb[d] = blocks(uint64_t((fe.ra[d].WA + 255) / 256) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
     lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
   const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
@@ -3704,13 +3844,15 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.D = D;
   fb.portok = c->portok.as<uint8_t>();
   fb.portbits = c->portbits.as<uint32_t>();
-  fb.nb[4] = bits ? blocks((uint64_t(M) + 255) / 256) : 0u;
+  fb.nb[6] = bits ? blocks((uint64_t(M) + 255) / 256) : 0u;
   fe.ra[1].portbits = bits && fe.nb[1] ? c->portbits.as<uint32_t>() : nullptr;
-  const uint64_t gb = uint64_t(fb.nb[0]) + fb.nb[1] + fb.nb[2] + fb.nb[3] + fb.nb[4];
-  if (!fits) return false;
+  uint64_t gb = 0, gc = 0;
+  for (uint32_t x : fb.nb) gb += x;
+  for (uint32_t x : fc.nb) gc += x;
+  if (!fits || gb >= (1ull << 31) || gc >= (1ull << 31)) return false;
   if (ga) k_front_a<<<unsigned(ga), 256, 0, st>>>(fa);
   if (gb) k_front_b<<<unsigned(gb), 256, 0, st>>>(fb);
-  if (fc.nb[0] + fc.nb[1] + fc.nb[2] + fc.nb[3]) k_front_c<<<fc.nb[0] + fc.nb[1] + fc.nb[2] + fc.nb[3], 256, 0, st>>>(fc);
+  if (gc) k_front_c<<<unsigned(gc), 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
     if (fd.nb[0] + fd.nb[1] && pl_wave_ok(c)) k_front_d_pm<true><<<fd.nb[0] + fd.nb[1], pl_threads(c), 0, st>>>(fd);
@@ -3728,8 +3870,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
 
 // Eager launch, in phase order with the timing events: [0] start, [1] after the front (peer
 // rows, classes), [2] after the class rows, [3] after both emits.
-static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
-                             int64_t hi) {
+static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status) {
   Problem& pb = c->pb;
   HIPCHK(hipEventRecord(c->ev[0], st));
   const bool ip = inplace_ok(c, d_in, d_eg);
@@ -3742,7 +3883,7 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
     for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
     HIPCHK(hipEventRecord(c->ev[2], st));
   }
-  const bool status_done = enq_emit(c, st, d_in, d_eg, lo, hi, d_status, ip && fused);
+  const bool status_done = enq_emit(c, st, d_in, d_eg, d_status, ip && fused);
   HIPCHK(hipEventRecord(c->ev[3], st));
   if (!status_done && d_status && uint64_t(pb.P) * pb.K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
@@ -3753,11 +3894,11 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
 // st, egress on st2) pod-peer sets -> membership / classes -> (wait for st3) class rows, joined
 // into one emit of both planes (fork / join through events, graph dependencies when captured).
 static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStream_t st3, uint64_t* d_in, uint64_t* d_eg,
-                             uint8_t* d_status, int64_t lo, int64_t hi) {
+                             uint8_t* d_status) {
   Problem& pb = c->pb;
   const bool ip = inplace_ok(c, d_in, d_eg);
   if (front_fused_ok(c) && enq_front_fused(c, st, nullptr, nullptr, ip ? d_in : nullptr, ip ? d_eg : nullptr)) {
-    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status, ip)) return;
+    if (enq_emit(c, st, d_in, d_eg, d_status, ip)) return;
   } else {
     HIPCHK(hipEventRecord(c->fork_ev, st));
     HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
@@ -3777,7 +3918,7 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
     HIPCHK(hipEventRecord(c->join_ev, st2));
     HIPCHK(hipStreamWaitEvent(st, c->join_ev, 0));
     // the emit also writes the status plane; the copy node below only ends steps without rows
-    if (enq_emit(c, st, d_in, d_eg, lo, hi, d_status)) return;
+    if (enq_emit(c, st, d_in, d_eg, d_status)) return;
   }
   // The step always ends with the status-plane copy (into a sink buffer when the caller passed no
   // status pointer), so every captured graph has the same shape: one node after the join.
@@ -3825,13 +3966,16 @@ static void ensure_cap_streams(cyc_ctx* c) {
 
 // allow_capture = false: never capture a graph for this run (cyc_table_run's planes are new on
 // every call, so a captured graph would be re-instantiated each time): graphs = 1 runs as 2.
+// src: rows [lo, hi) are a source shard (CYC_ROWS_SOURCE), else target rows.
 static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
-                        int64_t hi, bool allow_capture = true) {
+                        int64_t hi, bool allow_capture = true, bool src = false) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W;
   if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
-  if (c->order_lo != lo || c->order_hi != hi) drop_graph(c);  // range plan buffers are re-made
-  ensure_range(c, lo, hi);
+  if (src && (lo % 64 || (hi % 64 && hi != int64_t(P))))
+    return fail(c, CYC_ERR_ARG, "source rows: row_lo must be a multiple of 64, row_hi too unless it is the pod count");
+  if (c->order_lo != lo || c->order_hi != hi || c->order_src != src) drop_graph(c);  // range plan buffers are re-made
+  ensure_range(c, lo, hi, src);
   if (!c->plvt_ready && front_fused_ok(c) && pod_sparse(c)) {
     drop_graph(c);  // a graph captured without the per-pod table would keep the slower gathers
     ensure_plvt(c, st);
@@ -3843,20 +3987,21 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     // joins them back before the emit (events), without hipGraphLaunch's per-replay latency
     ensure_cap_streams(c);
     if (c->step_events) HIPCHK(hipEventRecord(c->ev[0], st));
-    capture_pipeline(c, st, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status, lo, hi);
+    capture_pipeline(c, st, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status);
     if (c->step_events) HIPCHK(hipEventRecord(c->ev[3], st));
     c->timed = c->step_events != 0;
     c->timed_graph = true;
   } else if (graphs && !pb.may_err) {
     // The whole pipeline as one hipGraph (captured once per output buffers / row range):
     // removes the host launch cost of ~16 launches per run (dominant on small problems).
-    const void* key[5] = {d_in, d_eg, d_status, reinterpret_cast<void*>(lo), reinterpret_cast<void*>(hi)};
+    const void* key[6] = {d_in, d_eg, d_status, reinterpret_cast<void*>(lo), reinterpret_cast<void*>(hi),
+                          reinterpret_cast<void*>(intptr_t(src))};
     if (!c->graph_exec || memcmp(key, c->graph_key, sizeof(key)) != 0) {
       drop_graph(c);
       ensure_cap_streams(c);
       hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
-      capture_pipeline(c, c->cap_stream, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status, lo, hi);
+      capture_pipeline(c, c->cap_stream, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status);
       HIPCHK(hipStreamEndCapture(c->cap_stream, &g));
       c->graph = g;  // destroyed with the exec (drop_graph / reap_graphs)
       HIPCHK(hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
@@ -3870,7 +4015,7 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     c->timed = c->step_events != 0;
     c->timed_graph = true;
   } else {
-    enqueue_pipeline(c, st, d_in, d_eg, d_status, lo, hi);
+    enqueue_pipeline(c, st, d_in, d_eg, d_status);
     c->timed = true;
     c->timed_graph = false;
   }
@@ -3892,6 +4037,9 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     e.n_cfg = pb.n_cfg;
     e.row_lo = uint32_t(lo);
     e.row_hi = uint32_t(hi);
+    e.src = src ? 1u : 0u;
+    e.w0 = c->win_w0;
+    e.WA = c->win_wa;
     e.slot_status = c->slot_status.as<uint8_t>();
     e.slot_cfg = c->slot_cfg.as<uint32_t>();
     e.slot_idx = c->slot_idx.as<uint32_t>();
@@ -4146,37 +4294,50 @@ int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* s
   });
 }
 
-int cyc_probe_run(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo, int64_t hi) {
+int cyc_probe_run_rows(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int part, int64_t lo,
+                       int64_t hi) {
   if (!c) return CYC_ERR_ARG;
   if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
   if ((!d_in || !d_eg) && hi > lo) return fail(c, CYC_ERR_ARG, "null output plane");
+  if (part != CYC_ROWS_TARGET && part != CYC_ROWS_SOURCE) return fail(c, CYC_ERR_ARG, "unknown partition");
   return guarded(c, [&] {
     DeviceGuard dg(c->device);
     hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the HIP default (null) stream
-    return run_pipeline(c, st, d_in, d_eg, d_status, lo, hi);
+    return run_pipeline(c, st, d_in, d_eg, d_status, lo, hi, true, part == CYC_ROWS_SOURCE);
   });
 }
 
-int cyc_probe_run_host(cyc_ctx* c, uint64_t* h_in, uint64_t* h_eg, uint8_t* h_status, int64_t lo, int64_t hi) {
+int cyc_probe_run(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo, int64_t hi) {
+  return cyc_probe_run_rows(c, stream, d_in, d_eg, d_status, CYC_ROWS_TARGET, lo, hi);
+}
+
+int cyc_probe_run_host_rows(cyc_ctx* c, uint64_t* h_in, uint64_t* h_eg, uint8_t* h_status, int part, int64_t lo, int64_t hi) {
   if (!c) return CYC_ERR_ARG;
   if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
-  return guarded(c, [&] {
+  return guarded(c, [&]() -> int {
     DeviceGuard dg(c->device);
-    uint64_t rows = uint64_t(std::max<int64_t>(hi - lo, 0));
-    uint64_t words = rows * c->pb.K * c->pb.W;
+    int64_t v[5];
+    std::string why;
+    if (!rows_layout(c, part, lo, hi, v, why)) return fail(c, CYC_ERR_ARG, why);
+    const uint64_t words_in = uint64_t(v[0]) * c->pb.K * v[1], words_eg = uint64_t(v[2]) * c->pb.K * v[3];
     DevBuf din, deg, dst;
-    din.alloc(std::max<uint64_t>(words * 8, 16));
-    deg.alloc(std::max<uint64_t>(words * 8, 16));
+    din.alloc(std::max<uint64_t>(words_in * 8, 16));
+    deg.alloc(std::max<uint64_t>(words_eg * 8, 16));
     dst.alloc(std::max<uint64_t>(uint64_t(c->pb.P) * c->pb.K, 16));
-    int rc = run_pipeline(c, c->stream, din.as<uint64_t>(), deg.as<uint64_t>(), dst.as<uint8_t>(), lo, hi);
+    int rc = run_pipeline(c, c->stream, din.as<uint64_t>(), deg.as<uint64_t>(), dst.as<uint8_t>(), lo, hi, true,
+                          part == CYC_ROWS_SOURCE);
     HIPCHK(hipStreamSynchronize(c->stream));
     if (rc != CYC_OK) return rc;
-    if (h_in && words) HIPCHK(hipMemcpy(h_in, din.p, words * 8, hipMemcpyDeviceToHost));
-    if (h_eg && words) HIPCHK(hipMemcpy(h_eg, deg.p, words * 8, hipMemcpyDeviceToHost));
+    if (h_in && words_in) HIPCHK(hipMemcpy(h_in, din.p, words_in * 8, hipMemcpyDeviceToHost));
+    if (h_eg && words_eg) HIPCHK(hipMemcpy(h_eg, deg.p, words_eg * 8, hipMemcpyDeviceToHost));
     if (h_status && uint64_t(c->pb.P) * c->pb.K)
       HIPCHK(hipMemcpy(h_status, dst.p, uint64_t(c->pb.P) * c->pb.K, hipMemcpyDeviceToHost));
     return (int)CYC_OK;
   });
+}
+
+int cyc_probe_run_host(cyc_ctx* c, uint64_t* h_in, uint64_t* h_eg, uint8_t* h_status, int64_t lo, int64_t hi) {
+  return cyc_probe_run_host_rows(c, h_in, h_eg, h_status, CYC_ROWS_TARGET, lo, hi);
 }
 
 // ---------------------------------------------------------------- device-resident tables
@@ -4186,13 +4347,35 @@ struct cyc_table {
   std::string err;
   uint32_t P = 0, K = 0, W = 0;
   int64_t row_lo = 0, row_hi = 0;
+  int partition = CYC_ROWS_TARGET;  // CYC_ROWS_SOURCE: rows are sources; ingress rows cover words [w0, w0 + wa)
+  uint32_t w0 = 0, wa = 0;
   const uint64_t *in = nullptr, *eg = nullptr;
   const uint8_t* status = nullptr;
   DevBuf own_in, own_eg, own_st;  // cyc_table_run: the table owns its planes
 };
 
-static int table_new(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) {
-  if (lo < 0 || hi > int64_t(c->pb.P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
+// Plane shapes of rows [lo, hi) under a partition: ingress rows, words per ingress row slot, egress
+// rows, words per egress row slot, first word of the ingress window.
+static bool rows_layout(const cyc_ctx* c, int part, int64_t lo, int64_t hi, int64_t v[5], std::string& why) {
+  const int64_t P = c->pb.P, W = c->pb.W;
+  if (part != CYC_ROWS_TARGET && part != CYC_ROWS_SOURCE) return why = "unknown partition", false;
+  if (lo < 0 || hi > P || lo > hi) return why = "row range out of bounds", false;
+  if (part == CYC_ROWS_SOURCE && (lo % 64 || (hi % 64 && hi != P)))
+    return why = "source rows: row_lo must be a multiple of 64, row_hi too unless it is the pod count", false;
+  const bool src = part == CYC_ROWS_SOURCE;
+  const int64_t wa = src ? (hi > lo ? (hi + 63) / 64 - lo / 64 : 0) : W;
+  v[0] = src ? P : hi - lo;
+  v[1] = wa;
+  v[2] = hi - lo;
+  v[3] = W;
+  v[4] = src ? lo / 64 : 0;
+  return true;
+}
+
+static int table_new(cyc_ctx* c, int part, int64_t lo, int64_t hi, cyc_table** out) {
+  int64_t v[5];
+  std::string why;
+  if (!rows_layout(c, part, lo, hi, v, why)) return fail(c, CYC_ERR_ARG, why);
   auto* t = new cyc_table();
   t->device = c->device;
   t->P = c->pb.P;
@@ -4200,29 +4383,33 @@ static int table_new(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) {
   t->W = c->pb.W;
   t->row_lo = lo;
   t->row_hi = hi;
+  t->partition = part;
+  t->w0 = uint32_t(v[4]);
+  t->wa = uint32_t(v[1]);
   *out = t;
   return (int)CYC_OK;
 }
 
-int cyc_table_run(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) {
+int cyc_table_run_rows(cyc_ctx* c, int part, int64_t lo, int64_t hi, cyc_table** out) {
   if (!c || !out) return CYC_ERR_ARG;
   *out = nullptr;
   if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
   return guarded(c, [&]() -> int {
     DeviceGuard dg(c->device);
     cyc_table* t = nullptr;
-    int rc = table_new(c, lo, hi, &t);
+    int rc = table_new(c, part, lo, hi, &t);
     if (rc != CYC_OK) return rc;
     std::unique_ptr<cyc_table> hold(t);
-    const uint64_t words = uint64_t(hi - lo) * c->pb.K * c->pb.W;
-    t->own_in.alloc(std::max<uint64_t>(words * 8, 16));
-    t->own_eg.alloc(std::max<uint64_t>(words * 8, 16));
+    const uint64_t words_in = uint64_t(part == CYC_ROWS_SOURCE ? c->pb.P : hi - lo) * c->pb.K * t->wa;
+    const uint64_t words_eg = uint64_t(hi - lo) * c->pb.K * c->pb.W;
+    t->own_in.alloc(std::max<uint64_t>(words_in * 8, 16));
+    t->own_eg.alloc(std::max<uint64_t>(words_eg * 8, 16));
     t->own_st.alloc(std::max<uint64_t>(uint64_t(c->pb.P) * c->pb.K, 16));
     t->in = t->own_in.as<uint64_t>();
     t->eg = t->own_eg.as<uint64_t>();
     t->status = t->own_st.as<uint8_t>();
     rc = run_pipeline(c, c->stream, t->own_in.as<uint64_t>(), t->own_eg.as<uint64_t>(), t->own_st.as<uint8_t>(), lo, hi,
-                      false);
+                      false, part == CYC_ROWS_SOURCE);
     HIPCHK(hipStreamSynchronize(c->stream));
     if (rc != CYC_OK) return rc;
     *out = hold.release();
@@ -4230,14 +4417,16 @@ int cyc_table_run(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) {
   });
 }
 
-int cyc_table_wrap(cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg, const uint8_t* d_status, int64_t lo, int64_t hi,
-                   cyc_table** out) {
+int cyc_table_run(cyc_ctx* c, int64_t lo, int64_t hi, cyc_table** out) { return cyc_table_run_rows(c, CYC_ROWS_TARGET, lo, hi, out); }
+
+int cyc_table_wrap_rows(cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg, const uint8_t* d_status, int part, int64_t lo,
+                        int64_t hi, cyc_table** out) {
   if (!c || !out) return CYC_ERR_ARG;
   *out = nullptr;
   if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
   if (!d_status || ((!d_in || !d_eg) && hi > lo)) return fail(c, CYC_ERR_ARG, "null plane");
   cyc_table* t = nullptr;
-  int rc = table_new(c, lo, hi, &t);
+  int rc = table_new(c, part, lo, hi, &t);
   if (rc != CYC_OK) return rc;
   t->in = d_in;
   t->eg = d_eg;
@@ -4246,12 +4435,27 @@ int cyc_table_wrap(cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg, const
   return (int)CYC_OK;
 }
 
+int cyc_table_wrap(cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg, const uint8_t* d_status, int64_t lo, int64_t hi,
+                   cyc_table** out) {
+  return cyc_table_wrap_rows(c, d_in, d_eg, d_status, CYC_ROWS_TARGET, lo, hi, out);
+}
+
+int cyc_rows_layout(cyc_ctx* c, int part, int64_t lo, int64_t hi, int64_t* out, int n) {
+  if (!c || !out) return CYC_ERR_ARG;
+  if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
+  int64_t v[5];
+  std::string why;
+  if (!rows_layout(c, part, lo, hi, v, why)) return fail(c, CYC_ERR_ARG, why);
+  for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
+  return (int)CYC_OK;
+}
+
 const char* cyc_table_error(const cyc_table* t) { return t ? t->err.c_str() : "null table"; }
 
 int cyc_table_shape(const cyc_table* t, int64_t* out, int n) {
   if (!t || !out) return CYC_ERR_ARG;
-  const int64_t v[5] = {t->P, t->K, t->W, t->row_lo, t->row_hi};
-  for (int i = 0; i < n && i < 5; i++) out[i] = v[i];
+  const int64_t v[8] = {t->P, t->K, t->W, t->row_lo, t->row_hi, t->partition, t->w0, t->wa};
+  for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
   return (int)CYC_OK;
 }
 
@@ -4265,11 +4469,14 @@ int cyc_table_cells(cyc_table* t, int64_t s_lo, int64_t s_hi, int64_t d_lo, int6
   if (s_lo < 0 || s_hi > int64_t(t->P) || s_lo > s_hi || d_lo < 0 || d_hi > int64_t(t->P) || d_lo > d_hi || k_lo < 0 ||
       k_hi > int64_t(t->K) || k_lo > k_hi)
     return bad("cell range out of bounds");
-  // ingress rows are keyed by destination, egress rows by source (include/cyclonus_hip.h)
-  const bool need_d = ingress || combined, need_s = egress || combined;
+  // ingress rows are keyed by destination, egress rows by source (include/cyclonus_hip.h); a
+  // source-row table holds both directions of its sources' cells
+  const bool src = t->partition == CYC_ROWS_SOURCE;
+  const bool need_d = !src && (ingress || combined), need_s = egress || combined || (src && ingress);
   if (s_hi > s_lo && d_hi > d_lo && k_hi > k_lo) {
     if (need_d && (d_lo < t->row_lo || d_hi > t->row_hi)) return bad("ingress cells need destinations inside the table's rows");
-    if (need_s && (s_lo < t->row_lo || s_hi > t->row_hi)) return bad("egress cells need sources inside the table's rows");
+    if (need_s && (s_lo < t->row_lo || s_hi > t->row_hi))
+      return bad(src ? "cells of a source-row table need sources inside its rows" : "egress cells need sources inside the table's rows");
   }
   const uint64_t n = uint64_t(s_hi - s_lo) * uint64_t(d_hi - d_lo) * uint64_t(k_hi - k_lo);
   if (!n) return (int)CYC_OK;
@@ -4285,6 +4492,9 @@ int cyc_table_cells(cyc_table* t, int64_t s_lo, int64_t s_hi, int64_t d_lo, int6
     a.W = t->W;
     a.row_lo = uint32_t(t->row_lo);
     a.row_hi = uint32_t(t->row_hi);
+    a.src = src ? 1u : 0u;
+    a.w0 = t->w0;
+    a.WA = t->wa;
     a.in = t->in;
     a.eg = t->eg;
     a.status = t->status;

@@ -1053,6 +1053,76 @@ static void finish_tables(Problem& pb) {
   }
 }
 
+// NewTableFromJobResults (table.go:38-48) for one probe config: the first result whose Item already
+// holds its key (Item.AddJobResult table.go:16-22 -> utils.DoOrDie), or "".  Results come in
+// runProbe's order (jobrunner.go:33-58): valid jobs in RunJobs order (podFrom, podTo[, container],
+// resources.go:286-287, 345-347), then BadPortProtocol, then BadNamedPort jobs; an Item is the
+// (FromKey, ToKey) = ns/name pair, so pods sharing a name share Items; the key is Protocol/ResolvedPort
+// (job.go:23-25).  The reference walks all P^2 K results; this finds the same first duplicate in
+// O(P K) from the structure of that order.  A job's category c (0 valid, 1 BadPortProtocol,
+// 2 BadNamedPort) and key depend on the destination only, so the results are, per category, every
+// source times the destination jobs J_c = (d[, container]) of that category in (d, container) order:
+//  (A) a destination job j of J_c whose key its destination's name group (pods sharing its ns/name)
+//      already produced in an earlier category or earlier in J_c repeats for EVERY source, first at
+//      (c, source 0, j) — source 0 adds the earlier one before it;
+//  (B) a source that is not the first pod of its name group repeats at its first job, because the
+//      group's first pod added the same (Item, key) earlier in the same category.
+// In the first category where either happens, (A) at source 0 precedes (B) at a later source.  The
+// reference's message continues with the Job as %+v and the stack pkg/errors prints; the job is
+// named here by FromKey, ToKey and ToContainer (the oracle's text, oracle/oracle.cpp).
+static std::string table_build_error(const Resources& res, const Problem& pb, const ProbeConfig& pc, size_t c, uint32_t koff) {
+  const uint32_t P = pb.P;
+  if (!P) return "";
+  std::unordered_map<std::string, uint32_t> first_of;  // name group: first pod with the ns/name
+  std::vector<uint32_t> grp(P);
+  uint32_t s_b = P;  // the first pod that is not the first of its name group
+  for (uint32_t p = 0; p < P; p++) {
+    grp[p] = first_of.emplace(pb.pod_key[p], p).first->second;
+    if (grp[p] != p && s_b == P) s_b = p;
+  }
+  struct DJob {
+    uint32_t d, i;  // destination pod, container index (AllAvailable) or 0
+    std::string key;
+  };
+  std::vector<DJob> jobs[3];
+  for (uint32_t d = 0; d < P; d++) {
+    const Pod& pod = res.pods[d];
+    const size_t base = size_t(d) * pb.K + koff;
+    if (pc.all_available) {
+      for (uint32_t i = 0; i < pod.conts.size(); i++)
+        jobs[0].push_back({d, i, pod.conts[i].proto + "/" + std::to_string(pod.conts[i].port)});
+      continue;
+    }
+    const uint8_t st = pb.slot_status[base];
+    int port = -1;  // ResolvedPort: -1 for a named port that does not resolve (resources.go:303-308)
+    if (st == CYC_JOB_VALID) port = pb.descs[size_t(pb.slot_desc[base])].port;
+    else if (st == CYC_JOB_BAD_PORT_PROTOCOL) port = pc.port.i;
+    const int cat = st == CYC_JOB_VALID ? 0 : st == CYC_JOB_BAD_PORT_PROTOCOL ? 1 : 2;
+    jobs[cat].push_back({d, 0, pc.proto + "/" + std::to_string(port)});
+  }
+  std::set<std::pair<uint32_t, std::string>> seen;  // (name group of the destination, key)
+  for (int cat = 0; cat < 3; cat++) {
+    const DJob* hit = nullptr;
+    for (const DJob& j : jobs[cat])
+      if (!seen.insert({grp[j.d], j.key}).second) {
+        hit = &j;
+        break;
+      }
+    if (!hit && s_b < P && !jobs[cat].empty()) {
+      hit = &jobs[cat][0];
+      const std::string to_cont = pc.all_available ? res.pods[hit->d].conts[hit->i].name : "";
+      return "unable to add job result: duplicate key " + hit->key + " (job {FromKey:" + pb.pod_key[s_b] +
+             " ToKey:" + pb.pod_key[hit->d] + " ToContainer:" + to_cont + "})";
+    }
+    if (hit) {
+      const std::string to_cont = pc.all_available ? res.pods[hit->d].conts[hit->i].name : "";
+      return "unable to add job result: duplicate key " + hit->key + " (job {FromKey:" + pb.pod_key[0] + " ToKey:" +
+             pb.pod_key[hit->d] + " ToContainer:" + to_cont + "})";
+    }
+  }
+  return "";
+}
+
 Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vector<ProbeConfig>& probes) {
   Problem pb;
   Flattener F(pb, ir);
@@ -1108,34 +1178,20 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
     for (size_t c = 0; c < probes.size(); c++)  // PortProtocol: every (from, to) pair builds a job;
       pb.expand_panic[c] = bare && (probes[c].all_available ? any_cont : true);  // AllAvailable: one per dst container
   }
-  std::unordered_map<std::string, int> key_count;
-  bool dup_pod = false;
-  std::string dup_pod_key;
-  for (auto& k : pb.pod_key)
-    if (++key_count[k] == 2 && !dup_pod) {
-      dup_pod = true;
-      dup_pod_key = k;
-    }
   for (size_t c = 0; c < probes.size(); c++) {
     const ProbeConfig& pc = probes[c];
-    bool any_job = false;
     for (uint32_t d = 0; d < pb.P; d++) {
       const Pod& pod = res.pods[d];
       size_t base = size_t(d) * pb.K + cfg_off[c];
       if (pc.all_available) {  // GetJobsAllAvailableServers :336-364
-        std::set<std::string> keys;
         for (size_t i = 0; i < pod.conts.size(); i++) {
           auto& ct = pod.conts[i];
           pb.slot_desc[base + i] = int32_t(F.desc(ct.port, ct.port_name, ct.proto));
           pb.slot_status[base + i] = CYC_JOB_VALID;
-          any_job = true;
-          std::string key = ct.proto + "/" + std::to_string(ct.port);  // JobResult.Key job.go:23-25
-          if (!keys.insert(key).second && pb.dup_key_msg[c].empty())
-            pb.dup_key_msg[c] = "unable to add job result: duplicate key " + key;
         }
         continue;
       }
-      any_job = true;  // GetJobsForNamedPortProtocol :284-334 (every pair gets a job)
+      // GetJobsForNamedPortProtocol :284-334 (every pair gets a job)
       if (pc.port.is_str) {  // ResolveNamedPort pod.go:132-139
         const Container* hit = nullptr;
         for (auto& ct : pod.conts)
@@ -1164,8 +1220,7 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
         }
       }
     }
-    if (dup_pod && any_job && pb.dup_key_msg[c].empty())
-      pb.dup_key_msg[c] = "unable to add job result: duplicate key (pod " + dup_pod_key + " appears twice)";
+    pb.dup_key_msg[c] = table_build_error(res, pb, pc, c, cfg_off[c]);
   }
 
   finish_tables(pb);

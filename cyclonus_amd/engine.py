@@ -73,45 +73,60 @@ class Engine:
         return self.shape
 
     # ---------------------------------------------------------------- runs
-    def run_host(self, row_lo: int = 0, row_hi: Optional[int] = None):
-        """Run on the GPU and copy back: (status[P,K] u8, ingress[R,K,W] u64, egress[R,K,W] u64)."""
-        P, K, W = self.shape["pods"], self.shape["slots"], self.shape["words"]
+    # partition: "target" (rows are the pods both planes are keyed by) or "source" (rows are source
+    # pods: every cell (s in rows, d, k); include/cyclonus_hip.h, cyc_rows)
+    def layout(self, row_lo: int = 0, row_hi: Optional[int] = None, partition: str = "target"):
+        """(ingress rows, ingress words per slot, egress rows, egress words per slot, window start word)."""
+        hi = self.shape["pods"] if row_hi is None else row_hi
+        v = (ctypes.c_int64 * 5)()
+        check(self._ctx, lib().cyc_rows_layout(self._ctx, _lib.PARTITIONS[partition], int(row_lo), int(hi), v, 5))
+        return tuple(int(x) for x in v)
+
+    def run_host(self, row_lo: int = 0, row_hi: Optional[int] = None, partition: str = "target"):
+        """Run on the GPU and copy back: (status[P,K] u8, ingress[rows_in,K,Wi] u64, egress[rows_eg,K,W] u64).
+        Target rows: both planes are [row_hi - row_lo, K, W].  Source rows: ingress is [P, K, Wi], the
+        words [row_lo/64, row_lo/64 + Wi) of every destination's row."""
+        P, K = self.shape["pods"], self.shape["slots"]
         hi = P if row_hi is None else row_hi
-        rows = max(hi - row_lo, 0)
-        ing = np.zeros((rows, K, W), np.uint64)
-        eg = np.zeros((rows, K, W), np.uint64)
+        ri, wi, re_, we, _ = self.layout(row_lo, hi, partition)
+        ing = np.zeros((ri, K, wi), np.uint64)
+        eg = np.zeros((re_, K, we), np.uint64)
         st = np.zeros((P, K), np.uint8)
         check(
             self._ctx,
-            lib().cyc_probe_run_host(self._ctx, ing.ctypes.data, eg.ctypes.data, st.ctypes.data, int(row_lo), int(hi)),
+            lib().cyc_probe_run_host_rows(self._ctx, ing.ctypes.data, eg.ctypes.data, st.ctypes.data,
+                                          _lib.PARTITIONS[partition], int(row_lo), int(hi)),
         )
         return st, ing, eg
 
-    def run_device(self, d_ingress: int, d_egress: int, d_status: int, stream: int = 0, row_lo: int = 0, row_hi=None):
+    def run_device(self, d_ingress: int, d_egress: int, d_status: int, stream: int = 0, row_lo: int = 0, row_hi=None,
+                   partition: str = "target"):
         """Enqueue the pipeline on `stream` writing device pointers (e.g. torch .data_ptr())."""
         P = self.shape["pods"]
         hi = P if row_hi is None else row_hi
         check(
             self._ctx,
-            lib().cyc_probe_run(
+            lib().cyc_probe_run_rows(
                 self._ctx, ctypes.c_void_p(stream or None), ctypes.c_void_p(d_ingress), ctypes.c_void_p(d_egress),
-                ctypes.c_void_p(d_status or None), int(row_lo), int(hi),
+                ctypes.c_void_p(d_status or None), _lib.PARTITIONS[partition], int(row_lo), int(hi),
             ),
         )
 
-    def table(self, row_lo: int = 0, row_hi: Optional[int] = None) -> "DeviceTable":
-        """Run the probe into a device-resident table (cyc_table_run) for target rows [row_lo, row_hi)."""
+    def table(self, row_lo: int = 0, row_hi: Optional[int] = None, partition: str = "target") -> "DeviceTable":
+        """Run the probe into a device-resident table (cyc_table_run_rows) for rows [row_lo, row_hi)."""
         hi = self.shape["pods"] if row_hi is None else row_hi
         t = ctypes.c_void_p()
-        check(self._ctx, lib().cyc_table_run(self._ctx, int(row_lo), int(hi), ctypes.byref(t)))
+        check(self._ctx, lib().cyc_table_run_rows(self._ctx, _lib.PARTITIONS[partition], int(row_lo), int(hi), ctypes.byref(t)))
         return DeviceTable(t)
 
-    def wrap_table(self, d_ingress: int, d_egress: int, d_status: int, row_lo: int = 0, row_hi=None) -> "DeviceTable":
-        """A table over planes produced by run_device (cyc_table_wrap; the caller keeps them alive)."""
+    def wrap_table(self, d_ingress: int, d_egress: int, d_status: int, row_lo: int = 0, row_hi=None,
+                   partition: str = "target") -> "DeviceTable":
+        """A table over planes produced by run_device (cyc_table_wrap_rows; the caller keeps them alive)."""
         hi = self.shape["pods"] if row_hi is None else row_hi
         t = ctypes.c_void_p()
-        check(self._ctx, lib().cyc_table_wrap(self._ctx, ctypes.c_void_p(d_ingress), ctypes.c_void_p(d_egress),
-                                              ctypes.c_void_p(d_status), int(row_lo), int(hi), ctypes.byref(t)))
+        check(self._ctx, lib().cyc_table_wrap_rows(self._ctx, ctypes.c_void_p(d_ingress), ctypes.c_void_p(d_egress),
+                                                   ctypes.c_void_p(d_status), _lib.PARTITIONS[partition], int(row_lo), int(hi),
+                                                   ctypes.byref(t)))
         return DeviceTable(t)
 
     def query_traffic(self, traffics):
@@ -170,9 +185,11 @@ class DeviceTable:
 
     def __init__(self, handle: ctypes.c_void_p):
         self._t = handle
-        v = (ctypes.c_int64 * 5)()
-        lib().cyc_table_shape(self._t, v, 5)
-        self.pods, self.slots, self.words, self.row_lo, self.row_hi = (int(x) for x in v)
+        v = (ctypes.c_int64 * 8)()
+        lib().cyc_table_shape(self._t, v, 8)
+        self.pods, self.slots, self.words, self.row_lo, self.row_hi = (int(x) for x in v[:5])
+        self.partition = "source" if v[5] == _lib.ROWS_SOURCE else "target"
+        self.window = (int(v[6]), int(v[7]))  # ingress words [first, first + count) of a source-row table
 
     def close(self):
         if self._t:

@@ -1,42 +1,86 @@
-"""Multi-GPU layout: target-pod rows sharded across ranks (one process per GPU).
+"""Multi-GPU layout: row shards across ranks (one process per GPU), two partitions.
 
-Each rank computes the verdict planes for rows [row_range(P, world, rank)) of BOTH planes
-(ingress rows keyed by destination, egress rows keyed by source).  Nothing on the data path
-is exchanged; `assemble` is the optional RCCL all-gather (torch.distributed, backend "nccl" on
-ROCm) that materialises the whole table on every rank.
+* "source" (north_star): rank r owns SOURCE pods [lo, hi) — 64-pod aligned, so the
+  ranks' 64-pod words tile every ingress row.  It computes every cell (s in [lo, hi), d, k): the
+  egress rows of its sources and, for every destination, the words [lo/64, ceil(hi/64)) of the
+  ingress row (include/cyclonus_hip.h, CYC_ROWS_SOURCE).  Table.Get(from, *) of a source is answered
+  by one rank (pkg/connectivity/probe/table.go:54-56).
+* "target": rank r owns target pods [lo, hi) of BOTH planes (ingress rows keyed by destination,
+  egress rows keyed by source).
+
+Every verdict depends only on replicated inputs: nothing on the data path is exchanged.  `assemble`
+/ `assemble_sources` are the optional RCCL all-gathers (torch.distributed, backend "nccl" on ROCm)
+that materialise the whole table on every rank.
 """
 from __future__ import annotations
 
 
 def row_range(P: int, world: int, rank: int):
-    """Contiguous, balanced shard of P target rows for `rank` (differs by at most one row)."""
+    """Target-row shard: contiguous, balanced shard of P rows for `rank` (differs by at most one row)."""
     return rank * P // world, (rank + 1) * P // world
 
 
-def assemble(local_rows, P: int, group=None):
-    """All-gather row shards [rows, K, W] into the full [P, K, W] table on every rank.
+def source_range(P: int, world: int, rank: int):
+    """Source-row shard: the pods of a balanced share of the W = ceil(P/64) 64-pod words."""
+    W = (P + 63) // 64
+    return min(P, (rank * W // world) * 64), min(P, ((rank + 1) * W // world) * 64)
 
-    Shards are padded to the largest shard so a single all_gather_into_tensor moves them.
-    """
+
+def shard_range(P: int, world: int, rank: int, partition: str = "target"):
+    return source_range(P, world, rank) if partition == "source" else row_range(P, world, rank)
+
+
+def _gather(send, world, group):
+    """All-gather equal-shaped tensors -> list of world tensors (gloo: list form; RCCL: one buffer)."""
     import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(send) for _ in range(world)]
+        dist.all_gather(parts, send, group=group)
+        return parts
+    out = send.new_empty((world,) + tuple(send.shape))
+    dist.all_gather_into_tensor(out, send, group=group)
+    return list(out.unbind(0))
+
+
+def assemble(local_rows, P: int, group=None, partition: str = "target"):
+    """All-gather row shards [rows, K, W] (target rows of either plane, or a source partition's egress
+    rows) into the full [P, K, W] plane on every rank.  Shards are padded to the largest shard so a
+    single all-gather moves them."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    maxrows = max(hi - lo for lo, hi in (row_range(P, world, r) for r in range(world)))
-    lo, hi = row_range(P, world, rank)
+    ranges = [shard_range(P, world, r, partition) for r in range(world)]
+    maxrows = max(hi - lo for lo, hi in ranges)
+    lo, hi = ranges[rank]
     K, W = local_rows.shape[1], local_rows.shape[2]
-    send = local_rows.new_zeros((maxrows, K, W))
+    send = local_rows.new_zeros((max(maxrows, 1), K, W))
     send[: hi - lo] = local_rows[: hi - lo]
-    out = local_rows.new_empty((world * maxrows, K, W))
-    if dist.get_backend(group) == "gloo":
-        parts = list(out.chunk(world))
-        dist.all_gather(parts, send, group=group)
-        out = torch.cat(parts)
-    else:
-        dist.all_gather_into_tensor(out, send, group=group)
+    parts = _gather(send, world, group)
     full = local_rows.new_empty((P, K, W))
-    for r in range(world):
-        a, b = row_range(P, world, r)
-        full[a:b] = out[r * maxrows : r * maxrows + (b - a)]
+    for r, (a, b) in enumerate(ranges):
+        full[a:b] = parts[r][: b - a]
+    return full
+
+
+def assemble_sources(local_ingress, P: int, group=None):
+    """All-gather a source partition's ingress slices [P, K, Wr] (each rank: the words of its
+    sources in every destination's row) into the full [P, K, W] ingress plane on every rank."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    W = (P + 63) // 64
+    wr = [((r * W // world), ((r + 1) * W // world)) for r in range(world)]
+    maxw = max(b - a for a, b in wr)
+    K = local_ingress.shape[1]
+    a, b = wr[rank]
+    send = local_ingress.new_zeros((P, K, max(maxw, 1)))
+    send[:, :, : b - a] = local_ingress[:, :, : b - a]
+    parts = _gather(send, world, group)
+    full = local_ingress.new_empty((P, K, W))
+    for r, (a, b) in enumerate(wr):
+        full[:, :, a:b] = parts[r][:, :, : b - a]
     return full

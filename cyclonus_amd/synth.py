@@ -352,13 +352,13 @@ def config4(n_pods=50_000, n_policies=5000, n_ns=500, seed=20250217):
             "probes": [{"AllAvailable": True}], "description": f"{n_pods} pods x {n_policies} IPBlock policies x 4 ports"}
 
 
-def config3u(seed=20250217):
+def config3u(n_ns=1000, seed=20250217):
     """Class-explosion variant of config #3 (SURVEY §7 "class explosion"): the
     same 100k pods x 10k policies x 8 port/protocols, but every pod has its own label set (100
     templates per namespace, one replica each), so pod identities are all distinct and the
     policies' selectors split each namespace into many target classes.  A stress workload for the
     class rows, not a BASELINE config."""
-    d = config3(templates_per_ns=100, replicas=1, seed=seed)
+    d = config3(n_ns=n_ns, templates_per_ns=100, replicas=1, seed=seed)
     d["name"] = "config3u"
     d["description"] += " (all pod identities distinct)"
     return d

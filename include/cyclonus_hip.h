@@ -113,6 +113,32 @@ int cyc_probe_run(cyc_ctx* ctx, void* hip_stream, uint64_t* d_ingress, uint64_t*
 int cyc_probe_run_host(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_t* status, int64_t row_lo,
                        int64_t row_hi);
 
+/* ---- Row partitions for one-process-per-GPU runs (north_star: "source-pod rows shard across the
+ * GPUs").  A rank runs rows [row_lo, row_hi) of the pods under one of two partitions:
+ *   CYC_ROWS_TARGET  the rows are TARGET pods of both planes (cyc_probe_run's layout above): rank r
+ *                    holds the ingress rows of destinations and the egress rows of sources in the range.
+ *   CYC_ROWS_SOURCE  the rows are SOURCE pods: rank r holds every cell (s in [row_lo, row_hi), d, k),
+ *                    i.e. Table.Get(from, *) for its sources (pkg/connectivity/probe/table.go:54-56, the
+ *                    reference's jobs are generated source-major, resources.go:286-287):
+ *                      egress [((s - row_lo)*K + k)*W  + d/64]              bit d%64 (full rows of its sources)
+ *                      ingress[(d*K + k)*Wr + (s/64 - row_lo/64)]          bit s%64, for EVERY destination d,
+ *                    Wr = ceil(row_hi/64) - row_lo/64 words: the rank's slice of each ingress row.
+ *                    row_lo must be a multiple of 64, and row_hi too unless it is P, so the slices of
+ *                    a partition tile every ingress row.  The rank's peer rows and ingress class rows
+ *                    cover only its words, so its front work shrinks with the partition too.
+ * The union of the ranks' planes is the whole table either way, with no data exchange (the inputs are
+ * replicated); assembling it on every rank is one all-gather per plane (cyclonus_amd/shard.py). */
+typedef enum { CYC_ROWS_TARGET = 0, CYC_ROWS_SOURCE = 1 } cyc_rows;
+
+/* Plane shapes of rows [row_lo, row_hi) under `partition`: out[0] ingress rows, out[1] words per
+ * ingress (row, slot), out[2] egress rows, out[3] words per egress (row, slot), out[4] the ingress
+ * window's first word (0 for target rows).  Needs cyc_probe_prepare. */
+int cyc_rows_layout(cyc_ctx* ctx, int partition, int64_t row_lo, int64_t row_hi, int64_t* out, int n);
+int cyc_probe_run_rows(cyc_ctx* ctx, void* hip_stream, uint64_t* d_ingress, uint64_t* d_egress, uint8_t* d_status,
+                       int partition, int64_t row_lo, int64_t row_hi);
+int cyc_probe_run_host_rows(cyc_ctx* ctx, uint64_t* ingress, uint64_t* egress, uint8_t* status, int partition,
+                            int64_t row_lo, int64_t row_hi);
+
 /* ---- Device-resident verdict tables: the lazy probe.Table (pkg/connectivity/probe/table.go:24-56).
  * The reference's Runner.RunProbeForConfig returns *Table = NewTableFromJobResults(resources,
  * runProbe(jobs)) (jobrunner.go:29-58, table.go:38-48): one Item per (from, to) pod pair holding a
@@ -138,15 +164,21 @@ int cyc_table_run(cyc_ctx* ctx, int64_t row_lo, int64_t row_hi, cyc_table** out)
  * must outlive the table and the run must be complete before cyc_table_cells). */
 int cyc_table_wrap(cyc_ctx* ctx, const uint64_t* d_ingress, const uint64_t* d_egress, const uint8_t* d_status,
                    int64_t row_lo, int64_t row_hi, cyc_table** out);
+/* The same under a row partition (cyc_probe_run_rows).  A CYC_ROWS_SOURCE table answers every cell
+ * (s, d, k) with s inside its rows: Ingress, Egress and Combined of Table.Get(from = s, to = d). */
+int cyc_table_run_rows(cyc_ctx* ctx, int partition, int64_t row_lo, int64_t row_hi, cyc_table** out);
+int cyc_table_wrap_rows(cyc_ctx* ctx, const uint64_t* d_ingress, const uint64_t* d_egress, const uint8_t* d_status,
+                        int partition, int64_t row_lo, int64_t row_hi, cyc_table** out);
 /* Connectivity of every cell (s, d, k) of sources [s_lo,s_hi) x destinations [d_lo,d_hi) x slots
  * [k_lo,k_hi), computed on the device, into host arrays indexed
  *   ((s - s_lo) * (d_hi - d_lo) + (d - d_lo)) * (k_hi - k_lo) + (k - k_lo)
  * ingress / egress / combined are each optional (NULL = not wanted): JobResult.Ingress, .Egress and
- * .Combined of that job (jobrunner.go:36-55,85-93).  Ingress needs the destinations inside the
- * table's rows, egress the sources, combined both (a row shard answers its own rows). */
+ * .Combined of that job (jobrunner.go:36-55,85-93).  Target rows: ingress needs the destinations
+ * inside the table's rows, egress the sources, combined both.  Source rows: every output needs the
+ * sources inside the table's rows (any destination). */
 int cyc_table_cells(cyc_table* t, int64_t s_lo, int64_t s_hi, int64_t d_lo, int64_t d_hi, int64_t k_lo, int64_t k_hi,
                     uint8_t* ingress, uint8_t* egress, uint8_t* combined);
-/* out[0..4] = pods, slots, words, row_lo, row_hi */
+/* out[0..7] = pods, slots, words, row_lo, row_hi, partition, ingress window first word, window words */
 int cyc_table_shape(const cyc_table* t, int64_t* out, int n);
 const char* cyc_table_error(const cyc_table* t);
 void cyc_table_destroy(cyc_table* t);

@@ -33,6 +33,8 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "gonet.hpp"
@@ -1018,6 +1020,42 @@ struct Handle {
   Resources res;
 };
 
+// NewTableFromJobResults (table.go:38-48) over runProbe's result list (jobrunner.go:33-58): the
+// valid jobs in RunJobs order (resources.go:286-287 podFrom, podTo[, container]), then every
+// BadPortProtocol job, then every BadNamedPort job, each added to the Item of (FromKey, ToKey) —
+// PodString ns/name, so pods sharing a name share Items — under JobResult.Key() = Protocol/ResolvedPort
+// (job.go:23-25); Item.AddJobResult (table.go:16-22) rejects a key the Item already holds and
+// utils.DoOrDie (utils.go:10-14) ends the program.  Returns "" or the error text.  The reference's
+// text continues with the whole Job as %+v (its ToHost depends on the probe mode) and the stack
+// pkg/errors prints; here the job is named by FromKey, ToKey and ToContainer.
+static std::string table_build_error(const Resources& r, const ProbeConfig& c, int nslot) {
+  const auto& pods = r.pods;
+  const size_t P = pods.size();
+  std::unordered_map<std::string, uint64_t> pod_id, key_id;
+  std::vector<uint64_t> pid(P);
+  for (size_t p = 0; p < P; p++) pid[p] = pod_id.emplace(pods[p].ns + "/" + pods[p].name, pod_id.size()).first->second;
+  std::unordered_set<std::string> held;  // (FromKey id, ToKey id, key) of every added result
+  auto add = [&](size_t s, size_t d, const JobDesc& j, const std::string& to_cont) -> std::string {
+    const std::string key = j.protocol + "/" + std::to_string(j.port);
+    std::string item = std::to_string(pid[s]) + "|" + std::to_string(pid[d]) + "|" + key;
+    if (held.insert(item).second) return "";
+    return "unable to add job result: duplicate key " + key + " (job {FromKey:" + pods[s].ns + "/" + pods[s].name +
+           " ToKey:" + pods[d].ns + "/" + pods[d].name + " ToContainer:" + to_cont + "})";
+  };
+  for (int pass = 0; pass < 3; pass++) {  // valid jobs, BadPortProtocol, BadNamedPort
+    const int want = pass == 0 ? ST_VALID : pass == 1 ? ST_BAD_PORT_PROTOCOL : ST_BAD_NAMED_PORT;
+    for (size_t s = 0; s < P; s++)
+      for (size_t d = 0; d < P; d++)
+        for (int i = 0; i < nslot; i++) {
+          JobDesc j = job_desc(pods[d], c, i);
+          if (j.status != want) continue;
+          std::string e = add(s, d, j, c.allAvailable ? pods[d].containers[i].name : "");
+          if (!e.empty()) return e;
+        }
+  }
+  return "";
+}
+
 static void set_err(char* err, size_t cap, const std::string& m) {
   if (!err || !cap) return;
   size_t n = std::min(cap - 1, m.size());
@@ -1139,6 +1177,13 @@ int orc_probe_run(void* hv, const char* probes_json, uint8_t* status, uint64_t* 
               return 1;
             }
           }
+      // the config's table is built after its jobs ran (jobrunner.go:29-31)
+      std::string dup = table_build_error(h->res, cfgs[c], nslot);
+      if (!dup.empty()) {
+        set_err(err, errcap, dup);
+        if (panic_cell) *panic_cell = -2;
+        return 1;
+      }
     }
     return 0;
   } catch (std::exception& e) {

@@ -4,6 +4,7 @@
 #   bash scripts/_prof.sh OUTDIR config3
 set -e
 OUT=gpurun_out/$1; CFG=$2; mkdir -p $OUT
+cp cyclonus_amd/_build/build_info.json $OUT/build_info.json
 timeout -k 10 300 python -u bench.py --config $CFG > $OUT/bench_$CFG.log 2>&1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$CFG -o run -- python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_$CFG.log 2>&1

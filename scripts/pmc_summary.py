@@ -4,7 +4,11 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes
 coalesced streaming read -> doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores;
 both are in KiB (hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024).
 
-    python scripts/pmc_summary.py FETCH.csv WRITE.csv OUT.json [workload-name] [--mfma MFMA.csv]
+    python scripts/pmc_summary.py FETCH.csv WRITE.csv OUT.json [workload-name] [--mfma MFMA.csv] [--build-info INFO.json]
+
+--build-info: the cyclonus_amd/_build/build_info.json of the profiled library (copied into the run's
+output directory by the profiling script): its git head and sha256 go into OUT.json, and bench.py
+quotes OUT.json's traffic only when the library it loads has that sha256.
 
 --mfma: a pass with SQ_INSTS_VALU_MFMA_* / SQ_INSTS_MFMA / SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CYCLES
 (scripts/pmc_mfma.sh) -> per step (one launch of every library kernel): MFMA instructions, MFMA
@@ -45,10 +49,13 @@ def mfma_summary(path):
 
 def main():
     args = sys.argv[1:]
-    mfma = None
+    mfma = info = None
     if "--mfma" in args:
         mfma = args[args.index("--mfma") + 1]
         args = [a for a in args if a not in ("--mfma", mfma)]
+    if "--build-info" in args:
+        info = args[args.index("--build-info") + 1]
+        args = [a for a in args if a not in ("--build-info", info)]
     fetch, write, out = args[0], args[1], args[2]
     name = args[3] if len(args) > 3 else "config3"
     f = per_kernel(fetch, "FETCH_SIZE")
@@ -64,6 +71,8 @@ def main():
            "emit_hbm_bytes_per_launch": emit[0]["hbm_bytes"] if emit else None}
     if mfma:
         doc["mfma"] = mfma_summary(mfma)
+    if info:
+        doc["build"] = json.load(open(info))
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps({"emit_hbm_bytes_per_launch": doc["emit_hbm_bytes_per_launch"], "mfma": doc.get("mfma")}))
 

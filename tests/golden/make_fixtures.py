@@ -382,7 +382,22 @@ def builder_kats():
     return {"source": "pkg/matcher/builder_tests.go, simplifier_tests.go", "cases": cases}
 
 
+def policy_yaml_files():
+    """networkpolicies/**/*.yaml copied byte for byte (data: the policy inputs config #1 and the
+    policy fixtures are read from, cli/utils.go:14-60) into tests/golden/yaml/, so the product's YAML
+    loader is tested on the reference's own policy text."""
+    import shutil
+
+    src_root = os.path.join(REF, "networkpolicies")
+    dst_root = os.path.join(OUT, "yaml")
+    for f in sorted(glob.glob(os.path.join(src_root, "**", "*.yaml"), recursive=True)):
+        dst = os.path.join(dst_root, os.path.relpath(f, src_root))
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
+        shutil.copyfile(f, dst)
+
+
 def main():
+    policy_yaml_files()
     json.dump(config1(), open(os.path.join(OUT, "config1.json"), "w"), indent=1, sort_keys=True)
     json.dump(policy_fixtures(), open(os.path.join(OUT, "policy_fixtures.json"), "w"), indent=1, sort_keys=True)
     kat = {"ip": ip_kats(), "selector": selector_kats(), "policy": policy_test_kats(), "builder": builder_kats()}

@@ -126,7 +126,7 @@ def random_policy(r: random.Random, i: int, v6=False, bad=False):
     return {"apiVersion": "networking.k8s.io/v1", "kind": "NetworkPolicy", "metadata": md, "spec": spec}
 
 
-def random_resources(r: random.Random, n_pods: int, v6=False, bad=False):
+def random_resources(r: random.Random, n_pods: int, v6=False, bad=False, dups=False):
     nss = {}
     for ns in NS[:3]:
         nss[ns] = {"ns": ns, **_labels(r, 2)} if r.random() < 0.9 else None
@@ -144,11 +144,15 @@ def random_resources(r: random.Random, n_pods: int, v6=False, bad=False):
         for j in range(r.randint(1, 4)):
             port = r.choice([80, 81, 53, 443, 8080, 9000])
             proto = r.choice(PROTOS + ["tcp"])
-            if (proto, port) in used:
+            if (proto, port) in used and not (dups and r.random() < 0.3):
                 continue
             used.add((proto, port))
             conts.append({"Name": f"c{j}", "Port": port, "Protocol": proto, "PortName": f"serve-{port}-{proto.lower()}"})
-        pods.append({"Namespace": ns, "Name": f"p{i}", "Labels": _labels(r), "IP": ip, "Containers": conts})
+        name = f"p{i}"
+        if dups and pods and r.random() < 0.08:  # a second pod with an earlier pod's ns/name (one table Item)
+            twin = r.choice(pods)
+            ns, name = twin["Namespace"], twin["Name"]
+        pods.append({"Namespace": ns, "Name": name, "Labels": _labels(r), "IP": ip, "Containers": conts})
     return {"Namespaces": {k: v for k, v in nss.items()}, "Pods": pods}
 
 
@@ -165,11 +169,13 @@ def random_probes(r: random.Random):
     return out
 
 
-def random_problem(seed: int, n_pods=None, n_pols=None, v6=None, bad=False):
+def random_problem(seed: int, n_pods=None, n_pols=None, v6=None, bad=False, dups=False):
+    """dups=True: pods may repeat an earlier pod's ns/name and containers may repeat a (protocol, port):
+    the reference's table build then dies on a duplicate job key (table.go:16-22, 38-48)."""
     r = random.Random(seed)
     if v6 is None:
         v6 = r.random() < 0.5
     n_pods = n_pods or r.randint(1, 40)
     n_pols = n_pols if n_pols is not None else r.randint(0, 12)
     pols = [random_policy(r, i, v6, bad) for i in range(n_pols)]
-    return pols, random_resources(r, n_pods, v6, bad), random_probes(r)
+    return pols, random_resources(r, n_pods, v6, bad, dups), random_probes(r)

@@ -160,19 +160,15 @@ def test_runner_all_available_and_named(gpu):
         assert t.render_table() == want
 
 
-def test_config1_through_yaml_loader(gpu, tmp_path):
-    """analyze --mode probe's input path: the policy directory (cli/utils.go:14-60, YAML written
-    from the committed fixture with quoted strings, as networkpolicies/simple-example quotes "y")
-    -> BuildNetworkPolicies -> GPU table -> README.md:294-313 byte for byte."""
-    import yaml
-
+def test_config1_through_yaml_loader(gpu):
+    """analyze --mode probe's input path on the reference's own files: the policy directory
+    networkpolicies/simple-example (copied byte for byte to tests/golden/yaml/, read as
+    cli/utils.go:14-60 does) -> BuildNetworkPolicies -> GPU table -> README.md:294-313 byte for byte."""
     from cyclonus_amd.loader import read_policies_from_path
 
     c = json.load(open(os.path.join(GOLD, "config1.json")))
-    for p in c["policies"]:
-        (tmp_path / f"{p['metadata']['name']}.yaml").write_text(yaml.safe_dump(p, default_style='"'))
-    pols = read_policies_from_path(str(tmp_path))
-    assert sorted(json.dumps(p, sort_keys=True) for p in pols) == sorted(json.dumps(p, sort_keys=True) for p in c["policies"])
+    pols = read_policies_from_path(os.path.join(GOLD, "yaml", "simple-example"))
+    assert json.dumps(pols, sort_keys=True) == json.dumps(c["policies"], sort_keys=True)
     runner = new_simulated_runner(build_network_policies(True, pols))
     table = runner.run_probe_for_config(new_probe_config(80, "TCP"), Resources.from_json(c["resources"]))
     assert table.render_table() == c["readme_combined_tcp80"]["text"]

@@ -1,8 +1,9 @@
-"""Whole plane rows at full size (configs #3 and #4): complete ingress rows (one destination, every
+"""Whole plane rows at full size (configs #2, #3 and #4): complete ingress rows (one destination, every
 source, every slot) and egress rows (one source, every destination, every slot) from the device
 table equal the oracle's rows bit for bit — rows from the first / last positions, 64-pod word
-edges, the most populous identities (largest classes) and random positions, on the whole table and
-on row shards (row_lo > 0)."""
+edges, the most populous identities (largest classes) and random positions, on the whole table, on
+target-row shards (row_lo > 0) and on source-row shards (the shard's egress rows, and its word slice
+of every picked destination's ingress row)."""
 import json
 from collections import Counter
 
@@ -11,7 +12,7 @@ import pytest
 
 from cyclonus_amd import synth
 from cyclonus_amd.engine import Engine
-from cyclonus_amd.shard import row_range
+from cyclonus_amd.shard import row_range, source_range
 from oracle.oracle import Oracle
 
 pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("gpu")]
@@ -31,7 +32,7 @@ def _pick_rows(res, lo, hi, n_random, seed):
     return sorted(lo + r for r in rows if 0 <= r < len(pods))
 
 
-def _check(name, kw, shards):
+def _check(name, kw, shards, source_shards=()):
     import torch
 
     data = synth.CONFIGS[name](**kw)
@@ -39,6 +40,32 @@ def _check(name, kw, shards):
     sh = eng.prepare(data["probes"])
     P, K, W = sh["pods"], sh["slots"], sh["words"]
     orc = Oracle(data["policies"], data["resources"])
+    for world, rank in source_shards:
+        lo, hi = source_range(P, world, rank)
+        ri, wi, re_, we, w0 = eng.layout(lo, hi, "source")
+        d_in = torch.empty((ri, K, wi), dtype=torch.int64, device="cuda")
+        d_eg = torch.empty((re_, K, we), dtype=torch.int64, device="cuda")
+        d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
+        eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), torch.cuda.current_stream().cuda_stream, lo, hi,
+                       "source")
+        torch.cuda.synchronize()
+        dsts = _pick_rows(data["resources"], 0, P, 6, seed=world * 1000 + rank)  # any destination
+        srcs = _pick_rows(data["resources"], lo, hi, 4, seed=world * 1000 + rank + 1)  # the shard's sources
+        g_in = d_in[torch.as_tensor(dsts, device="cuda")].cpu().numpy().view(np.uint64)
+        g_eg = d_eg[torch.as_tensor([p - lo for p in srcs], device="cuda")].cpu().numpy().view(np.uint64)
+        del d_in, d_eg
+        torch.cuda.empty_cache()
+        for k in range(K):
+            for x, pod in enumerate(dsts):
+                want = orc.row(data["probes"], "ingress", pod, k, threads=THREADS)[w0:w0 + wi]
+                bad = np.nonzero(g_in[x, k] != want)[0]
+                assert bad.size == 0, (f"{name} source shard {rank}/{world} ingress row {pod} slot {k}: {bad.size} words "
+                                       f"of the slice differ, first at word {w0 + int(bad[0])}")
+            for x, pod in enumerate(srcs):
+                want = orc.row(data["probes"], "egress", pod, k, threads=THREADS)
+                bad = np.nonzero(g_eg[x, k] != want)[0]
+                assert bad.size == 0, (f"{name} source shard {rank}/{world} egress row {pod} slot {k}: {bad.size} words "
+                                       f"differ, first at word {int(bad[0])}")
     for world, rank in shards:
         lo, hi = row_range(P, world, rank)
         rows = hi - lo
@@ -63,12 +90,18 @@ def _check(name, kw, shards):
                                            f"{bad.size} words differ, first at word {int(bad[0])}")
 
 
+def test_config2_full_rows():
+    """Config #2 (per-pod PM rows, in-place class rows, the flat emit): whole table, a target shard
+    and a source shard."""
+    _check("config2", {}, [(1, 0), (4, 2)], [(8, 5)])
+
+
 def test_config3_full_rows():
-    _check("config3", {}, [(1, 0), (8, 3)])
+    _check("config3", {}, [(1, 0), (8, 3)], [(8, 3)])
 
 
 def test_config4_full_rows():
-    _check("config4", {}, [(1, 0), (4, 3)])
+    _check("config4", {}, [(1, 0), (4, 3)], [(4, 1)])
 
 
 def test_config3u_full_rows():

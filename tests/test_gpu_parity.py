@@ -665,3 +665,149 @@ def test_long_class_lists_pm_items(gpu, seed):
             for fused in (1, 0):
                 eng.set_option("front_fused", fused)
                 assert_same(want, eng.run_host(), f"seed {seed} simplify {simplify} pl_wave {wave} fused {fused}")
+
+
+def _source_shards_equal(eng, full, worlds, ctx):
+    """Every source shard of every partition size equals the full table's slices: its sources'
+    egress rows, and the words of its sources in every destination's ingress row."""
+    from cyclonus_amd.shard import source_range
+
+    st, ing, eg = full
+    P = st.shape[0]
+    for world in worlds:
+        for rank in range(world):
+            lo, hi = source_range(P, world, rank)
+            st2, ing2, eg2 = eng.run_host(lo, hi, "source")
+            w0, wa = lo // 64, ing2.shape[2]
+            assert ing2.shape[0] == P and eg2.shape[0] == hi - lo, (ctx, world, rank, ing2.shape, eg2.shape)
+            assert np.array_equal(st, st2), (ctx, world, rank)
+            assert np.array_equal(ing[:, :, w0:w0 + wa], ing2), f"{ctx}: ingress slice of source shard {rank}/{world}"
+            assert np.array_equal(eg[lo:hi], eg2), f"{ctx}: egress rows of source shard {rank}/{world}"
+
+
+def test_source_rows_random(gpu):
+    """Source-row runs (CYC_ROWS_SOURCE) on random problems, through the fused front, the DAG (graph
+    and eager), IDO and PM builds, against the full table (itself checked against the oracle)."""
+    eng = Engine(0)
+    n = 0
+    for seed in range(24):
+        pols, res, probes = random_problem(120_000 + seed, n_pods=70 + 23 * seed, bad=seed % 4 == 3)
+        try:
+            want = Oracle(pols, res).probe(probes)
+        except OraclePanic:
+            continue
+        eng.build_policies(pols).load_resources(res)
+        eng.prepare(probes)
+        for graphs, fused, pod_words in ((-1, 1, -1), (1, 0, -1), (0, 1, 0), (2, 0, 0)):
+            eng.set_option("graphs", graphs)
+            eng.set_option("front_fused", fused)
+            eng.set_option("pod_words", pod_words)
+            full = eng.run_host()
+            assert_same(want, full, f"seed {seed}")
+            _source_shards_equal(eng, full, (2, 3, 5), f"seed {seed} graphs {graphs} fused {fused} pod_words {pod_words}")
+            n += 1
+    assert n >= 40
+
+
+def test_source_rows_deployments_and_ip(gpu):
+    """Source shards on IDO builds (deployment-style identity runs) and IP-interval problems (IP rows
+    computed only over the shard's chunks)."""
+    eng = Engine(0)
+    problems = [_deployment_problem(s) for s in range(6)] + [_ip_interval_problem(s, n_pods=900 + 131 * s) for s in range(3)]
+    for n, (pols, res, probes) in enumerate(problems):
+        want = Oracle(pols, res).probe(probes)
+        eng.build_policies(pols).load_resources(res)
+        eng.prepare(probes)
+        for pod_words, wave in ((-1, 1), (0, 1), (0, 0)):
+            eng.set_option("pod_words", pod_words)
+            eng.set_option("pl_wave", wave)
+            full = eng.run_host()
+            assert_same(want, full, f"problem {n}")
+            _source_shards_equal(eng, full, (2, 4, 7), f"problem {n} pod_words {pod_words} pl_wave {wave}")
+        eng.set_option("pod_words", -1)
+        eng.set_option("pl_wave", 1)
+
+
+@pytest.mark.parametrize("name,kw", [("config3", {"n_ns": 60}), ("config4", {"n_pods": 6000, "n_policies": 600, "n_ns": 60}),
+                                     ("config2", {"n_ns": 30}), ("config3u", {"n_ns": 40})])
+def test_source_rows_synthetic(gpu, name, kw):
+    """Source shards of the synthetic workloads (fused front, sparse pod rows, IP rows, in-place class
+    rows) equal the full table's slices, on the device path with the emit's per-plane launches."""
+    from cyclonus_amd import synth
+
+    data = synth.CONFIGS[name](**kw)
+    eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
+    eng.prepare(data["probes"])
+    full = eng.run_host()
+    _source_shards_equal(eng, full, (2, 8), name)
+
+
+def test_source_rows_panics(gpu):
+    """A panicking problem: the source shard holding the first panicking job's source reports the
+    reference's panic (jobs are source-major, so the shard's first panic is the global first)."""
+    from cyclonus_amd.shard import source_range
+
+    eng = Engine(0)
+    seen = 0
+    for seed in range(10_000, 10_120):
+        pols, res, probes = random_problem(seed, bad=True)
+        try:
+            Oracle(pols, res).probe(probes)
+            continue
+        except OraclePanic as e:
+            want = e
+        eng.build_policies(pols).load_resources(res)
+        try:
+            sh = eng.prepare(probes)
+        except CyclonusPanic as e:
+            assert e.msg == str(want), seed
+            continue
+        P, K = sh["pods"], sh["slots"]
+        if want.cell is None or want.cell < 0 or not P or not K:
+            continue
+        s_first = want.cell // (P * K)
+        for world in (2, 3):
+            r = next(r for r in range(world) if source_range(P, world, r)[0] <= s_first < source_range(P, world, r)[1])
+            lo, hi = source_range(P, world, r)
+            with pytest.raises(CyclonusPanic) as ei:
+                eng.run_host(lo, hi, "source")
+            assert ei.value.msg == str(want), (seed, world)
+            seen += 1
+    assert seen >= 10
+
+
+def test_source_rows_arguments(gpu):
+    """Source rows must start on a 64-pod word (and end on one, or at P); empty shards are valid."""
+    pols, res, probes = random_problem(777, n_pods=200, n_pols=30)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    eng.prepare(probes)
+    st, ing, eg = eng.run_host()
+    for lo, hi in ((1, 64), (0, 65), (64, 100)):
+        with pytest.raises(Exception):
+            eng.run_host(lo, hi, "source")
+    st2, ing2, eg2 = eng.run_host(64, 64, "source")
+    assert ing2.shape == (200, ing.shape[1], 0) and eg2.shape[0] == 0
+    st2, ing2, eg2 = eng.run_host(128, 200, "source")
+    assert np.array_equal(ing[:, :, 2:4], ing2) and np.array_equal(eg[128:200], eg2)
+    assert eng.layout(128, 200, "source") == (200, 2, 72, 4, 2)
+
+
+@pytest.mark.parametrize("block", range(2))
+def test_duplicate_job_keys(gpu, block):
+    """Pods sharing a ns/name and containers sharing a (protocol, port): the reference's table build
+    dies on the first result whose Item already holds its key (table.go:16-22, 38-48 via
+    utils.DoOrDie), in runProbe's result order (valid, BadPortProtocol, BadNamedPort jobs,
+    jobrunner.go:33-58), after the config's evaluation panics and before the next config.  The GPU
+    build reports CYC_ERR_DUPLICATE_KEY exactly when the oracle's literal walk does, for the same job
+    and key; tables without a duplicate are unchanged."""
+    eng = Engine(0)
+    n_dup = n_ok = 0
+    for seed in range(200_000 + block * 100, 200_000 + block * 100 + 100):
+        pols, res, probes = random_problem(seed, dups=True, bad=seed % 7 == 0)
+        o, g = run_both(pols, res, probes, engine=eng)
+        assert_same(o, g, f"dups seed {seed}")
+        if isinstance(o, Panicked) and "duplicate key" in o.msg:
+            n_dup += 1
+        elif not isinstance(o, Panicked):
+            n_ok += 1
+    assert n_dup >= 40 and n_ok >= 10, (n_dup, n_ok)

@@ -11,7 +11,7 @@ from cyclonus_amd import _lib
 from cyclonus_amd._lib import CyclonusError, CyclonusPanic
 from cyclonus_amd.engine import Engine
 from cyclonus_amd.probe import PlaneCells
-from cyclonus_amd.shard import row_range
+from cyclonus_amd.shard import row_range, source_range
 from oracle.oracle import Oracle, OraclePanic
 from randgen import random_problem
 
@@ -93,6 +93,41 @@ def test_table_row_shards_and_wrap():
     eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     _same(eng.wrap_table(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr()), want, P, K, "wrap")
+
+
+def test_table_source_shards():
+    """Source-row tables (CYC_ROWS_SOURCE) answer Table.Get(from, *) for their sources: every
+    Ingress / Egress / Combined value of (s in shard, any d, k), from owned planes and from wrapped
+    run_device planes; cells of other sources are refused."""
+    import torch
+
+    for seed in (6300, 6301, 6302):
+        pols, res, probes = random_problem(seed, n_pods=190, n_pols=30)
+        want = PlaneCells(*Oracle(pols, res).probe(probes))
+        eng = Engine(0).build_policies(pols).load_resources(res)
+        sh = eng.prepare(probes)
+        P, K = sh["pods"], sh["slots"]
+        for world in (2, 3):
+            for rank in range(world):
+                lo, hi = source_range(P, world, rank)
+                t = eng.table(lo, hi, "source")
+                assert t.partition == "source" and t.window[0] == lo // 64
+                g = t.cells(lo, hi, 0, P, 0, K)
+                w = want.cells(lo, hi, 0, P, 0, K)
+                assert all(np.array_equal(g[n], w[n]) for n in g), (seed, world, rank)
+                if hi < P:
+                    with pytest.raises(CyclonusError):
+                        t.cells(hi, P, 0, P, 0, K, want=("ingress",))
+                ri, wi, re_, we, _ = eng.layout(lo, hi, "source")
+                d_in = torch.zeros((ri, K, max(wi, 1)), dtype=torch.int64, device="cuda")
+                d_eg = torch.zeros((max(re_, 1), K, we), dtype=torch.int64, device="cuda")
+                d_st = torch.zeros((P, K), dtype=torch.uint8, device="cuda")
+                eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                               lo, hi, "source")
+                torch.cuda.synchronize()
+                t2 = eng.wrap_table(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), lo, hi, "source")
+                g2 = t2.cells(lo, hi, 0, P, 0, K)
+                assert all(np.array_equal(g2[n], w[n]) for n in g2), (seed, world, rank, "wrap")
 
 
 def test_table_panics_and_lifetime():

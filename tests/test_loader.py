@@ -81,3 +81,23 @@ def test_first_document_only_and_strictness(tmp_path):
     got = _one(tmp_path, "Kind: NetworkPolicy\nMetadata: {Name: a, namespace: p, Namespace: q}\nSPEC: {policyTypes: [Ingress]}\n")
     assert got[0]["metadata"] == {"name": "a", "namespace": "q"} and got[0]["kind"] == "NetworkPolicy"
     assert _one(tmp_path, "") == []  # an empty file is an empty list
+
+
+YAML = os.path.join(GOLD, "yaml")
+
+
+def test_reference_policy_files():
+    """The reference's own policy files (networkpolicies/**, copied byte for byte by
+    tests/golden/make_fixtures.py): plain scalars (`pod: b`, `values: [a, b]`), a commented-out line,
+    multi-rule lists.  The simple-example directory loads to config #1's policies in filepath.Walk
+    order, and each fixture file to its policies."""
+    c = json.load(open(os.path.join(GOLD, "config1.json")))
+    got = read_policies_from_path(os.path.join(YAML, "simple-example"))
+    assert json.dumps(got, sort_keys=True) == json.dumps(c["policies"], sort_keys=True)
+    fx = json.load(open(os.path.join(GOLD, "policy_fixtures.json")))
+    for rel, want in fx.items():
+        path = os.path.join(YAML, os.path.relpath(rel, "networkpolicies"))
+        assert json.dumps(read_policies_from_path(path), sort_keys=True) == json.dumps(want, sort_keys=True), rel
+    # the whole tree: every file, directories descended in lexical order
+    every = read_policies_from_path(YAML)
+    assert len(every) == len(c["policies"]) + sum(len(v) for v in fx.values())
