@@ -33,13 +33,12 @@ def load_workload(name: str):
 
     if name != "config5":
         return synth.CONFIGS[name]()
-    from cyclonus_amd.batch import Batch
     from cyclonus_amd.generator import sweep
 
     steps = sweep()
-    bt = Batch(steps)
-    return {"name": "config5", "policies": bt.policies, "resources": bt.resources, "probes": bt.probes, "batch": bt,
-            "steps": steps, "description": f"cyclonus generate sweep: {len(steps)} probe steps batched in one pass"}
+    return {"name": "config5", "steps": steps,
+            "description": f"cyclonus generate sweep: {len(steps)} probe steps batched in one pass, a block per step "
+                           "(only intra-step cells computed)"}
 
 
 def cpu_baseline(data, seconds: float, seed: int = 1):
@@ -137,42 +136,63 @@ def main():
             dist.barrier()
 
     data = load_workload(args.config)
-    # the drop-in's host cost (analyze --mode probe, pkg/cli/analyze.go:121, 232-243): policy build
-    # (BuildNetworkPolicies + Simplify), Resources load and cyc_probe_prepare (interning, job
-    # expansion, table upload) — paid once per probe model, outside `value`
-    pols_json, res_json = json.dumps(data["policies"]), json.dumps(data["resources"])
+    bt = None
+    stream = torch.cuda.current_stream().cuda_stream
+    part = args.partition
     t_prep = time.perf_counter()
     eng = Engine(device)
     for o in args.opt:
         k, v = o.split("=")
         eng.set_option(k, int(v))
-    eng.build_policies(pols_json)
-    t_built = time.perf_counter()
-    eng.load_resources(res_json)
-    t_loaded = time.perf_counter()
-    shape = eng.prepare(data["probes"])
-    torch.cuda.synchronize()
-    t_prepared = time.perf_counter()
-    prepare_s = {"policy_build_s": t_built - t_prep, "resources_load_s": t_loaded - t_built,
-                 "probe_prepare_s": t_prepared - t_loaded, "total_s": t_prepared - t_prep}
-    P, K, W = shape["pods"], shape["slots"], shape["words"]
-    part = args.partition
-    lo, hi = shard_range(P, world, rank, part)
-    rows = hi - lo
+    if "steps" in data:
+        # config #5: the generate sweep's probe problems as blocks of one pass (cyc_probe_prepare_blocks);
+        # N > 1 gives each rank a contiguous share of the problems (independent: no exchange)
+        from cyclonus_amd.batch import Batch
 
-    # shards differ by at most one row (target) / one 64-pod word (source): every rank allocates the
-    # largest, so the optional all-gather (assembled table) moves the planes as they are
-    lays = [eng.layout(*shard_range(P, world, r, part), part) for r in range(world)]
-    ri, wi, re_, we, w0 = lays[rank]
-    max_in = max(x[0] * x[1] for x in lays)
-    max_eg = max(x[2] * x[3] for x in lays)
-    d_in = torch.empty((max(max_in, 1) * K,), dtype=torch.int64, device="cuda")
-    d_eg = torch.empty((max(max_eg, 1) * K,), dtype=torch.int64, device="cuda")
-    d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
+        steps = data["steps"]
+        bt = Batch(steps[rank * len(steps) // world:(rank + 1) * len(steps) // world])
+        shape = bt.prepare(eng)
+        torch.cuda.synchronize()
+        t_prepared = time.perf_counter()
+        prepare_s = {"total_s": t_prepared - t_prep, "note": "policy build + Resources load + cyc_probe_prepare_blocks"}
+        data["policies"] = bt.policies
+        P, K, W = shape["pods"], shape["slots"], shape["words"]
+        lo, hi, rows = 0, P, P
+        d_in, d_eg, d_st = bt.alloc()
 
-    def step():
-        eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), stream, lo, hi, part)
+        def step():
+            eng.run_blocks_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), stream)
+    else:
+        # the drop-in's host cost (analyze --mode probe, pkg/cli/analyze.go:121, 232-243): policy build
+        # (BuildNetworkPolicies + Simplify), Resources load and cyc_probe_prepare (interning, job
+        # expansion, table upload) — paid once per probe model, outside `value`
+        pols_json, res_json = json.dumps(data["policies"]), json.dumps(data["resources"])
+        t_prep = time.perf_counter()
+        eng.build_policies(pols_json)
+        t_built = time.perf_counter()
+        eng.load_resources(res_json)
+        t_loaded = time.perf_counter()
+        shape = eng.prepare(data["probes"])
+        torch.cuda.synchronize()
+        t_prepared = time.perf_counter()
+        prepare_s = {"policy_build_s": t_built - t_prep, "resources_load_s": t_loaded - t_built,
+                     "probe_prepare_s": t_prepared - t_loaded, "total_s": t_prepared - t_prep}
+        P, K, W = shape["pods"], shape["slots"], shape["words"]
+        lo, hi = shard_range(P, world, rank, part)
+        rows = hi - lo
+
+        # shards differ by at most one row (target) / one 64-pod word (source): every rank allocates the
+        # largest, so the optional all-gather (assembled table) moves the planes as they are
+        lays = [eng.layout(*shard_range(P, world, r, part), part) for r in range(world)]
+        ri, wi, re_, we, w0 = lays[rank]
+        max_in = max(x[0] * x[1] for x in lays)
+        max_eg = max(x[2] * x[3] for x in lays)
+        d_in = torch.empty((max(max_in, 1) * K,), dtype=torch.int64, device="cuda")
+        d_eg = torch.empty((max(max_eg, 1) * K,), dtype=torch.int64, device="cuda")
+        d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
+
+        def step():
+            eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), stream, lo, hi, part)
 
     for _ in range(args.warmup):
         step()
@@ -262,6 +282,8 @@ def main():
     # packed planes' device-to-host copy rate
     readback = None
     try:
+        if bt is not None:
+            raise RuntimeError("batched blocks: per-block slabs, no whole-table view")
         torch.cuda.synchronize()
         tab = eng.wrap_table(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), lo, hi, part)
         s_hi = min(hi, lo + 64)
@@ -283,8 +305,12 @@ def main():
         readback = {"error": f"{type(e).__name__}: {e}"}
 
     status = d_st.cpu().numpy()
-    if "batch" in data:  # only the cells inside each batched problem are answers
-        cells = data["batch"].cells(status)
+    if bt is not None:  # the cells of each batched problem (the slabs hold nothing else)
+        cells = bt.cells(status)
+        if world > 1:
+            ct = torch.tensor([cells], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(ct)
+            cells = int(ct.item())
     else:
         valid_slots = int((status == 1).sum())  # (dst, slot) pairs with a VALID job
         cells = P * valid_slots  # every source pod x every valid (dst, slot) job
@@ -297,10 +323,18 @@ def main():
     # by the class-row kernel, the emit copies it to the class's other rows)
     # a source shard's planes differ in row length (ingress: every destination over the shard's
     # words; egress: its sources over all words) and are emitted by one launch each
-    launches = 1 if (ri, wi) == (re_, we) else 2
-    inplace = eng.get_option("class_inplace_active") == 1
-    emit_rows = ri + re_ - (classes_in + classes_eg if inplace else 0)
-    emit_bytes = (ri - (classes_in if inplace else 0)) * K * wi * 8 + (re_ - (classes_eg if inplace else 0)) * K * we * 8
+    if bt is not None:  # k_emit_blocks: every block's slabs (answered cells' bits) and its status rows
+        ri = re_ = P
+        wi = we = W
+        launches = 1
+        inplace = False
+        emit_rows = 2 * P
+        emit_bytes = 2 * int(bt.layout[-1][0]) * 8 + int(bt.layout[-1][1])
+    else:
+        launches = 1 if (ri, wi) == (re_, we) else 2
+        inplace = eng.get_option("class_inplace_active") == 1
+        emit_rows = ri + re_ - (classes_in + classes_eg if inplace else 0)
+        emit_bytes = (ri - (classes_in if inplace else 0)) * K * wi * 8 + (re_ - (classes_eg if inplace else 0)) * K * we * 8
     emit_launch_ms = emit_ms  # both launches when there are two (HIP events around the emit phase)
     achieved = emit_bytes / (emit_launch_ms * 1e-3) / 1e9
 
@@ -311,6 +345,8 @@ def main():
                 "k_emit_wide<256,U> (one single-pass block per row)" if row_bytes >= 16384 else
                 "k_emit_flat (multi-row blocks)")
     emit_kernel = kernel_of(we) if launches == 1 else f"ingress {kernel_of(wi)}; egress {kernel_of(we)}"
+    if bt is not None:
+        emit_kernel = "k_emit_blocks (a workgroup per block: its slabs, bits relative to its first pod)"
 
     # HBM traffic of k_emit from the committed PMC passes for this same workload (rocprofv3
     # --pmc FETCH_SIZE / WRITE_SIZE, corrected per MI355X_MICROARCH.md; scripts/pmc_summary.py)

@@ -55,6 +55,10 @@ EXPORTS = [
     "cyc_probe_run_host_rows",
     "cyc_table_run_rows",
     "cyc_table_wrap_rows",
+    "cyc_probe_prepare_blocks",
+    "cyc_blocks_layout",
+    "cyc_probe_run_blocks",
+    "cyc_block_error",
 ]
 
 # cyc_rows (row partitions for one-process-per-GPU runs)
@@ -129,6 +133,11 @@ def lib():
         L.cyc_probe_run_host_rows.argtypes = [vp, vp, vp, vp, i, i64, i64]
         L.cyc_table_run_rows.argtypes = [vp, i, i64, i64, ctypes.POINTER(vp)]
         L.cyc_table_wrap_rows.argtypes = [vp, vp, vp, vp, i, i64, i64, ctypes.POINTER(vp)]
+        L.cyc_probe_prepare_blocks.argtypes = [vp, cp, sz, vp, vp, i64, ctypes.POINTER(ProbeShape)]
+        L.cyc_blocks_layout.argtypes = [vp, vp, i64]
+        L.cyc_probe_run_blocks.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.cyc_block_error.argtypes = [vp, i64]
+        L.cyc_block_error.restype = cp
         _lib = L
     return _lib
 

@@ -1,20 +1,21 @@
 """Batched small-problem mode (config #5): many independent probe problems in ONE GPU pass.
 
-Each problem (policies, Resources, probe config) becomes a block of one combined problem: its
-namespaces are renamed "<block>~<ns>" everywhere (pods, Resources.Namespaces keys, policy
-metadata.namespace — so the reference's default namespace becomes "<block>~default").  Targets,
-their primary keys and the exact-namespace peer matchers then never cross blocks, so for every
-(source, destination) pair INSIDE a block the verdict is exactly the stand-alone problem's:
-namespace / pod label selectors and IPBlocks can match pods of other blocks only in cross-block
-cells, which are computed but never read.  The probe configs of all problems become slot ranges
-of the combined problem; each block reads the slots of its own config.
+The reference runs each step of a generated test case as its own small table: the interpreter
+calls Runner.RunProbeForConfig per step (pkg/connectivity/interpreter.go:137-148), i.e. its own
+policies, Resources and probe config.  Here every problem becomes a BLOCK of one combined input
+(cyc_probe_prepare_blocks, include/cyclonus_hip.h):
 
-Panics are the exception: the reference panics on the FIRST panicking job of a problem's own table
-(ippeermatcher.go:46-48, labelselector.go:57), but a combined problem also evaluates cross-block
-cells, so one block's unparsable pod IP met by another block's IPBlock peer would panic the whole
-batch although neither problem panics alone.  `run` therefore answers every block from the batched
-pass when that pass does not panic (then no cell panicked, intra-block cells included), and
-otherwise re-runs each problem stand-alone, so each block gets its own table or its own panic.
+* its pods are a consecutive range of the combined Resources.Pods;
+* its namespaces are renamed "<block>~<ns>" everywhere (pods, Resources.Namespaces keys, policy
+  metadata.namespace — so the reference's default namespace becomes "<block>~default"), so a
+  block's targets apply to its own pods only (TargetsApplyingToPod compares namespaces,
+  policy.go:68-82) and its exact-namespace peers match its own pods only;
+* it answers its own probe config only, over its own pods only: the device computes class rows over
+  the block's 64-pod words and writes the block's table as a slab [pods][slots][words] with bits
+  relative to its first pod — the cells computed are the cells answered;
+* a Go panic or table-build fatal is reported per block, as that problem's stand-alone run would
+  report it (its first panicking job in its own job order): one block's bad pod IP does not touch
+  any other block.
 """
 from __future__ import annotations
 
@@ -39,7 +40,7 @@ class Batch:
                 self.probe_index[k] = len(self.probes)
                 self.probes.append(p["probe"])
         pols, pods, nss = [], [], {}
-        self.offsets, self.sizes = [], []
+        self.offsets, self.sizes, self.block_end, self.block_config = [], [], [], []
         for b, p in enumerate(problems):
             pre = f"{b}~"
             for pol in p["policies"]:
@@ -55,69 +56,72 @@ class Batch:
                 q = dict(pod)
                 q["Namespace"] = pre + pod.get("Namespace", "")
                 pods.append(q)
+            self.block_end.append(len(pods))
+            self.block_config.append(self.probe_index[_key(p["probe"])])
         self.policies = pols
         self.resources = {"Namespaces": nss, "Pods": pods}
-        maxc = max((len(p.get("Containers") or []) for p in pods), default=0)
-        self.slot_lo = []
-        lo = 0
-        for pr in self.probes:
-            self.slot_lo.append(lo)
-            lo += maxc if pr.get("AllAvailable") else 1
-        self.K = lo
-        self.maxc = maxc
+        self.maxc = max((len(p.get("Containers") or []) for p in pods), default=0)
 
-    def slots(self, b):
-        c = self.probe_index[_key(self.problems[b]["probe"])]
-        n = self.maxc if self.probes[c].get("AllAvailable") else 1
-        return self.slot_lo[c], self.slot_lo[c] + n
+    def prepare(self, engine):
+        """Load the combined input into `engine` and prepare its blocks."""
+        engine.build_policies(json.dumps(self.policies)).load_resources(json.dumps(self.resources))
+        shape = engine.prepare_blocks(self.probes, self.block_end, self.block_config)
+        self.layout = engine.block_layout  # per block (plane slab offset, status offset); then totals
+        return shape
+
+    def slab_dims(self, b):
+        """(pods, slots, words) of block b's slab."""
+        n = self.sizes[b]
+        k = self.maxc if self.probes[self.block_config[b]].get("AllAvailable") else 1
+        return n, k, (n + 63) // 64
+
+    def alloc(self):
+        """Device slabs (ingress, egress, status) for one run of every block."""
+        import torch
+
+        words, st = (int(x) for x in self.layout[-1])
+        return (torch.empty(max(words, 2), dtype=torch.int64, device="cuda"),
+                torch.empty(max(words, 2), dtype=torch.int64, device="cuda"),
+                torch.empty(max(st, 16), dtype=torch.uint8, device="cuda"))
 
     def cells(self, status):
-        """Valid intra-block cells (the verdicts the batch actually answers)."""
+        """Valid intra-block cells (the verdicts the batch answers) from the host status slab."""
         n = 0
         for b in range(len(self.problems)):
-            o, s = self.offsets[b], self.sizes[b]
-            lo, hi = self.slots(b)
-            n += s * int((status[o : o + s, lo:hi] == 1).sum())
+            p, k, _ = self.slab_dims(b)
+            so = int(self.layout[b][1])
+            n += p * int((status[so : so + p * k] == 1).sum())
         return n
 
-    def extract(self, b, status, ingress, egress):
-        """Block b's own table in the standard layout: (status[P,K], in[P,K,W], eg[P,K,W])."""
-        o, s = self.offsets[b], self.sizes[b]
-        lo, hi = self.slots(b)
-        W = (s + 63) // 64
-
-        def plane(rows):
-            bits = np.unpackbits(rows.view(np.uint8), axis=2, bitorder="little")[:, :, o : o + s]
-            pad = np.zeros((bits.shape[0], bits.shape[1], W * 64), np.uint8)
-            pad[:, :, :s] = bits
-            return np.packbits(pad, axis=2, bitorder="little").view(np.uint64)
-
-        return (status[o : o + s, lo:hi].copy(), plane(ingress[o : o + s, lo:hi]), plane(egress[o : o + s, lo:hi]))
+    def block_table(self, b, status, ingress, egress):
+        """Block b's own table from host copies of the slabs: (status[P,K], in[P,K,W], eg[P,K,W])."""
+        p, k, w = self.slab_dims(b)
+        wo, so = (int(x) for x in self.layout[b])
+        st = status[so : so + p * k].reshape(p, k)
+        ing = ingress[wo : wo + p * k * w].reshape(p, k, w)
+        eg = egress[wo : wo + p * k * w].reshape(p, k, w)
+        if self.probes[self.block_config[b]].get("AllAvailable"):  # the stand-alone table's own max containers
+            kk = max((len(q.get("Containers") or []) for q in self.problems[b]["resources"].get("Pods") or []), default=0)
+            st, ing, eg = st[:, :kk], ing[:, :kk], eg[:, :kk]
+        return st.copy(), ing.copy(), eg.copy()
 
     def run(self, engine):
         """Per block: (status, in, eg) of its own table, or the CyclonusPanic its stand-alone run raises."""
+        import torch
+
         from ._lib import CyclonusPanic
 
-        try:
-            engine.build_policies(json.dumps(self.policies)).load_resources(json.dumps(self.resources))
-            engine.prepare(self.probes)
-            st, ing, eg = engine.run_host()
-            out = []
-            for b, p in enumerate(self.problems):
-                t = self.extract(b, st, ing, eg)
-                if p["probe"].get("AllAvailable"):  # the stand-alone table has its own pods' max containers
-                    k = max((len(q.get("Containers") or []) for q in p["resources"].get("Pods") or []), default=0)
-                    t = (t[0][:, :k], t[1][:, :k], t[2][:, :k])
-                out.append(t)
-            return out
-        except CyclonusPanic:
-            pass
+        self.prepare(engine)
+        d_in, d_eg, d_st = self.alloc()
+        rcs = engine.run_blocks_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        st = d_st.cpu().numpy()
+        ing = d_in.cpu().numpy().view(np.uint64)
+        eg = d_eg.cpu().numpy().view(np.uint64)
         out = []
-        for p in self.problems:  # a cell of the combined problem panicked: each problem on its own
-            try:
-                engine.build_policies(json.dumps(p["policies"])).load_resources(json.dumps(p["resources"]))
-                engine.prepare([p["probe"]])
-                out.append(engine.run_host())
-            except CyclonusPanic as e:
-                out.append(e)
+        for b, (rc, msg) in enumerate(rcs):
+            # the block's own namespace names in a table-build message (pod keys ns/name, job.go)
+            msg = msg.replace(f"FromKey:{b}~", "FromKey:").replace(f"ToKey:{b}~", "ToKey:")
+            out.append(CyclonusPanic(rc, msg) if rc else self.block_table(b, st, ing, eg))
         return out

@@ -881,6 +881,7 @@ struct MemberArgs {
   uint32_t n_act;
   uint32_t* reps;             // class representatives, act[] order within each block (k_classify)
   uint32_t* rep_cnt;          // set to ~0 by k_member: ends at count - 1
+  const uint32_t* id_blk;     // batched blocks: each identity's block (classes never span blocks), else null
 };
 
 __device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* keys, uint32_t cap, uint64_t h) {
@@ -955,6 +956,7 @@ __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t
       h = mix64(h ^ ((st << 40) | uint32_t(d + 1)) ^ (uint64_t(k) << 48));
     }
   }
+  if (a.id_blk) h = mix64(h ^ (uint64_t(a.id_blk[i]) << 24) ^ 0xB10Cull);  // a class row covers one block's words
   h &= 0x7FFFFFFFFFFFFFFFull;  // never the empty key (~0)
   a.cnt[i] = n;
   a.hash[i] = h;
@@ -1005,6 +1007,7 @@ __device__ __forceinline__ void member_wave_blk(MemberArgs a, uint32_t bid_, uin
       h = mix64(h ^ ((st << 40) | uint32_t(d + 1)) ^ (uint64_t(k) << 48));
     }
   }
+  if (a.id_blk) h = mix64(h ^ (uint64_t(a.id_blk[i]) << 24) ^ 0xB10Cull);  // a class row covers one block's words
   h &= 0x7FFFFFFFFFFFFFFFull;  // never the empty key (~0)
   if (lane == 0) {
     a.cnt[i] = n;
@@ -1030,7 +1033,7 @@ __device__ __forceinline__ void classify_blk(MemberArgs a, uint32_t* __restrict_
     uint32_t s = ht_find(a.ht_key, a.ht_cap, a.hash[i]);
     uint32_t r = s == 0xFFFFFFFFu ? i : a.ht_rep[s];
     if (r != i) {  // verify (a 64-bit hash collision must never merge distinct classes)
-      bool eq = a.cnt[r] == a.cnt[i];
+      bool eq = a.cnt[r] == a.cnt[i] && (!a.id_blk || a.id_blk[r] == a.id_blk[i]);
       for (uint32_t j = 0; eq && j < a.cnt[i]; j++) eq = a.list[a.list_off[r] + j] == a.list[a.list_off[i] + j];
       if (eq && a.id_desc) {
         for (uint32_t k = 0; eq && k < a.K; k++) {
@@ -1073,6 +1076,9 @@ struct RowArgs {
   // the word window of the class rows: words [w0, w0 + WA) of each row (a source shard's ingress
   // rows: its sources' words; otherwise 0, W); A rows hold WA words, word w at w - w0
   uint32_t w0, WA;
+  // batched blocks (cyc_probe_prepare_blocks): each identity's own window (its block's words,
+  // (w0, words)), at most WA words; A rows keep the stride WA
+  const uint2* id_win;
   const uint32_t* reps;     // class representatives (k_classify)
   const uint32_t* rep_cnt;  // count = value + 1
   uint32_t rep_blocks;      // block rows of the grid; they stride over the representatives
@@ -1102,6 +1108,8 @@ struct RowArgs {
   const uint32_t* ip_cnz;    // [R][W/64] 1 if the 64-word chunk of an IP peer's PM row was written
   uint32_t pod_sparse;       // PM builds' fused front: pod-peer rows are stored like IP rows (pod_rows_sparse_blk)
   uint32_t E, EW, NB;
+  uint32_t ew_lo, ew_hi;     // IDO identity sets: the identity words the class rows read (a source shard's
+                             // ingress rows: those of its sources' egress identities; else 0, EW)
   uint32_t rpb;              // IDO class rows: representatives per block (class_rows_ido_blk)
   // the direction's hash table (keys + reps), emptied for the NEXT run by the first class-row
   // kernel in block slices once k_classify is done with it: no memset node precedes k_member
@@ -1113,6 +1121,18 @@ struct RowArgs {
 // plane row of the first pod of identity i in the run's rows — that pod's plane row IS the class
 // row, so the emit leaves it alone and copies it to the class's other pods.
 __device__ __forceinline__ uint64_t arow_of(const RowArgs& a, uint32_t i) { return a.arow ? a.arow[i] : i; }
+
+// Words [w0, w0 + wa) of representative i's class rows: the run's window, or its block's.
+__device__ __forceinline__ void rep_window(const RowArgs& a, uint32_t i, uint32_t& w0, uint32_t& wa) {
+  if (a.id_win) {
+    const uint2 v = a.id_win[i];
+    w0 = v.x;
+    wa = v.y;
+  } else {
+    w0 = a.w0;
+    wa = a.WA;
+  }
+}
 
 __device__ __forceinline__ void ht_clear_slice(const RowArgs& a, uint32_t bid, uint32_t nblk) {
   if (!a.ht_clear_words) return;
@@ -1138,14 +1158,17 @@ constexpr uint32_t IDO_LDS_BYTES = 48 * 1024;  // staged identity sets per class
 #define CYC_PB_GROUP 16  // pod peers per identity-set wave (8: +4 % launch B, profiles/r02_pb_group_ab.txt)
 #endif
 constexpr uint32_t PB_GROUP = CYC_PB_GROUP;
+// Identity words [ew0, ew0 + new) of the rows only (a source shard's ingress peers: the words of the
+// egress identities its sources have).
 __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
                                                    const DPeer* __restrict__ peers, const SelView& sv,
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
-                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t bid_, uint32_t nblk_) {
+                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t bid_, uint32_t nblk_,
+                                                   uint32_t ew0, uint32_t new_) {
   const uint32_t wv = bid_ * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t groups = (Rp + PB_GROUP - 1) / PB_GROUP;
-  if (wv >= groups * EW) return;
-  const uint32_t g = wv / EW, ew = wv % EW;
+  if (wv >= groups * new_) return;
+  const uint32_t g = wv / new_, ew = ew0 + wv % new_;
   const uint32_t e = ew * 64 + lane;
   const bool live = e < E;
   const uint32_t ns = live ? id_ns[e] : 0u, nsls = live ? id_nsls[e] : 0u, ls = live ? id_ls[e] : 0u;
@@ -1168,11 +1191,12 @@ __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t 
 __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
                                                    const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres, uint32_t L,
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
-                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob) {
+                                                   const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t ew0,
+                                                   uint32_t new_) {
   SelView sv{};
   sv.selres = selres;
   sv.L = L;
-  peer_bits_blk(Rp, E, EW, pod_peers, peers, sv, id_ns, id_nsls, id_ls, idob, blockIdx.x, gridDim.x);
+  peer_bits_blk(Rp, E, EW, pod_peers, peers, sv, id_ns, id_nsls, id_ls, idob, blockIdx.x, gridDim.x, ew0, new_);
 }
 
 // Per class representative and NB index (ingress: job slot, egress: job descriptor): the set of
@@ -1227,7 +1251,7 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the list is read back by other lanes
   const bool flat = m <= CI_LDS;
-  for (uint32_t ew0 = 0; ew0 < a.EW; ew0 += 64) {
+  for (uint32_t ew0 = a.ew_lo; ew0 < a.ew_hi; ew0 += 64) {
     const uint32_t ew = ew0 + lane;
     uint64_t b[G];
 #pragma unroll
@@ -1280,7 +1304,7 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
         }
       }
     }
-    if (ew < a.EW) {
+    if (ew < a.ew_hi) {
 #pragma unroll
       for (uint32_t x = 0; x < uint32_t(G); x++)
         if (nb0 + x < a.NB) a.B[(uint64_t(i) * a.NB + nb0 + x) * a.EW + ew] = b[x];
@@ -1344,7 +1368,7 @@ __device__ __forceinline__ uint64_t port_mask(const RowArgs& a, const uint8_t* p
 constexpr uint32_t PEER_BATCH = CYC_PEER_BATCH;  // IDO class rows: IP peers whose PM words are loaded at once
 
 template <bool EGRESS, bool ERR, int KC>
-__device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uint32_t kc, uint32_t w) {
+__device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uint32_t kc, uint32_t w, uint32_t w0) {
   const uint32_t k0 = kc * KC;
   const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
   const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
@@ -1425,7 +1449,7 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
   for (int kk = 0; kk < KC; kk++) {
     uint32_t k = k0 + kk;
     if (k < a.K) {
-      uint64_t idx = (uint64_t(i) * a.K + k) * a.WA + (w - a.w0);
+      uint64_t idx = (uint64_t(i) * a.K + k) * a.WA + (w - w0);
       a.A[idx] = allow[kk] & valid[kk];
       if (ERR) a.AE[idx] = err[kk] & valid[kk];
     }
@@ -1441,10 +1465,13 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
   ht_clear_slice(a, blockIdx.x, gridDim.x);
   const uint32_t chunks = (a.WA + 255) / 256, nkc = (a.K + KC - 1) / KC;
   const uint32_t kc = (blockIdx.x / chunks) % nkc;
-  const uint32_t w = a.w0 + (blockIdx.x % chunks) * 256 + threadIdx.x;
-  if (w >= a.w0 + a.WA) return;
+  const uint32_t lw = (blockIdx.x % chunks) * 256 + threadIdx.x;
   const uint32_t r = blockIdx.x / (chunks * nkc);
-  if (r < *a.rep_cnt + 1u) class_row_word<EGRESS, true, KC>(a, a.reps[r], kc, w);
+  if (r >= *a.rep_cnt + 1u) return;
+  const uint32_t i = a.reps[r];
+  uint32_t w0, wa;
+  rep_window(a, i, w0, wa);
+  if (lw < wa) class_row_word<EGRESS, true, KC>(a, i, kc, w0 + lw, w0);
 }
 
 // Class rows of PM builds without a panic.  Block = class representative (blocks stride over
@@ -1498,7 +1525,8 @@ constexpr int PL_ITEMS = CYC_PL_ITEMS;
 // PL_ITEMS (slot chunk, pod word) items of class representative i: items it0, it0 + blockDim.x, ...
 template <bool EGRESS>
 __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, const uint4* spill, uint32_t i, uint32_t m,
-                                         bool allow_all, bool kbits, uint32_t it0, uint32_t items, uint64_t lastmask) {
+                                         bool allow_all, bool kbits, uint32_t it0, uint32_t items, uint64_t lastmask,
+                                         uint32_t w0, uint32_t wa) {
   constexpr int KC = 4, NI = PL_ITEMS;
   uint64_t valid[NI][KC], allow[NI][KC];
   int32_t du[NI][KC];
@@ -1508,8 +1536,8 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
   for (int q = 0; q < NI; q++) {
     const uint32_t it = it0 + q * blockDim.x;
     const bool live = it < items;
-    const uint32_t kc = live ? it / a.WA : 0u;
-    w[q] = a.w0 + (live ? it - kc * a.WA : 0u);
+    const uint32_t kc = live ? it / wa : 0u;
+    w[q] = w0 + (live ? it - kc * wa : 0u);
     k0[q] = live ? kc * KC : a.K;  // a dead item has no slot
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
@@ -1609,7 +1637,7 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
       const uint32_t k = k0[q] + kk;
-      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.WA + (w[q] - a.w0)] = allow[q][kk] & valid[q][kk];
+      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.WA + (w[q] - w0)] = allow[q][kk] & valid[q][kk];
     }
 }
 
@@ -1646,16 +1674,16 @@ __device__ __forceinline__ PlLane pl_lane(const RowArgs& a, const uint4* src, ui
 
 template <bool EGRESS>
 __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared& sh, const uint4* spill, uint32_t i,
-                                               uint32_t m, bool allow_all, uint64_t lastmask) {
+                                               uint32_t m, bool allow_all, uint64_t lastmask, uint32_t w0, uint32_t wa) {
   static_assert(PL_LDS % 64 == 0, "a lane group of entries is all in LDS or all spilled");
   const uint32_t lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
   // the chunks holding the window's words (<= 64 chunks in all: pl_wave_ok)
-  const uint32_t cend = (a.w0 + a.WA + 63) / 64;
+  const uint32_t cend = (w0 + wa + 63) / 64;
   const PlLane g0 = pl_lane(a, sh.e, lane, m);  // entries 0..63, one per lane, for every chunk
-  for (uint32_t c = a.w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cend; c += nwaves) {
+  for (uint32_t c = w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cend; c += nwaves) {
     const uint32_t w = c * 64 + lane;
-    const bool live = w >= a.w0 && w < a.w0 + a.WA;
-    const uint32_t wl = live ? w : a.w0;  // dead lanes load a valid word and store nothing
+    const bool live = w >= w0 && w < w0 + wa;
+    const uint32_t wl = live ? w : w0;  // dead lanes load a valid word and store nothing
     uint64_t valid[PL_NB];
     int32_t du[PL_NB];
 #pragma unroll
@@ -1719,7 +1747,7 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
           if (d < a.D) r |= acc[d] & dm[uint64_t(d) * a.W];
         r &= valid[k];
       }
-      a.A[(arow_of(a, i) * a.K + k) * a.WA + (w - a.w0)] = r;
+      a.A[(arow_of(a, i) * a.K + k) * a.WA + (w - w0)] = r;
     }
   }
 }
@@ -1728,7 +1756,7 @@ template <bool EGRESS, bool WAVE>
 __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
   ht_clear_slice(a, bid_, nblk_);
-  const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC, items = nkc * a.WA;
+  const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC;
   const bool kbits = EGRESS ? a.portbits != nullptr : a.K <= 32;
   for (uint32_t r = bid_; r < n_reps; r += nblk_) {
     const uint32_t i = a.reps[r];
@@ -1818,11 +1846,14 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     const bool allow_all = nt == 0 || sh.all;
     const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
     // the class's (slot chunk, word) items, PL_ITEMS per thread at once (their loads overlap)
+    uint32_t w0, wa;
+    rep_window(a, i, w0, wa);
     if (WAVE) {
-      pl_wave_chunks<EGRESS>(a, sh, spill, i, m, allow_all, lastmask);
+      pl_wave_chunks<EGRESS>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
     } else {
+      const uint32_t items = nkc * wa;
       for (uint32_t it0 = threadIdx.x; it0 < items; it0 += PL_ITEMS * blockDim.x)
-        pl_items<EGRESS>(a, sh, spill, i, m, allow_all, kbits, it0, items, lastmask);
+        pl_items<EGRESS>(a, sh, spill, i, m, allow_all, kbits, it0, items, lastmask, w0, wa);
     }
     __syncthreads();  // LDS reused by the next representative
   }
@@ -2016,12 +2047,14 @@ struct FrontB {
   uint64_t* PM;
   uint32_t* rng;
   uint32_t* cnz;
-  uint32_t Ru, E, EW, L;
-  const uint32_t* pod_peers_u;
+  uint32_t E, EW, L;
+  // identity sets (IDO builds) per segment x: its pod peers and identity word window
+  uint32_t Ru_[2], ew0[2], new_[2];
+  const uint32_t* pod_peers_u_[2];
+  uint64_t* idob_[2];
   const DPeer* peers;
   const uint8_t* selres;
   const uint32_t *id_ns, *id_nsls, *id_ls;
-  uint64_t* idob;
   MemberArgs ma[2];
   uint32_t member_wave[2];  // 1: a wave per identity (k_member_wave), 0: a thread per identity
 };
@@ -2040,7 +2073,8 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
       if (f.pod_direct)
         return pod_rows_direct_blk<false>(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls,
                                           f.id_ls, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
-      return peer_bits_blk(f.Ru, f.E, f.EW, f.pod_peers_u, f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob, b, f.nb[2 + x]);
+      return peer_bits_blk(f.Ru_[x], f.E, f.EW, f.pod_peers_u_[x], f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob_[x], b,
+                           f.nb[2 + x], f.ew0[x], f.new_[x]);
     }
     b -= f.nb[2 + x];
   }
@@ -2166,6 +2200,11 @@ __global__ __launch_bounds__(256) CYC_PL_WAVES void k_front_d_pm(FrontRows f) {
 #define CYC_E_KC 4  // job slots per thread in the fused IDO class rows (k_front_e)
 #endif
 constexpr int E_KC = CYC_E_KC;
+#ifndef CYC_E_SPLIT
+#define CYC_E_SPLIT 1  // 1: launch E as one kernel per direction (k_class_rows_ido, each at its own register
+                       // budget: egress 101 VGPRs, ingress 61) instead of k_front_e (both at 101): config #3
+                       // 189 -> 170 us (profiles/r03_e_split_ab.txt)
+#endif
 __global__ __launch_bounds__(256) CYC_E_WAVES void k_front_e(FrontRows f) {
   const uint32_t b = blockIdx.x;
   if (b < f.nb[1]) class_rows_ido_blk<true, E_KC>(f.ra[1], b, f.nb[1]);
@@ -2320,6 +2359,83 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
 #pragma unroll
     for (int u = 0; u < UNROLL; u++)
       if (x0 + u * BS < n2) __builtin_nontemporal_store(v[u], &di[x0 + u * BS]);
+  }
+}
+
+// Batched blocks (cyc_probe_prepare_blocks): block b's own table, bits relative to its first pod.
+// One workgroup per block sweeps its output words — ingress[d][k][j], egress[s][k][j] for its pods
+// and its probe config's slots — each the class row's words [j, j + 1] of the block's window
+// shifted down by the block's first pod's bit, masked to its pods; and its status rows.  The bytes
+// written are exactly the answered cells' bits plus their status.
+struct BlockArgs {
+  uint32_t n_blk, K, AS;               // blocks, slots of the class rows, A row stride (words)
+  const uint4* blk;                     // per block: (first pod, pods, first slot, slots)
+  const uint64_t* boff;                 // per block: plane slab offset (words), status offset (bytes)
+  const uint32_t *pod_id[2], *class_of[2];
+  const uint64_t* A[2];
+  const uint8_t* st_src;                // [P][K]
+  uint64_t* out[2];
+  uint8_t* st_out;
+};
+__global__ __launch_bounds__(256) void k_emit_blocks(BlockArgs a) {
+  const uint32_t b = blockIdx.x;
+  if (b >= a.n_blk) return;
+  const uint4 bl = a.blk[b];  // (p0, np, k0, nk)
+  const uint32_t p0 = bl.x, np = bl.y, k0 = bl.z, nk = bl.w, wb = (np + 63) / 64, sh = p0 % 64;
+  const uint32_t wa = (p0 + np + 63) / 64 - p0 / 64;  // the class rows' window words
+  const uint64_t n = uint64_t(np) * nk * wb, off = a.boff[2 * b];
+  const uint64_t tail = np % 64 ? (1ull << (np % 64)) - 1 : ~0ull;
+  for (uint64_t x = threadIdx.x; x < 2 * n; x += blockDim.x) {
+    const uint32_t pl = x >= n ? 1u : 0u;
+    const uint64_t y = x - pl * n;
+    const uint32_t j = uint32_t(y % wb), k = uint32_t((y / wb) % nk), q = uint32_t(y / (uint64_t(wb) * nk));
+    const uint32_t c = a.class_of[pl][a.pod_id[pl][p0 + q]];
+    const uint64_t* row = a.A[pl] + (uint64_t(c) * a.K + k0 + k) * a.AS;
+    uint64_t v = row[j] >> sh;
+    if (sh && j + 1 < wa) v |= row[j + 1] << (64 - sh);
+    if (j == wb - 1) v &= tail;
+    a.out[pl][off + y] = v;
+  }
+  const uint64_t soff = a.boff[2 * b + 1];
+  for (uint32_t x = threadIdx.x; x < np * nk; x += blockDim.x)
+    a.st_out[soff + x] = a.st_src[uint64_t(p0 + x / nk) * a.K + k0 + x % nk];
+}
+
+// First panicking job of every block in its own job order (key ((s - p0) * np + d - p0) * 65536 +
+// job index, resources.go:286-333): thread per (source, destination of its block).
+struct BlockErrArgs {
+  uint32_t n_blk, P, K, AS;
+  const uint4* blk;
+  const uint32_t* pod_blk;
+  const uint32_t* slot_idx;
+  const uint8_t* slot_status;
+  const uint32_t *pod_iid, *pod_eid, *class_in, *class_eg;
+  const uint8_t *err_in, *err_eg;
+  const uint64_t *AE_in, *AE_eg;
+  unsigned long long* first;  // [n_blk]
+  uint32_t dchunks;           // 256-destination chunks of the largest block
+};
+__global__ __launch_bounds__(256) void k_first_error_blocks(BlockErrArgs a) {
+  const uint64_t n = uint64_t(a.P) * a.dchunks;
+  for (uint64_t g = blockIdx.x; g < n; g += gridDim.x) {
+    const uint32_t s = uint32_t(g / a.dchunks), b = a.pod_blk[s];
+    const uint4 bl = a.blk[b];
+    const uint32_t dl = uint32_t(g % a.dchunks) * blockDim.x + threadIdx.x;
+    if (dl >= bl.y) continue;
+    const uint32_t d = bl.x + dl, w0 = bl.x / 64;
+    const bool s_err = a.err_eg[a.pod_eid[s]], d_err = a.err_in[a.pod_iid[d]];
+    const uint32_t ci = a.class_in[a.pod_iid[d]], ce = a.class_eg[a.pod_eid[s]];
+    unsigned long long best = ~0ull;
+    for (uint32_t k = bl.z; k < bl.z + bl.w; k++) {
+      if (a.slot_status[uint64_t(d) * a.K + k] != CYC_JOB_VALID) continue;
+      bool e = d_err || s_err;
+      if (!e) e = (a.AE_in[(uint64_t(ci) * a.K + k) * a.AS + (s / 64 - w0)] >> (s % 64)) & 1;
+      if (!e) e = (a.AE_eg[(uint64_t(ce) * a.K + k) * a.AS + (d / 64 - w0)] >> (d % 64)) & 1;
+      if (!e) continue;
+      const unsigned long long key = (uint64_t(s - bl.x) * bl.y + dl) * 65536ull + a.slot_idx[k];
+      best = key < best ? key : best;
+    }
+    if (best != ~0ull) atomicMin(&a.first[b], best);
   }
 }
 
@@ -2726,12 +2842,19 @@ struct cyc_ctx {
   // those words); target-row plans: both directions [lo, hi), window [0, W)
   int64_t rl[2] = {0, 0}, rh[2] = {0, 0};
   uint32_t win_w0 = 0, win_wa = 0;
+  uint32_t ido_ew0 = 0, ido_ew1 = 0;  // ingress identity sets: egress-identity words of the window's sources
   uint32_t scan_off[3] = {0, 0, 0}, post_off[3] = {0, 0, 0};  // pp_scan / pp_post: ingress peers, then egress
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   double last_ms[3] = {0, 0, 0};
   bool timed = false;  // the last run recorded the step timing events
   bool ran = false;    // a run has been enqueued
   hipEvent_t run_done = nullptr;  // recorded on the run's stream after every run (cyc_last_classes)
+  // batched blocks (cyc_probe_prepare_blocks; pb.blocks non-empty)
+  DevBuf blk, blk_off, id_blk[2], id_win[2], first_blk;
+  uint32_t blk_wa_max = 0, blk_np_max = 0;
+  std::vector<uint64_t> blk_off_h;          // per block: plane slab offset (words), status offset (bytes); then totals
+  std::vector<int> blk_rc;                  // per block status of the last run
+  std::vector<std::string> blk_msg;         // and its message
 };
 
 int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t idx);
@@ -2866,6 +2989,48 @@ static uint64_t ido_lds_bytes(const cyc_ctx* c) {  // k_class_rows_ido: staged i
 static bool ido_possible(const cyc_ctx* c) {
   return !c->pb.may_err && c->plan.max_runs <= IDO_MAX_RUNS && ido_lds_bytes(c) <= IDO_LDS_BYTES &&
          ido_b_bytes(c, 0) + ido_b_bytes(c, 1) <= (1ull << 30);
+}
+
+// Batched blocks: per block (first pod, pods, first slot, slots) and its output slab offsets; per
+// identity its block and class-row window (its block's words).
+static void prepare_blocks_device(cyc_ctx* c) {
+  Problem& pb = c->pb;
+  c->blk_off_h.clear();
+  c->blk_wa_max = c->blk_np_max = 0;
+  if (pb.blocks.empty()) return;
+  std::vector<uint32_t> cfg_k0(pb.n_cfg + 1, pb.K), cfg_nk(pb.n_cfg, 0);
+  for (uint32_t k = pb.K; k-- > 0;) cfg_k0[pb.slot_cfg[k]] = k;
+  for (uint32_t k = 0; k < pb.K; k++) cfg_nk[pb.slot_cfg[k]]++;
+  std::vector<uint4> bl(pb.blocks.size());
+  uint64_t words = 0, bytes = 0;
+  for (size_t b = 0; b < pb.blocks.size(); b++) {
+    const ProbeBlock& x = pb.blocks[b];
+    const uint32_t np = x.p1 - x.p0, nk = cfg_nk[x.cfg];
+    bl[b] = uint4{x.p0, np, cfg_k0[x.cfg], nk};
+    c->blk_off_h.push_back(words);
+    c->blk_off_h.push_back(bytes);
+    words += uint64_t(np) * nk * ((np + 63) / 64);
+    bytes += uint64_t(np) * nk;
+    c->blk_wa_max = std::max<uint32_t>(c->blk_wa_max, np ? (x.p1 + 63) / 64 - x.p0 / 64 : 0u);
+    c->blk_np_max = std::max(c->blk_np_max, np);
+  }
+  c->blk_off_h.push_back(words);
+  c->blk_off_h.push_back(bytes);
+  upload(c->blk, bl);
+  upload(c->blk_off, c->blk_off_h);
+  for (int d = 0; d < 2; d++) {
+    const Identities& I = c->ids[d];
+    std::vector<uint32_t> ib(I.ns.size(), 0);
+    std::vector<uint2> iw(I.ns.size(), uint2{0, 0});
+    for (uint32_t q = 0; q < pb.P; q++) {
+      const ProbeBlock& x = pb.blocks[pb.pod_blk[q]];
+      ib[I.of_pod[q]] = pb.pod_blk[q];
+      iw[I.of_pod[q]] = uint2{x.p0 / 64, (x.p1 + 63) / 64 - x.p0 / 64};
+    }
+    upload(c->id_blk[d], ib);
+    upload(c->id_win[d], iw);
+  }
+  c->first_blk.alloc(std::max<uint64_t>(pb.blocks.size() * 8, 16));
 }
 
 static void prepare_device(cyc_ctx* c) {
@@ -3073,6 +3238,7 @@ static void prepare_device(cyc_ctx* c) {
       dd.ip_list.alloc(std::max<uint64_t>(uint64_t(off[dd.n]) * 16, 16));
     }
   }
+  prepare_blocks_device(c);
   c->order_lo = c->order_hi = -1;
   c->order_src = false;
 }
@@ -3160,6 +3326,7 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   a.n_act = c->n_act[d];
   a.reps = dd.reps.as<uint32_t>();
   a.rep_cnt = dd.rep_cnt();
+  a.id_blk = c->pb.blocks.empty() ? nullptr : c->id_blk[d].as<uint32_t>();
   return a;
 }
 
@@ -3189,6 +3356,21 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   c->win_w0 = src ? uint32_t(lo / 64) : 0u;
   c->win_wa = src ? uint32_t((hi + 63) / 64 - lo / 64) : pb.W;
   if (src && hi <= lo) c->win_wa = 0;
+  {  // the egress identities of the window's pods (identity ids follow first appearance in pod order, so a
+     // source shard's are mostly one range): the ingress identity sets need only their words
+    const uint32_t EW = uint32_t((c->ids[1].ns.size() + 63) / 64);
+    c->ido_ew0 = 0;
+    c->ido_ew1 = EW;
+    if (src) {
+      uint32_t e0 = UINT32_MAX, e1 = 0;
+      for (int64_t q = c->win_w0 * 64ll; q < std::min<int64_t>(int64_t(c->win_w0 + c->win_wa) * 64, pb.P); q++) {
+        e0 = std::min(e0, c->ids[1].of_pod[size_t(q)]);
+        e1 = std::max(e1, c->ids[1].of_pod[size_t(q)] + 1);
+      }
+      c->ido_ew0 = e0 == UINT32_MAX ? 0u : e0 / 64;
+      c->ido_ew1 = e0 == UINT32_MAX ? 0u : (e1 + 63) / 64;
+    }
+  }
   for (int d = 0; d < 2; d++) {  // emit row order: clustered by this direction's identity
     std::vector<uint32_t> ord(size_t(c->rh[d] - c->rl[d]));
     std::iota(ord.begin(), ord.end(), uint32_t(c->rl[d]));
@@ -3378,7 +3560,7 @@ ports:
 // Pod peers folded into per-class identity sets, expanded by the class rows over each word's
 // identity runs (no PM pod rows)?  Needs: no panic possible (the panic path walks PM / ER rows in
 // peer order), few runs per word, and identity sets of bounded size.
-static bool ido_mode(const cyc_ctx* c) { return c->pod_words != 0 && ido_possible(c); }
+static bool ido_mode(const cyc_ctx* c) { return c->pod_words != 0 && c->pb.blocks.empty() && ido_possible(c); }
 
 // 2. peer rows of direction d's peers: pod peers in identity space, expanded over word runs
 // (skipped in IDO mode: the class rows expand them); IP peers per pod
@@ -3400,11 +3582,15 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
   const uint32_t r0 = c->rp_off[dlo], Rp = (which & PEERS_POD) ? c->rp_off[dhi] - r0 : 0u;
   if (Rp && E && W && ido_mode(c)) {
     const uint32_t EW = (E + 63) / 64;
-    const uint32_t u0 = c->rpu_off[dlo], Ru = c->rpu_off[dhi] - u0;  // distinct matchers only
-    k_peer_bits<<<unsigned((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4), 256, 0, st>>>(
-        Ru, E, EW, c->pod_peers_u.as<uint32_t>() + u0, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
-        c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(),
-        c->idob.as<uint64_t>() + uint64_t(u0) * EW);
+    for (int x = dlo; x < dhi; x++) {  // per direction: its identity word window
+      const uint32_t u0 = c->rpu_off[x], Ru = c->rpu_off[x + 1] - u0;  // distinct matchers only
+      const uint32_t ew0 = x == 0 ? c->ido_ew0 : 0u, new_ = x == 0 ? c->ido_ew1 - c->ido_ew0 : EW;
+      if (Ru && new_)
+        k_peer_bits<<<unsigned((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * new_ + 3) / 4), 256, 0, st>>>(
+            Ru, E, EW, c->pod_peers_u.as<uint32_t>() + u0, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
+            c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(),
+            c->idob.as<uint64_t>() + uint64_t(u0) * EW, ew0, new_);
+    }
   } else if (Rp && E && nw && (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= P)) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
     const unsigned g = unsigned((uint64_t(Rp) * nw + 3) / 4);
@@ -3503,6 +3689,11 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.W = W;
   ra.P = P;
   peer_window(c, d, ra.w0, ra.WA);  // the class rows cover their peers' word window
+  if (!c->pb.blocks.empty()) {     // batched blocks: each class row covers its block's words
+    ra.w0 = 0;
+    ra.WA = c->blk_wa_max;
+    ra.id_win = c->id_win[d].as<uint2>();
+  }
   ra.class_of = dd.class_of.as<uint32_t>();
   ra.cnt = dd.cnt.as<uint32_t>();
   ra.list_off = dd.list_off.as<uint32_t>();
@@ -3529,6 +3720,8 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.ip_cnz = ip_cnz(c);
   ra.E = c->dir[1].n;
   ra.EW = (ra.E + 63) / 64;
+  ra.ew_lo = d == 0 ? c->ido_ew0 : 0u;
+  ra.ew_hi = d == 0 ? c->ido_ew1 : ra.EW;
   ra.NB = d == 0 ? K : D;
   // the first kernel below empties the hash table for the next run (keys + reps; not the counter)
   ra.ht_clear = reinterpret_cast<uint32_t*>(dd.ht_key.p);
@@ -3582,6 +3775,9 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // shard's word window, egress rows of its sources over all words).  d_status (may be null): the
 // status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
 // in the plan; the caller then copies the status plane itself).
+#ifndef CYC_EMIT_WIDE_MIN
+#define CYC_EMIT_WIDE_MIN 16384  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
+#endif
 static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out_in, uint64_t* out_eg) {
   EmitArgs ea = ea_in;
   ea.per_xcd = (ea.n_rows[0] + ea.n_rows[1] + 7) / 8;
@@ -3600,9 +3796,10 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     else if (need <= 13) k_emit_wide<512, 13><<<g, 512, 0, st>>>(ea);
     else if (need <= 14) k_emit_wide<512, 14><<<g, 512, 0, st>>>(ea);
     else k_emit_wide<512, 16><<<g, 512, 0, st>>>(ea);
-  } else if (row_bytes >= 16384) {  // 256-thread single pass (16-64 KB rows)
+  } else if (row_bytes >= CYC_EMIT_WIDE_MIN) {  // 256-thread single pass (16-64 KB rows)
     const uint64_t need = (ea.row_words / 2 + 255) / 256;
-    if (need <= 4) k_emit_wide<256, 4><<<g, 256, 0, st>>>(ea);
+    if (need <= 2) k_emit_wide<256, 2><<<g, 256, 0, st>>>(ea);
+    else if (need <= 4) k_emit_wide<256, 4><<<g, 256, 0, st>>>(ea);
     else if (need <= 6) k_emit_wide<256, 6><<<g, 256, 0, st>>>(ea);
     else if (need <= 7) k_emit_wide<256, 7><<<g, 256, 0, st>>>(ea);
     else if (need <= 8) k_emit_wide<256, 8><<<g, 256, 0, st>>>(ea);
@@ -3615,8 +3812,32 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
   }
 }
 
+static bool enq_emit_blocks(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, uint8_t* d_status) {
+  Problem& pb = c->pb;
+  if (pb.blocks.empty()) return false;
+  if (!pb.K || !d_status) return true;  // nothing to write (the status plane of blocks is their slabs)
+  BlockArgs ba{};
+  ba.n_blk = uint32_t(pb.blocks.size());
+  ba.K = pb.K;
+  ba.AS = c->blk_wa_max;
+  ba.blk = c->blk.as<uint4>();
+  ba.boff = c->blk_off.as<uint64_t>();
+  for (int pl = 0; pl < 2; pl++) {
+    ba.pod_id[pl] = c->dir[pl].pod_id.as<uint32_t>();
+    ba.class_of[pl] = c->dir[pl].class_of.as<uint32_t>();
+    ba.A[pl] = c->dir[pl].A.as<uint64_t>();
+  }
+  ba.st_src = c->slot_status.as<uint8_t>();
+  ba.out[0] = out_in;
+  ba.out[1] = out_eg;
+  ba.st_out = d_status;
+  k_emit_blocks<<<ba.n_blk, c->blk_np_max * 2 > 128 ? 256 : 128, 0, st>>>(ba);
+  return true;
+}
+
 static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, uint8_t* d_status, bool inplace = false) {
   Problem& pb = c->pb;
+  if (!pb.blocks.empty()) return enq_emit_blocks(c, st, out_in, out_eg, d_status);
   const uint32_t K = pb.K;
   const uint64_t rw[2] = {uint64_t(K) * c->win_wa, uint64_t(K) * pb.W};  // words per plane row
   uint32_t nr[2];
@@ -3679,7 +3900,7 @@ static bool front_fused_ok(const cyc_ctx* c) {
 // #3u -7 %); with few identities the rows saved are few while the class rows, scattered over the
 // planes, write slower (config #3: 2 % of the rows, net +1 %: profiles/r02_class_inplace_ab.txt).
 static bool inplace_ok(const cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg) {
-  if (!c->class_inplace || !d_in || !d_eg || !front_fused_ok(c)) return false;
+  if (!c->class_inplace || !d_in || !d_eg || !front_fused_ok(c) || !c->pb.blocks.empty()) return false;
   const uint64_t rows = uint64_t(std::max<int64_t>((c->rh[0] - c->rl[0] + c->rh[1] - c->rl[1]) / 2, 1));
   return c->class_inplace == 1 || uint64_t(c->n_act[0] + c->n_act[1]) * 16 >= 2 * rows;
 }
@@ -3749,20 +3970,24 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     peer_chunks(c, one_win ? 1 : x, fb.ic0[x], fb.inch[x]);
     fb.nb[x] = fb.Ri[x] && fb.inch[x] ? blocks(ip_rows_blocks(fb.Ri[x], fb.inch[x], fb.ip_grp)) : 0u;
   }
-  const uint32_t Rp = c->rp_off[2] - c->rp_off[0], u0 = c->rpu_off[0], Ru = c->rpu_off[2] - u0;
-  fb.Ru = Ru;
   fb.E = E;
   fb.EW = EW;
   fb.L = pb.L;
-  fb.pod_peers_u = c->pod_peers_u.as<uint32_t>() + u0;
   fb.peers = c->peers.as<DPeer>();
   fb.selres = c->selres.as<uint8_t>();
   fb.id_ns = c->dir[1].id_ns.as<uint32_t>();
   fb.id_nsls = c->id_nsls.as<uint32_t>();
   fb.id_ls = c->dir[1].id_ls.as<uint32_t>();
-  fb.idob = c->idob.as<uint64_t>() + uint64_t(u0) * EW;
   fb.sv = sel_view(c);
-  fb.nb[2] = (Rp && E) ? blocks((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * EW + 3) / 4) : 0u;  // identity sets
+  for (int x = 0; x < 2; x++) {  // identity sets per direction: the ingress ones over the window's identity words
+    const uint32_t ux = c->rpu_off[x];
+    fb.Ru_[x] = c->rpu_off[x + 1] - ux;
+    fb.pod_peers_u_[x] = c->pod_peers_u.as<uint32_t>() + ux;
+    fb.idob_[x] = c->idob.as<uint64_t>() + uint64_t(ux) * EW;
+    fb.ew0[x] = x == 0 ? c->ido_ew0 : 0u;
+    fb.new_[x] = x == 0 ? c->ido_ew1 - c->ido_ew0 : EW;
+    fb.nb[2 + x] = (fb.Ru_[x] && E && fb.new_[x]) ? blocks((uint64_t((fb.Ru_[x] + PB_GROUP - 1) / PB_GROUP) * fb.new_[x] + 3) / 4) : 0u;
+  }
   const bool ido = ido_mode(c);
   FrontC fc{};
   if (!ido && !pod_sparse(c)) {  // PM builds, few pod-peer words: full rows, a wave per (pod peer, word)
@@ -3776,7 +4001,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
       fb.nb[2 + x] = (fb.Rp[x] && E && fb.pnw[x]) ? blocks((uint64_t(fb.Rp[x]) * fb.pnw[x] + 3) / 4) : 0u;
     }
   } else if (!ido) {  // PM builds: sparse pod-peer rows in launch C (k_front_c)
-    fb.nb[2] = 0;
+    fb.nb[2] = fb.nb[3] = 0;
     fc.P = P;
     fc.W = W;
     fc.req_post = c->req_post.as<uint4>();
@@ -3861,7 +4086,10 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     return true;
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
-  if (fe.nb[0] + fe.nb[1]) {
+  if (CYC_E_SPLIT) {  // the directions' class rows as two launches, each at its own register budget
+    if (fe.nb[1]) k_class_rows_ido<true, E_KC><<<fe.nb[1], 256, lds, st>>>(fe.ra[1]);
+    if (fe.nb[0]) k_class_rows_ido<false, E_KC><<<fe.nb[0], 256, lds, st>>>(fe.ra[0]);
+  } else if (fe.nb[0] + fe.nb[1]) {
     k_front_e<<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
   }
   if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
@@ -3964,6 +4192,64 @@ static void ensure_cap_streams(cyc_ctx* c) {
   HIPCHK(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
 }
 
+// Batched blocks: each block's status, as its stand-alone run would end — the job expansion's
+// panic, else its first panicking job (its own job order), else its table build's duplicate key —
+// into c->blk_rc / c->blk_msg.  Synchronises only when the inputs can panic.
+static int blocks_status(cyc_ctx* c, hipStream_t st) {
+  Problem& pb = c->pb;
+  const size_t nb = pb.blocks.size();
+  c->blk_rc.assign(nb, CYC_OK);
+  c->blk_msg.assign(nb, "");
+  std::vector<unsigned long long> first(nb, ~0ull);
+  if (pb.may_err && pb.P && pb.K) {
+    HIPCHK(hipMemsetAsync(c->first_blk.p, 0xFF, nb * 8, st));
+    BlockErrArgs e{};
+    e.n_blk = uint32_t(nb);
+    e.P = pb.P;
+    e.K = pb.K;
+    e.AS = c->blk_wa_max;
+    e.blk = c->blk.as<uint4>();
+    e.pod_blk = nullptr;
+    e.slot_idx = c->slot_idx.as<uint32_t>();
+    e.slot_status = c->slot_status.as<uint8_t>();
+    e.pod_iid = c->dir[0].pod_id.as<uint32_t>();
+    e.pod_eid = c->dir[1].pod_id.as<uint32_t>();
+    e.class_in = c->dir[0].class_of.as<uint32_t>();
+    e.class_eg = c->dir[1].class_of.as<uint32_t>();
+    e.err_in = c->dir[0].err.as<uint8_t>();
+    e.err_eg = c->dir[1].err.as<uint8_t>();
+    e.AE_in = c->dir[0].AE.as<uint64_t>();
+    e.AE_eg = c->dir[1].AE.as<uint64_t>();
+    e.first = c->first_blk.as<unsigned long long>();
+    e.dchunks = (c->blk_np_max + 255) / 256;
+    DevBuf pod_blk;
+    upload(pod_blk, pb.pod_blk);
+    e.pod_blk = pod_blk.as<uint32_t>();
+    if (c->dir[0].n && c->dir[1].n)
+      k_first_error_blocks<<<grid1(uint64_t(pb.P) * e.dchunks, 1), 256, 0, st>>>(e);
+    HIPCHK(hipMemcpyAsync(first.data(), c->first_blk.p, nb * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  const std::string saved = c->err;
+  for (size_t b = 0; b < nb; b++) {
+    const ProbeBlock& x = pb.blocks[b];
+    if (pb.blk_expand_panic[b]) {
+      c->blk_rc[b] = CYC_ERR_PANIC_RUNTIME;
+      c->blk_msg[b] = "runtime error: index out of range [0] with length 0";
+    } else if (first[b] != ~0ull) {
+      const uint32_t np = x.p1 - x.p0, idx = uint32_t(first[b] % 65536);
+      const uint64_t rest = first[b] / 65536;
+      c->blk_rc[b] = describe_panic(c, x.p0 + uint32_t(rest / np), x.p0 + uint32_t(rest % np), x.cfg, idx);
+      c->blk_msg[b] = c->err;
+    } else if (!pb.blk_dup_msg[b].empty()) {
+      c->blk_rc[b] = CYC_ERR_DUPLICATE_KEY;
+      c->blk_msg[b] = pb.blk_dup_msg[b];
+    }
+  }
+  c->err = saved;
+  return (int)CYC_OK;
+}
+
 // allow_capture = false: never capture a graph for this run (cyc_table_run's planes are new on
 // every call, so a captured graph would be re-instantiated each time): graphs = 1 runs as 2.
 // src: rows [lo, hi) are a source shard (CYC_ROWS_SOURCE), else target rows.
@@ -4021,6 +4307,8 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
   }
   c->ran = true;
   HIPCHK(hipEventRecord(c->run_done, st));
+
+  if (!pb.blocks.empty()) return blocks_status(c, st);
 
   // 8. panic path: the first panicking job in job order, as the reference would hit it.  Configs
   // run in order (one RunProbeForConfig each); within one, the job expansion (may panic on a pod
@@ -4256,7 +4544,7 @@ int cyc_resources_load_json(cyc_ctx* c, const char* js, size_t len) {
   });
 }
 
-int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* shape) {
+static int probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* shape, const std::vector<ProbeBlock>* blocks) {
   if (!c || !js) return CYC_ERR_ARG;
   if (!c->have_policy || !c->have_res) return fail(c, CYC_ERR_ARG, "load a policy and resources first");
   return guarded(c, [&] {
@@ -4267,7 +4555,8 @@ int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* s
       HIPCHK(hipEventCreateWithFlags(&c->run_done, hipEventDisableTiming));
     }
     auto probes = load_probes(json::parse(js, len));
-    c->pb = build_problem(c->policy, c->res, probes);
+    c->prepared = false;
+    c->pb = build_problem(c->policy, c->res, probes, blocks);
     drop_graph(c);
     build_identities(c);
     prepare_device(c);
@@ -4292,6 +4581,53 @@ int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* s
     }
     return (int)CYC_OK;
   });
+}
+
+int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* shape) {
+  return probe_prepare(c, js, len, shape, nullptr);
+}
+
+int cyc_probe_prepare_blocks(cyc_ctx* c, const char* js, size_t len, const int64_t* block_end, const int32_t* block_config,
+                             int64_t n_blocks, cyc_probe_shape* shape) {
+  if (!c || !js || n_blocks < 1 || !block_end || !block_config) return CYC_ERR_ARG;
+  std::vector<ProbeBlock> bl(static_cast<size_t>(n_blocks));
+  int64_t at = 0;
+  for (int64_t b = 0; b < n_blocks; b++) {
+    if (block_end[b] < at || block_end[b] > int64_t(UINT32_MAX) || block_config[b] < 0)
+      return fail(c, CYC_ERR_ARG, "blocks must be consecutive pod ranges with a probe config each");
+    bl[size_t(b)] = ProbeBlock{uint32_t(at), uint32_t(block_end[b]), uint32_t(block_config[b])};
+    at = block_end[b];
+  }
+  return probe_prepare(c, js, len, shape, &bl);
+}
+
+int cyc_blocks_layout(cyc_ctx* c, int64_t* out, int64_t n) {
+  if (!c || !out) return CYC_ERR_ARG;
+  if (!c->prepared || c->pb.blocks.empty()) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare_blocks first");
+  const size_t nb = c->pb.blocks.size();
+  if (n < int64_t(nb + 1) * 2) return fail(c, CYC_ERR_ARG, "layout buffer needs 2 * (blocks + 1) entries");
+  for (size_t i = 0; i < 2 * (nb + 1); i++) out[i] = int64_t(c->blk_off_h[i]);
+  return (int)CYC_OK;
+}
+
+int cyc_probe_run_blocks(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int32_t* block_status) {
+  if (!c) return CYC_ERR_ARG;
+  if (!c->prepared || c->pb.blocks.empty()) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare_blocks first");
+  const uint64_t words = c->blk_off_h[2 * c->pb.blocks.size()];
+  if ((words && (!d_in || !d_eg)) || !d_status) return fail(c, CYC_ERR_ARG, "null output slab");
+  return guarded(c, [&]() -> int {
+    DeviceGuard dg(c->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int rc = run_pipeline(c, st, d_in, d_eg, d_status, 0, c->pb.P, false, false);
+    if (rc == CYC_OK && block_status)
+      for (size_t b = 0; b < c->blk_rc.size(); b++) block_status[b] = c->blk_rc[b];
+    return rc;
+  });
+}
+
+const char* cyc_block_error(const cyc_ctx* c, int64_t b) {
+  if (!c || b < 0 || size_t(b) >= c->blk_msg.size()) return "";
+  return c->blk_msg[size_t(b)].c_str();
 }
 
 int cyc_probe_run_rows(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int part, int64_t lo,

@@ -1070,13 +1070,15 @@ static void finish_tables(Problem& pb) {
 // In the first category where either happens, (A) at source 0 precedes (B) at a later source.  The
 // reference's message continues with the Job as %+v and the stack pkg/errors prints; the job is
 // named here by FromKey, ToKey and ToContainer (the oracle's text, oracle/oracle.cpp).
-static std::string table_build_error(const Resources& res, const Problem& pb, const ProbeConfig& pc, size_t c, uint32_t koff) {
-  const uint32_t P = pb.P;
-  if (!P) return "";
+// Pods [q0, q1) are the problem's pods (a batched block's, or all).
+static std::string table_build_error(const Resources& res, const Problem& pb, const ProbeConfig& pc, size_t c, uint32_t koff,
+                                     uint32_t q0, uint32_t q1) {
+  const uint32_t P = q1;
+  if (q1 <= q0) return "";
   std::unordered_map<std::string, uint32_t> first_of;  // name group: first pod with the ns/name
   std::vector<uint32_t> grp(P);
   uint32_t s_b = P;  // the first pod that is not the first of its name group
-  for (uint32_t p = 0; p < P; p++) {
+  for (uint32_t p = q0; p < P; p++) {
     grp[p] = first_of.emplace(pb.pod_key[p], p).first->second;
     if (grp[p] != p && s_b == P) s_b = p;
   }
@@ -1085,7 +1087,7 @@ static std::string table_build_error(const Resources& res, const Problem& pb, co
     std::string key;
   };
   std::vector<DJob> jobs[3];
-  for (uint32_t d = 0; d < P; d++) {
+  for (uint32_t d = q0; d < P; d++) {
     const Pod& pod = res.pods[d];
     const size_t base = size_t(d) * pb.K + koff;
     if (pc.all_available) {
@@ -1116,18 +1118,39 @@ static std::string table_build_error(const Resources& res, const Problem& pb, co
     }
     if (hit) {
       const std::string to_cont = pc.all_available ? res.pods[hit->d].conts[hit->i].name : "";
-      return "unable to add job result: duplicate key " + hit->key + " (job {FromKey:" + pb.pod_key[0] + " ToKey:" +
+      return "unable to add job result: duplicate key " + hit->key + " (job {FromKey:" + pb.pod_key[q0] + " ToKey:" +
              pb.pod_key[hit->d] + " ToContainer:" + to_cont + "})";
     }
   }
   return "";
 }
 
-Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vector<ProbeConfig>& probes) {
+Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vector<ProbeConfig>& probes,
+                      const std::vector<ProbeBlock>* blocks) {
   Problem pb;
   Flattener F(pb, ir);
   pb.P = uint32_t(res.pods.size());
   pb.W = (pb.P + 63) / 64;
+  if (blocks) {  // batched blocks: consecutive pod ranges covering the pods, namespaces private to a block
+    pb.blocks = *blocks;
+    pb.pod_blk.assign(pb.P, 0);
+    uint32_t at = 0;
+    std::unordered_map<std::string, uint32_t> ns_blk;
+    for (uint32_t b = 0; b < blocks->size(); b++) {
+      const ProbeBlock& bl = (*blocks)[b];
+      if (bl.p0 != at || bl.p1 < bl.p0 || bl.p1 > pb.P || bl.cfg >= probes.size())
+        throw Panic{CYC_ERR_ARG, "blocks must be consecutive pod ranges covering the pods, each with a probe config"};
+      for (uint32_t q = bl.p0; q < bl.p1; q++) {
+        pb.pod_blk[q] = b;
+        // a namespace's targets apply to all its pods (TargetsApplyingToPod policy.go:68-82): a block's
+        // problem is its own only if no other block has pods in its namespaces
+        auto it = ns_blk.emplace(res.pods[q].ns, b).first;
+        if (it->second != b) throw Panic{CYC_ERR_ARG, "namespace " + res.pods[q].ns + " has pods in two blocks"};
+      }
+      at = bl.p1;
+    }
+    if (at != pb.P) throw Panic{CYC_ERR_ARG, "blocks must cover every pod"};
+  }
 
   // ---- pods
   bool any_bad_ip = false;
@@ -1177,10 +1200,17 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
     for (auto& p : res.pods) (p.conts.empty() ? bare : any_cont) = true;
     for (size_t c = 0; c < probes.size(); c++)  // PortProtocol: every (from, to) pair builds a job;
       pb.expand_panic[c] = bare && (probes[c].all_available ? any_cont : true);  // AllAvailable: one per dst container
+    pb.blk_expand_panic.assign(pb.blocks.size(), 0);
+    for (size_t b = 0; b < pb.blocks.size(); b++) {  // the same, per block over its own pods
+      bool bb = false, bc = false;
+      for (uint32_t q = pb.blocks[b].p0; q < pb.blocks[b].p1; q++) (res.pods[q].conts.empty() ? bb : bc) = true;
+      pb.blk_expand_panic[b] = bb && (probes[pb.blocks[b].cfg].all_available ? bc : true);
+    }
   }
   for (size_t c = 0; c < probes.size(); c++) {
     const ProbeConfig& pc = probes[c];
     for (uint32_t d = 0; d < pb.P; d++) {
+      if (!pb.blocks.empty() && pb.blocks[pb.pod_blk[d]].cfg != c) continue;  // a block answers its config only
       const Pod& pod = res.pods[d];
       size_t base = size_t(d) * pb.K + cfg_off[c];
       if (pc.all_available) {  // GetJobsAllAvailableServers :336-364
@@ -1220,7 +1250,12 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
         }
       }
     }
-    pb.dup_key_msg[c] = table_build_error(res, pb, pc, c, cfg_off[c]);
+    if (pb.blocks.empty()) pb.dup_key_msg[c] = table_build_error(res, pb, pc, c, cfg_off[c], 0, pb.P);
+  }
+  pb.blk_dup_msg.assign(pb.blocks.size(), "");
+  for (size_t b = 0; b < pb.blocks.size(); b++) {
+    const ProbeBlock& bl = pb.blocks[b];
+    pb.blk_dup_msg[b] = table_build_error(res, pb, probes[bl.cfg], bl.cfg, cfg_off[bl.cfg], bl.p0, bl.p1);
   }
 
   finish_tables(pb);

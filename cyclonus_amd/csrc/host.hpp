@@ -139,6 +139,12 @@ struct ProbeConfig {  // generator.ProbeConfig (AllAvailable | PortProtocol)
 Resources load_resources(const json::Node& n);
 std::vector<ProbeConfig> load_probes(const json::Node& n);
 
+// A batched problem's block (cyc_probe_prepare_blocks): pods [p0, p1) of the Resources form an
+// independent probe problem answering probe config `cfg` only, over its own pods only.
+struct ProbeBlock {
+  uint32_t p0 = 0, p1 = 0, cfg = 0;
+};
+
 // ----------------------------------------------------------------------------- device tables
 // Everything engine.hip uploads, flattened and interned.
 struct Problem {
@@ -184,9 +190,16 @@ struct Problem {
   // per config: the job expansion itself panics (a pod without containers is some job's podFrom:
   // FromContainer = podFrom.Containers[0].Name, resources.go:296,349 -> index out of range)
   std::vector<uint8_t> expand_panic;
+  // batched blocks (empty: one problem over all pods); per block its own expansion panic and
+  // duplicate-key fatal, computed over its pods and config only
+  std::vector<ProbeBlock> blocks;
+  std::vector<uint32_t> pod_blk;  // [P] block of each pod
+  std::vector<uint8_t> blk_expand_panic;
+  std::vector<std::string> blk_dup_msg;
 };
 
-Problem build_problem(const PolicyIR& pol, const Resources& res, const std::vector<ProbeConfig>& probes);
+Problem build_problem(const PolicyIR& pol, const Resources& res, const std::vector<ProbeConfig>& probes,
+                      const std::vector<ProbeBlock>* blocks = nullptr);
 
 // matcher.Traffic (traffic.go:11-18) for the single-cell query API.
 struct QueryEnd {

@@ -129,6 +129,30 @@ class Engine:
                                                    ctypes.byref(t)))
         return DeviceTable(t)
 
+    # ---------------------------------------------------------------- batched blocks
+    def prepare_blocks(self, probes, block_end, block_config) -> dict:
+        """Batched independent problems (cyc_probe_prepare_blocks): block b = pods
+        [block_end[b-1], block_end[b]) answering probes[block_config[b]] over its own pods."""
+        b = _bytes(probes)
+        ends = np.ascontiguousarray(block_end, np.int64)
+        cfgs = np.ascontiguousarray(block_config, np.int32)
+        sh = _lib.ProbeShape()
+        check(self._ctx, lib().cyc_probe_prepare_blocks(self._ctx, b, len(b), ends.ctypes.data, cfgs.ctypes.data, len(ends),
+                                                        ctypes.byref(sh)))
+        self.shape = sh.as_dict()
+        self.n_blocks = len(ends)
+        lay = np.zeros(2 * (self.n_blocks + 1), np.int64)
+        check(self._ctx, lib().cyc_blocks_layout(self._ctx, lay.ctypes.data, len(lay)))
+        self.block_layout = lay.reshape(-1, 2)  # per block (plane slab offset in words, status offset); then totals
+        return self.shape
+
+    def run_blocks_device(self, d_ingress: int, d_egress: int, d_status: int, stream: int = 0):
+        """Every block's slab on the device (cyc_probe_run_blocks) -> per block (cyc_status, message)."""
+        rc = np.zeros(self.n_blocks, np.int32)
+        check(self._ctx, lib().cyc_probe_run_blocks(self._ctx, ctypes.c_void_p(stream or None), ctypes.c_void_p(d_ingress),
+                                                    ctypes.c_void_p(d_egress), ctypes.c_void_p(d_status), rc.ctypes.data))
+        return [(int(c), lib().cyc_block_error(self._ctx, b).decode(errors="replace") if c else "") for b, c in enumerate(rc)]
+
     def query_traffic(self, traffics):
         """Policy.IsTrafficAllowed on the GPU for a list of matcher.Traffic dicts -> [(ingress, egress)]."""
         b = _bytes(list(traffics))

@@ -183,6 +183,30 @@ int cyc_table_shape(const cyc_table* t, int64_t* out, int n);
 const char* cyc_table_error(const cyc_table* t);
 void cyc_table_destroy(cyc_table* t);
 
+/* ---- Batched independent problems ("blocks", SURVEY §8f row 3: the generate sweep's many small
+ * probe problems, interpreter.go:137-148, in one pass).  Resources.Pods is cut into consecutive pod
+ * ranges: block b = pods [block_end[b-1], block_end[b]) answering probe config block_config[b] (an
+ * index into probes_json) over its OWN pods only — its table is the one Runner.RunProbeForConfig
+ * would build for that problem alone.  The caller gives every block its own namespaces (a block's
+ * policies live in them; cyclonus_amd/batch.py prefixes "<b>~"), which the library checks: a
+ * namespace with pods in two blocks is refused.  Only intra-block cells are computed and written:
+ * each class row covers its block's 64-pod words only, and block b's output is a slab of
+ *   ingress[d][k][j], egress[s][k][j]   (pods of the block, slots of its config, j < ceil(n_b/64)),
+ *   status[d][k]
+ * with bit i of word j = the block's pod 64*j + i; slab offsets from cyc_blocks_layout. */
+int cyc_probe_prepare_blocks(cyc_ctx* ctx, const char* probes_json, size_t len, const int64_t* block_end,
+                             const int32_t* block_config, int64_t n_blocks, cyc_probe_shape* shape);
+/* out[2*b], out[2*b+1] = block b's plane slab offset (64-bit words) and status offset (bytes);
+ * out[2*n_blocks], out[2*n_blocks+1] = the totals (n >= 2 * (n_blocks + 1)). */
+int cyc_blocks_layout(cyc_ctx* ctx, int64_t* out, int64_t n);
+/* Run every block (device slabs, synchronous only when an input can panic).  block_status[b] (host,
+ * optional) = the cyc_status block b's stand-alone run would end with: CYC_OK, or the reference's
+ * panic / table-build fatal for THAT problem (its first panicking job in its own job order), with
+ * the message in cyc_block_error(ctx, b).  Other blocks are unaffected by one block's panic. */
+int cyc_probe_run_blocks(cyc_ctx* ctx, void* hip_stream, uint64_t* d_ingress, uint64_t* d_egress, uint8_t* d_status,
+                         int32_t* block_status);
+const char* cyc_block_error(const cyc_ctx* ctx, int64_t block);
+
 /* Average device time (ms) of the last run's kernels, measured with HIP events on the launch
  * stream: [0] whole pipeline, [1] the emit launch (the HBM-roofline kernel; one launch writes both
  * planes), [2] class rows of both directions.  Eager runs ("graphs" = 0) always record them; graph

@@ -19,7 +19,8 @@ if sys.argv[1] == "show":
                       "on d.kernel_id = s.id order by d.start").fetchall()
     # replays end with the emit (and the graph's trailing copy, if any): the last replay = the kernels
     # after the second-to-last emit ended
-    ends = [i for i, r in enumerate(rows) if "k_emit" in r[0]]
+    # a step's last emit launch (source shards emit each plane with its own launch)
+    ends = [i for i, r in enumerate(rows) if "k_emit" in r[0] and (i + 1 == len(rows) or "k_emit" not in rows[i + 1][0])]
     spans = []
     for a, b in zip(ends, ends[1:]):
         seg = rows[a + 1:b + 1]
@@ -52,15 +53,18 @@ d_eg = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
 d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 lo, hi = 0, P
+part = "source"
 for opt in sys.argv[4:]:
     k, v = opt.split("=")
-    if k == "shards":  # rank 0's rows of an N-way shard (cyclonus_amd.shard.row_range)
-        from cyclonus_amd.shard import row_range
+    if k == "part":  # source (default) or target shards
+        part = v
+    elif k == "shards":  # rank 0's rows of an N-way shard (cyclonus_amd.shard.shard_range)
+        from cyclonus_amd.shard import shard_range
 
-        lo, hi = row_range(P, int(v), 0)
+        lo, hi = shard_range(P, int(v), 0, part)
     else:
         eng.set_option(k, int(v))
 for _ in range(n):
-    eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), st, lo, hi)
+    eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), st, lo, hi, part)
 torch.cuda.synchronize()
 print(json.dumps({"config": name, "timings_last": eng.timings()}))

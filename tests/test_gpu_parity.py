@@ -194,26 +194,58 @@ def test_partial_ranges_match_full_on_synthetic(gpu):
             assert np.array_equal(ing[lo:hi], ing2) and np.array_equal(eg[lo:hi], eg2), (world, rank)
 
 
-def test_config5_generate_sweep_batched(gpu):
-    """All 242 probe steps of `cyclonus generate --mock --exclude ''` in one batched GPU pass,
-    each block bit-exact vs the oracle run on that step alone."""
+def _check_batch(problems, reps=1, ctx="batch"):
+    """Batch.run of the problems (each repeated `reps` times) equals each problem's own oracle run:
+    its table, or its panic / table-build fatal with the same message."""
     from cyclonus_amd.batch import Batch
+
+    blocks = [p for p in problems for _ in range(reps)]
+    bt = Batch(blocks)
+    got = bt.run(Engine(0))
+    want = []
+    for p in problems:
+        try:
+            want.append(Oracle(p["policies"], p["resources"]).probe([p["probe"]]))
+        except OraclePanic as e:
+            want.append(Panicked(str(e)))
+    for b, g in enumerate(got):
+        w = want[b // reps]
+        g = Panicked(g.msg) if isinstance(g, CyclonusPanic) else g
+        assert_same(w, g, f"{ctx} block {b} ({blocks[b].get('description', '')})")
+    return bt
+
+
+def test_config5_generate_sweep_batched(gpu):
+    """All 242 probe steps of `cyclonus generate --mock --exclude ''` in one batched GPU pass (a block
+    per step: only its own cells computed), each block bit-exact vs the oracle run on that step alone."""
     from cyclonus_amd.generator import sweep
 
     steps = sweep()
     assert len(steps) == 242
-    bt = Batch(steps)
-    eng = Engine(0).build_policies(json.dumps(bt.policies)).load_resources(json.dumps(bt.resources))
-    eng.prepare(bt.probes)
-    st, ing, eg = eng.run_host()
-    assert bt.cells(st) > 100_000
-    for b, step in enumerate(steps):
-        want = Oracle(step["policies"], step["resources"]).probe([step["probe"]])
-        got = bt.extract(b, st, ing, eg)
-        if step["probe"].get("AllAvailable"):
-            k = want[0].shape[1]
-            got = (got[0][:, :k], got[1][:, :k], got[2][:, :k])
-        assert_same(want, got, f"step {b} ({step['description']})")
+    _check_batch(steps, ctx="sweep")
+
+
+def test_config5_sweep_replicated(gpu):
+    """The sweep replicated 10x: 2,420 blocks in one pass, every block bit-exact vs its step's oracle
+    table; the slabs hold exactly the answered cells (2 bits per cell, 64-pod words per block row)."""
+    from cyclonus_amd.generator import sweep
+
+    steps = sweep()
+    bt = _check_batch(steps, reps=10, ctx="sweep x10")
+    assert len(bt.problems) == 2420
+    words = int(bt.layout[-1][0])
+    assert words == sum(n * k * w for n, k, w in (bt.slab_dims(b) for b in range(2420)))
+
+
+def test_batch_random_blocks(gpu):
+    """Random problems (panicking ones, duplicate job keys, every matcher feature) batched: each block
+    reports exactly its stand-alone outcome, whatever its neighbours do."""
+    probs = []
+    for seed in range(300_000, 300_160):
+        pols, res, probes = random_problem(seed, bad=seed % 3 == 0, dups=seed % 5 == 0)
+        for pr in probes:
+            probs.append({"policies": pols, "resources": res, "probe": pr})
+    _check_batch(probs, ctx="random blocks")
 
 
 def test_graph_and_eager_paths_agree(gpu):
@@ -583,8 +615,8 @@ def test_launch_modes_and_knobs(gpu):
 
 def test_batch_cross_block_panic_isolated(gpu):
     """Block B holds a pod with an unparsable IP and no IPBlock rule; block A has an IPBlock peer.
-    Neither panics alone, the combined problem does (cross-block cells): Batch.run must still give
-    each block its own stand-alone table; a block that panics alone reports its own panic."""
+    Neither panics alone (cross-block cells are never computed); a block that panics alone (C)
+    reports its own panic, and its neighbours their own tables."""
     from cyclonus_amd.batch import Batch
 
     def pod(ns, name, ip):
@@ -603,14 +635,14 @@ def test_batch_cross_block_panic_isolated(gpu):
     c = {"policies": a["policies"], "resources": {"Namespaces": {"x": {}}, "Pods": [pod("x", "e", "bad"), pod("x", "f", "10.0.0.9")]},
          "probe": {"AllAvailable": True}}
     eng = Engine(0)
-    got = Batch([a, b, c]).run(eng)
-    for blk, g in zip((a, b, c), got):
+    got = Batch([a, b, c, a]).run(eng)
+    for blk, g in zip((a, b, c, a), got):
         try:
             want = Oracle(blk["policies"], blk["resources"]).probe([blk["probe"]])
         except OraclePanic as e:
             want = Panicked(str(e))
         assert_same(want, Panicked(g.msg) if isinstance(g, CyclonusPanic) else g, blk["resources"]["Pods"][0]["Name"])
-    assert isinstance(got[2], CyclonusPanic) and not isinstance(got[0], CyclonusPanic)
+    assert isinstance(got[2], CyclonusPanic) and not isinstance(got[0], CyclonusPanic) and not isinstance(got[3], CyclonusPanic)
 
 
 def _long_class_problem(seed, n_peers=300, n_pods=260):
