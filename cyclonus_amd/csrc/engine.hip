@@ -342,7 +342,7 @@ __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uin
                                                          const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
                                                          uint64_t* __restrict__ ER, uint32_t bid_, uint32_t nblk_, uint32_t w0,
                                                          uint32_t nw) {
-  const uint32_t lane = threadIdx.x & 63, gw = bid_ * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63, gw = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6));  // wave-uniform
   const uint32_t p = gw / nw, w = w0 + (gw - p * nw);
   if (p >= Rp) return;
   const uint32_t j = pod_peers[p];
@@ -649,6 +649,10 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
 // none stores no PM word at all, any other chunk stores all 64.  Readers issue the PM and cnz loads
 // together and drop the PM word of an all-zero chunk, so the zero chunks — most of a row — cost
 // no HBM writes.
+#ifndef CYC_IP_MIXB
+#define CYC_IP_MIXB 2  // straddling words of an IP row whose pod addresses are loaded at once
+#endif
+constexpr uint32_t IP_MIXB = CYC_IP_MIXB;
 __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
                                             const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
                                             uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng,
@@ -683,15 +687,46 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
   uint32_t lo = nz ? w0 + __ffsll((unsigned long long)nz) - 1 : 0xFFFFFFFFu;
   uint32_t hi = nz ? w0 + 63 - __clzll((long long)nz) : 0u;
   uint64_t mixed = __ballot(valid && !uniform);
+  // words whose pods straddle the network (or an except) are tested a pod per lane, IP_MIXB words at
+  // once: only the network family's address words are loaded (a pod of the other family never
+  // matches, ippeermatcher / net.Contains), all of the batch's loads in flight together
+  const bool v4net = t.cidr.fam == 4;
   while (mixed) {
-    const uint32_t wl = __ffsll((unsigned long long)mixed) - 1;
-    mixed &= mixed - 1;
-    const uint32_t ww = chunk * 64 + wl;
-    const uint32_t q = ww * 64 + lane;
-    uint32_t o = 0;
-    if (q < P) {
-      const DIP ip = pod_ip[q];
-      if (cidr_contains(t.cidr, ip)) {
+    uint32_t wl[IP_MIXB], fam[IP_MIXB], a[IP_MIXB][4];
+#pragma unroll
+    for (uint32_t u = 0; u < IP_MIXB; u++) {
+      wl[u] = 64;
+      if (mixed) {
+        wl[u] = __ffsll((unsigned long long)mixed) - 1;
+        mixed &= mixed - 1;
+      }
+      const uint32_t q = (chunk * 64 + wl[u]) * 64 + lane;
+      fam[u] = 0;
+      a[u][0] = a[u][1] = a[u][2] = a[u][3] = 0;
+      if (wl[u] < 64 && q < P) {
+        const DIP* ip = pod_ip + q;
+        fam[u] = ip->fam;
+        if (v4net) a[u][3] = ip->w[3];
+        else {
+          a[u][0] = ip->w[0];
+          a[u][1] = ip->w[1];
+          a[u][2] = ip->w[2];
+          a[u][3] = ip->w[3];
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < IP_MIXB; u++) {
+      if (wl[u] >= 64) break;  // wave-uniform
+      DIP ip{};
+      ip.valid = 1;
+      ip.fam = fam[u];
+      ip.w[0] = a[u][0];
+      ip.w[1] = a[u][1];
+      ip.w[2] = a[u][2];
+      ip.w[3] = a[u][3];
+      uint32_t o = 0;
+      if (fam[u] && cidr_contains(t.cidr, ip)) {
         o = 1;
         for (uint32_t e = 0; e < t.excnt; e++)
           if (cidr_contains(ex[e], ip)) {
@@ -699,13 +734,14 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
             break;
           }
       }
-    }
-    const uint64_t m = __ballot(o == 1);
-    if (lane == 0) PM[uint64_t(t.peer) * W + ww] = m;
-    if (m) {
-      nz |= 1ull << wl;
-      lo = min(lo, ww);
-      hi = max(hi, ww);
+      const uint32_t ww = chunk * 64 + wl[u];
+      const uint64_t m = __ballot(o == 1);
+      if (lane == 0) PM[uint64_t(t.peer) * W + ww] = m;
+      if (m) {
+        nz |= 1ull << wl[u];
+        lo = min(lo, ww);
+        hi = max(hi, ww);
+      }
     }
   }
   if (lane == 0) {
@@ -826,7 +862,7 @@ __device__ __forceinline__ void slot_words_blk(uint32_t P, uint32_t K, uint32_t 
                                                     const uint8_t* __restrict__ slot_status, uint64_t* __restrict__ VALID,
                                                     int32_t* __restrict__ DESCW, uint64_t* __restrict__ DM, uint32_t bid_, uint32_t nblk_) {
   uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t idx = bid_ * 4 + wave;  // (k, w)
+  uint32_t idx = __builtin_amdgcn_readfirstlane(bid_ * 4 + wave);  // (k, w), wave-uniform
   if (idx >= K * W) return;
   uint32_t k = idx / W, w = idx % W;
   uint32_t q = w * 64 + lane;
@@ -983,7 +1019,7 @@ __global__ void k_member(MemberArgs a) { member_blk(a, blockIdx.x, gridDim.x); }
 // (ascending target id = primary-key order), same hash, same representative election.
 __device__ __forceinline__ void member_wave_blk(MemberArgs a, uint32_t bid_, uint32_t nblk_) {
   if (bid_ == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
-  const uint32_t lane = threadIdx.x & 63, ii = bid_ * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63, ii = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6));  // wave-uniform
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
   const uint32_t ns = a.id_ns[i], ls = a.id_ls[i];
@@ -1158,6 +1194,9 @@ constexpr uint32_t IDO_LDS_BYTES = 48 * 1024;  // staged identity sets per class
 #define CYC_PB_GROUP 16  // pod peers per identity-set wave (8: +4 % launch B, profiles/r02_pb_group_ab.txt)
 #endif
 constexpr uint32_t PB_GROUP = CYC_PB_GROUP;
+#ifndef CYC_PB_HALF
+#define CYC_PB_HALF 4  // pod peers whose selector loads are in flight together (8: k_front_b 61 -> 81 VGPRs)
+#endif
 // Identity words [ew0, ew0 + new) of the rows only (a source shard's ingress peers: the words of the
 // egress identities its sources have).
 __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
@@ -1165,7 +1204,8 @@ __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t 
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                    const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t bid_, uint32_t nblk_,
                                                    uint32_t ew0, uint32_t new_) {
-  const uint32_t wv = bid_ * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  // the wave index is wave-uniform: a scalar, so the peers' records below are scalar loads
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const uint32_t groups = (Rp + PB_GROUP - 1) / PB_GROUP;
   if (wv >= groups * new_) return;
   const uint32_t g = wv / new_, ew = ew0 + wv % new_;
@@ -1173,17 +1213,65 @@ __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t 
   const bool live = e < E;
   const uint32_t ns = live ? id_ns[e] : 0u, nsls = live ? id_nsls[e] : 0u, ls = live ? id_ls[e] : 0u;
   uint64_t mine = 0;
+  // PB_HALF peers at a time, in phases — their records, then every selector outcome, then the ballots —
+  // so the loads of all of them are in flight together instead of one dependent chain per peer
+  // (podpeermatcher.go:21-28 namespace then pod matcher; no panic on this path, so both matchers
+  // can be evaluated for every peer and combined)
+  constexpr uint32_t PB_HALF = PB_GROUP < CYC_PB_HALF ? PB_GROUP : CYC_PB_HALF;
 #pragma unroll
-  for (uint32_t x = 0; x < PB_GROUP; x++) {
-    const uint32_t p = g * PB_GROUP + x;
-    if (p >= Rp) break;
-    const DPeer pr = peers[pod_peers[p]];
-    bool m = live;  // podpeermatcher.go:21-28 (no panic on this path: outcomes are 0 / 1)
-    if (m && pr.nskind == 0) m = ns == pr.nsval;
-    else if (m && pr.nskind == 2) m = sel_at(sv, pr.nsval, nsls) == 1;
-    if (m && pr.podsel != CYC_ALL) m = sel_at(sv, pr.podsel, ls) == 1;
-    const uint64_t b = __ballot(m);
-    if (lane == x) mine = b;
+  for (uint32_t h = 0; h < PB_GROUP; h += PB_HALF) {
+    uint32_t nk[PB_HALF], nv[PB_HALF], ps[PB_HALF];
+    bool ok[PB_HALF];
+#pragma unroll
+    for (uint32_t x = 0; x < PB_HALF; x++) {
+      const uint32_t p = g * PB_GROUP + h + x;
+      ok[x] = p < Rp;
+      const DPeer pr = peers[pod_peers[ok[x] ? p : g * PB_GROUP]];
+      nk[x] = pr.nskind;
+      nv[x] = pr.nsval;
+      ps[x] = pr.podsel;
+    }
+    uint32_t rn[PB_HALF], rp[PB_HALF];
+    if (sv.selres) {  // dense selector table: one byte gather per matcher, all issued unconditionally
+      uint8_t an[PB_HALF], ap[PB_HALF];
+#pragma unroll
+      for (uint32_t x = 0; x < PB_HALF; x++) an[x] = sv.selres[uint64_t(nk[x] == 2 ? nv[x] : 0u) * sv.L + nsls];
+#pragma unroll
+      for (uint32_t x = 0; x < PB_HALF; x++) ap[x] = sv.selres[uint64_t(ps[x] != CYC_ALL ? ps[x] : 0u) * sv.L + ls];
+#pragma unroll
+      for (uint32_t x = 0; x < PB_HALF; x++) {
+        rn[x] = nk[x] == 2 ? an[x] : 1u;
+        rp[x] = ps[x] != CYC_ALL ? ap[x] : 1u;
+      }
+    } else {  // selectors evaluated here: one-requirement records (scalar), then every LVT gather at once
+      uint4 on[PB_HALF], op[PB_HALF];
+#pragma unroll
+      for (uint32_t x = 0; x < PB_HALF; x++) {
+        on[x] = sv.one[nk[x] == 2 ? nv[x] : 0u];
+        op[x] = sv.one[ps[x] != CYC_ALL ? ps[x] : 0u];
+      }
+      uint32_t xn[PB_HALF], xp[PB_HALF];
+#pragma unroll
+      for (uint32_t x = 0; x < PB_HALF; x++) {
+        xn[x] = sv.LVT[uint64_t(on[x].x < SEL_ALL ? on[x].y : 0u) * sv.L + nsls];
+        xp[x] = sv.LVT[uint64_t(op[x].x < SEL_ALL ? op[x].y : 0u) * sv.L + ls];
+      }
+#pragma unroll
+      for (uint32_t x = 0; x < PB_HALF; x++) {
+        rn[x] = 1u;
+        if (nk[x] == 2 && on[x].x == SEL_WALK) rn[x] = sel_eval(sv, sv.LVT, sv.L, nv[x], nsls);
+        else if (nk[x] == 2 && on[x].x != SEL_ALL) rn[x] = req_holds(on[x].x & 0xFFu, xn[x], on[x].z, on[x].w, on[x].x >> 8);
+        rp[x] = 1u;
+        if (ps[x] != CYC_ALL && op[x].x == SEL_WALK) rp[x] = sel_eval(sv, sv.LVT, sv.L, ps[x], ls);
+        else if (ps[x] != CYC_ALL && op[x].x != SEL_ALL) rp[x] = req_holds(op[x].x & 0xFFu, xp[x], op[x].z, op[x].w, op[x].x >> 8);
+      }
+    }
+#pragma unroll
+    for (uint32_t x = 0; x < PB_HALF; x++) {
+      const bool m = live && ok[x] && (nk[x] != 0 || ns == nv[x]) && rn[x] == 1 && rp[x] == 1;
+      const uint64_t b = __ballot(m);
+      if (lane == h + x) mine = b;
+    }
   }
   const uint32_t p = g * PB_GROUP + lane;
   if (lane < PB_GROUP && p < Rp) idob[uint64_t(p) * EW + ew] = mine;
@@ -1214,7 +1302,7 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
   __shared__ uint32_t s_j[4][CI_LDS];
   ht_clear_slice(a, bid_, nblk_);
   // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
-  const uint32_t wi = threadIdx.x >> 6, wv = bid_ * 4 + wi, lane = threadIdx.x & 63;
+  const uint32_t wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wv = bid_ * 4 + wi, lane = threadIdx.x & 63;
   const uint32_t nbc = (a.NB + G - 1) / G;
   const uint32_t r = wv / nbc, nb0 = (wv % nbc) * G;
   if (r >= *a.rep_cnt + 1u) return;
