@@ -1126,6 +1126,7 @@ struct RowArgs {
   const uint64_t* VALID;     // egress only [K][W]
   const int32_t* DESCW;      // egress only [K][W]
   const uint64_t* DM;        // egress only [K][D][W]
+  const int32_t* udesc;      // egress: per slot the descriptor every destination has VALID (all alike), else null
   uint64_t* A;               // [n_ident][K][W], or the output plane when arow is set
   const uint32_t* arow;      // in-place class rows: identity -> its first pod's row of the output plane
   uint64_t* AE;              // [n_ident][K][W] (ERR builds only)
@@ -1297,6 +1298,10 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
 // walk dominates this launch on row shards, where few classes leave the chip mostly idle).
 // Classes with more than CI_LDS peers walk the targets directly.
 constexpr uint32_t CI_LDS = 128, CI_BATCH = 4;
+#ifndef CYC_CI_G
+#define CYC_CI_G 4  // identity sets: job slots (ingress) / descriptors (egress) per wave
+#endif
+constexpr int CI_G = CYC_CI_G;
 template <bool EGRESS, int G>
 __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   __shared__ uint32_t s_j[4][CI_LDS];
@@ -1760,7 +1765,7 @@ __device__ __forceinline__ PlLane pl_lane(const RowArgs& a, const uint4* src, ui
   return l;
 }
 
-template <bool EGRESS>
+template <bool EGRESS, bool UNI = false>
 __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared& sh, const uint4* spill, uint32_t i,
                                                uint32_t m, bool allow_all, uint64_t lastmask, uint32_t w0, uint32_t wa) {
   static_assert(PL_LDS % 64 == 0, "a lane group of entries is all in LDS or all spilled");
@@ -1779,7 +1784,10 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
       valid[k] = 0;
       du[k] = -2;
       if (k < a.K) {
-        if (EGRESS) {
+        if (EGRESS && UNI) {  // one descriptor per slot for every destination (RowArgs::udesc)
+          valid[k] = w == a.W - 1 ? lastmask : ~0ull;
+          du[k] = a.udesc[k];
+        } else if (EGRESS) {
           valid[k] = a.VALID[uint64_t(k) * a.W + wl];
           du[k] = a.DESCW[uint64_t(k) * a.W + wl];
         } else if (a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) {
@@ -1836,6 +1844,104 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
         r &= valid[k];
       }
       a.A[(arow_of(a, i) * a.K + k) * a.WA + (w - w0)] = r;
+    }
+  }
+}
+
+// The same with two chunks per step of a wave (c and c + nwaves): the batches take the entries of
+// both chunks, so one memory round trip serves two chunks (CYC_PL_PAIR).
+#ifndef CYC_PL_PAIR
+#define CYC_PL_PAIR 0
+#endif
+template <bool EGRESS>
+__device__ __forceinline__ void pl_wave_chunk_pairs(const RowArgs& a, const PlShared& sh, const uint4* spill, uint32_t i,
+                                                    uint32_t m, bool allow_all, uint64_t lastmask, uint32_t w0, uint32_t wa) {
+  const uint32_t lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+  const uint32_t cend = (w0 + wa + 63) / 64;
+  const PlLane g0 = pl_lane(a, sh.e, lane, m);
+  for (uint32_t c = w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cend; c += 2 * nwaves) {
+    const uint32_t cc[2] = {c, c + nwaves};
+    uint32_t wv[2], wl[2];
+    bool live[2];
+    uint64_t valid[2][PL_NB], acc[2][PL_NB];
+    int32_t du[2][PL_NB];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      wv[h] = cc[h] * 64 + lane;
+      live[h] = cc[h] < cend && wv[h] >= w0 && wv[h] < w0 + wa;
+      wl[h] = live[h] ? wv[h] : w0;
+#pragma unroll
+      for (uint32_t k = 0; k < PL_NB; k++) {
+        valid[h][k] = 0;
+        du[h][k] = -2;
+        if (k < a.K) {
+          if (EGRESS) {
+            valid[h][k] = a.VALID[uint64_t(k) * a.W + wl[h]];
+            du[h][k] = a.DESCW[uint64_t(k) * a.W + wl[h]];
+          } else if (a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) {
+            valid[h][k] = wv[h] == a.W - 1 ? lastmask : ~0ull;
+          }
+        }
+        acc[h][k] = allow_all ? ~0ull : 0ull;
+      }
+    }
+    const bool second = cc[1] < cend;
+    for (uint32_t x0 = 0; x0 < (allow_all ? 0u : m); x0 += 64) {
+      PlLane g = g0;
+      if (x0 >= PL_LDS) g = pl_lane(a, spill, x0 + lane, m);
+      else if (x0) g = pl_lane(a, sh.e, x0 + lane, m);
+      uint64_t todo0 = __ballot((g.cm >> cc[0]) & 1ull);
+      uint64_t todo1 = second ? __ballot((g.cm >> cc[1]) & 1ull) : 0ull;
+      while (todo0 | todo1) {
+        uint32_t bits[PL_WBATCH], hh[PL_WBATCH];
+        uint64_t v[PL_WBATCH];
+#pragma unroll
+        for (uint32_t u = 0; u < PL_WBATCH; u++) {
+          bits[u] = 0;
+          v[u] = 0;
+          hh[u] = 0;
+          if (todo0 | todo1) {
+            const uint32_t h = todo0 ? 0u : 1u;  // wave-uniform
+            uint64_t& t = h ? todo1 : todo0;
+            const uint32_t src = __ffsll((unsigned long long)t) - 1;
+            t &= t - 1;
+            const uint32_t row = __builtin_amdgcn_readlane(g.row, src);
+            bits[u] = __builtin_amdgcn_readlane(g.bits, src);
+            hh[u] = h;
+            v[u] = row == PL_ONES ? ~0ull : a.PM[uint64_t(row) * a.W + (h ? wl[1] : wl[0])];
+          }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PL_WBATCH; u++)
+#pragma unroll
+          for (uint32_t d = 0; d < PL_NB; d++)
+            if ((bits[u] >> d) & 1u) {
+              if (hh[u]) acc[1][d] |= v[u];
+              else acc[0][d] |= v[u];
+            }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (!live[h]) continue;
+#pragma unroll
+      for (uint32_t k = 0; k < PL_NB; k++) {
+        if (k >= a.K) break;
+        uint64_t r = 0;
+        if (!EGRESS) r = acc[h][k] & valid[h][k];
+        else if (du[h][k] >= 0) {
+#pragma unroll
+          for (uint32_t d = 0; d < PL_NB; d++) r = uint32_t(du[h][k]) == d ? acc[h][d] : r;
+          r &= valid[h][k];
+        } else if (du[h][k] == -1) {  // destinations with mixed job descriptors (rare)
+          const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + wv[h];
+#pragma unroll
+          for (uint32_t d = 0; d < PL_NB; d++)
+            if (d < a.D) r |= acc[h][d] & dm[uint64_t(d) * a.W];
+          r &= valid[h][k];
+        }
+        a.A[(arow_of(a, i) * a.K + k) * a.WA + (wv[h] - w0)] = r;
+      }
     }
   }
 }
@@ -1936,7 +2042,11 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     // the class's (slot chunk, word) items, PL_ITEMS per thread at once (their loads overlap)
     uint32_t w0, wa;
     rep_window(a, i, w0, wa);
-    if (WAVE) {
+    if (WAVE && CYC_PL_PAIR) {
+      pl_wave_chunk_pairs<EGRESS>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
+    } else if (WAVE && EGRESS && a.udesc) {
+      pl_wave_chunks<EGRESS, true>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
+    } else if (WAVE) {
       pl_wave_chunks<EGRESS>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
     } else {
       const uint32_t items = nkc * wa;
@@ -1966,7 +2076,10 @@ __device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const Word
   return m;
 }
 
-template <bool EGRESS, int KC>
+// UNI (egress): every destination has the same VALID job descriptor in each slot (a.udesc[k]), so the
+// slot's descriptor is a scalar and its valid mask every pod: no per-word VALID / DESCW loads, and
+// only the block's KC descriptors' identity sets are staged (config #3 / #4: identical containers).
+template <bool EGRESS, int KC, bool UNI = false>
 __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   extern __shared__ uint64_t sB[];
   // block = (a.rpb consecutive class representatives, KC job slots, 256 pod words): the word's
@@ -1976,7 +2089,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   const uint32_t r0 = (bid_ / (chunks * nkc)) * a.rpb, n_reps = *a.rep_cnt + 1u;
   if (r0 >= n_reps) return;  // whole block
   const uint32_t nr = min(a.rpb, n_reps - r0), k0 = kc * KC;
-  const uint32_t nrow = EGRESS ? a.NB : min(uint32_t(KC), a.K - k0), rowsz = nrow * a.EW;
+  const uint32_t nrow = EGRESS && !UNI ? a.NB : min(uint32_t(KC), a.K - k0), rowsz = nrow * a.EW;
   // the word's own loads (runs, slot words) are issued before the staging barrier, so their
   // latency overlaps the staging loads instead of following them
   const uint32_t w = a.w0 + (bid_ % chunks) * 256 + threadIdx.x;
@@ -1992,12 +2105,22 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     const uint32_t k = k0 + kk;
     valid[kk] = 0;
     du[kk] = -2;
-    if (EGRESS && k < a.K && live) {
+    if (EGRESS && UNI && k < a.K) {
+      valid[kk] = live ? wmask : 0ull;
+      du[kk] = a.udesc[k];
+    } else if (EGRESS && k < a.K && live) {
       valid[kk] = a.VALID[uint64_t(k) * a.W + w];
       du[kk] = a.DESCW[uint64_t(k) * a.W + w];
     }
   }
   for (uint32_t q = 0; q < nr; q++) {
+    if (EGRESS && UNI) {  // the sets of the block's slots' descriptors, one row each
+      for (uint32_t x = threadIdx.x; x < rowsz; x += blockDim.x) {
+        const uint32_t kk = x / a.EW;
+        sB[q * rowsz + x] = a.B[(uint64_t(a.reps[r0 + q]) * a.NB + uint32_t(a.udesc[k0 + kk])) * a.EW + (x - kk * a.EW)];
+      }
+      continue;
+    }
     const uint64_t* src = a.B + (uint64_t(a.reps[r0 + q]) * a.NB + (EGRESS ? 0u : k0)) * a.EW;
     for (uint32_t x = threadIdx.x; x < rowsz; x += blockDim.x) sB[q * rowsz + x] = src[x];
   }
@@ -2018,8 +2141,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
           du[kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
         }
         if (du[kk] >= 0) {
-          allow[kk] = expand_runs(sb + uint64_t(EGRESS ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wr);
-        } else if (EGRESS && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
+          allow[kk] = expand_runs(sb + uint64_t(EGRESS && !UNI ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wr);
+        } else if (EGRESS && !UNI && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
           const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
           for (uint32_t d = 0; d < a.D; d++) allow[kk] |= expand_runs(sb + uint64_t(d) * a.EW, wr) & dm[uint64_t(d) * a.W];
         }
@@ -2055,7 +2178,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
           // egress: the descriptor varies per destination word, so the byte table would cost a
           // vector load per (slot, peer); the bit row is a shift
           if (EGRESS && a.portbits && du[kk] >= 0) allow[kk] |= ((pbits[u] >> du[kk]) & 1u) ? pm[u] : 0ull;
-          else allow[kk] |= pm[u] & port_mask<EGRESS>(a, a.portok + uint64_t(port[u]) * a.D, du[kk], k0 + kk, w);
+          else if (!UNI) allow[kk] |= pm[u] & port_mask<EGRESS>(a, a.portok + uint64_t(port[u]) * a.D, du[kk], k0 + kk, w);
+          else if (du[kk] >= 0 && a.portok[uint64_t(port[u]) * a.D + du[kk]]) allow[kk] |= pm[u];
         }
         undecided |= valid[kk] & ~allow[kk];
       }
@@ -2068,8 +2192,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     }
   }
 }
-template <bool EGRESS, int KC>
-__global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) { class_rows_ido_blk<EGRESS, KC>(a, blockIdx.x, gridDim.x); }
+template <bool EGRESS, int KC, bool UNI = false>
+__global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) { class_rows_ido_blk<EGRESS, KC, UNI>(a, blockIdx.x, gridDim.x); }
 
 // Fused front (cyc_set_option "front_fused", IDO builds): the front's ~15 kernels of two graph
 // branches become 5 launches on ONE stream, each launch a concatenation of independent block
@@ -2267,8 +2391,8 @@ struct FrontRows {
 };
 __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[0]) class_ident_blk<false, 4>(f.ra[0], b, f.nb[0]);
-  else class_ident_blk<true, 4>(f.ra[1], b - f.nb[0], f.nb[1]);
+  if (b < f.nb[0]) class_ident_blk<false, CI_G>(f.ra[0], b, f.nb[0]);
+  else class_ident_blk<true, CI_G>(f.ra[1], b - f.nb[0], f.nb[1]);
 }
 // PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
 template <bool WAVE>
@@ -2288,6 +2412,9 @@ __global__ __launch_bounds__(256) CYC_PL_WAVES void k_front_d_pm(FrontRows f) {
 #define CYC_E_KC 4  // job slots per thread in the fused IDO class rows (k_front_e)
 #endif
 constexpr int E_KC = CYC_E_KC;
+#ifndef CYC_UNI_DESC  // egress class rows with one descriptor per slot when every pod shares it
+#define CYC_UNI_DESC 1
+#endif
 #ifndef CYC_E_SPLIT
 #define CYC_E_SPLIT 1  // 1: launch E as one kernel per direction (k_class_rows_ido, each at its own register
                        // budget: egress 101 VGPRs, ingress 61) instead of k_front_e (both at 101): config #3
@@ -2857,6 +2984,8 @@ struct cyc_ctx {
   DevBuf pod_peers_u;  // identity-set (IDOB) rows: the needed pod peers, one per distinct
                        // (namespace matcher, pod selector) of a direction (peer_ido maps every peer)
   DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
+  DevBuf udesc;     // per slot the one VALID descriptor every pod has, when all slots are so (uni_desc)
+  bool uni_desc = false;
   DevBuf plvt;      // LVT per pod (SelView::PLVT), built by ensure_plvt when it fits PLVT_MAX_BYTES
   uint32_t n_lkeys = 0;     // dense label keys (LVT rows - 1)
   bool plvt_ready = false;
@@ -3282,6 +3411,17 @@ static void prepare_device(cyc_ctx* c) {
     }
     c->ido.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * c->ids[1].ns.size(), 16));
     c->idob.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * ((c->ids[1].ns.size() + 63) / 64) * 8, 16));
+  }
+  {  // one VALID descriptor per slot across all pods? (egress class rows then skip the per-word slot words)
+    std::vector<int32_t> ud(std::max<uint32_t>(pb.K, 1), -1);
+    bool uni = pb.P > 0 && pb.K > 0;
+    for (uint32_t k = 0; k < pb.K && uni; k++) {
+      ud[k] = pb.slot_desc[k];
+      for (uint32_t q = 0; q < pb.P && uni; q++)
+        uni = pb.slot_status[size_t(q) * pb.K + k] == CYC_JOB_VALID && pb.slot_desc[size_t(q) * pb.K + k] == ud[k];
+    }
+    c->uni_desc = CYC_UNI_DESC && uni;
+    upload(c->udesc, ud);
   }
   c->portok.alloc(std::max<uint64_t>(pb.pms.size() * D, 16));
   c->portbits.alloc(std::max<uint64_t>(pb.pms.size() * 4, 16));
@@ -3839,9 +3979,9 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     else k_class_rows<true><<<g, 256, 0, st>>>(ra);
   } else if (ido_mode(c)) {
     // identity sets first (one wave per representative and 4 slots / descriptors), then the rows
-    const uint64_t waves = uint64_t(c->n_act[d]) * ((ra.NB + 3) / 4);
-    if (d == 0) k_class_ident<false, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
-    else k_class_ident<true, 4><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
+    const uint64_t waves = uint64_t(c->n_act[d]) * ((ra.NB + CI_G - 1) / CI_G);
+    if (d == 0) k_class_ident<false, CI_G><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
+    else k_class_ident<true, CI_G><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
     ra.ht_clear_words = 0;
     const uint32_t rows = d == 0 ? std::min<uint32_t>(4, K) : D;
     const size_t per = size_t(rows) * ra.EW * 8;
@@ -4123,7 +4263,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     }
   }
   FrontRows fd{}, fe{};
-  size_t lds = 0;
+  size_t lds = 0, lds_uni = 0;
   for (int d = 0; d < 2; d++) {
     const uint32_t na = c->dir[d].n ? c->n_act[d] : 0u;
     fb.ma[d] = member_args(c, d);
@@ -4140,16 +4280,20 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     }
     if (!ido) {  // PM builds: launch D (k_front_d_pm) is the class rows from flattened peer lists
       fd.nb[d] = pl_blocks(c, d);
+      if (d == 1 && c->uni_desc && c->pb.blocks.empty()) fd.ra[d].udesc = c->udesc.as<int32_t>();
       fd.ra[d].pod_sparse = pod_sparse(c);  // pod rows from pod_rows_sparse_blk (launch C)
       continue;
     }
     fe.ra[d] = fd.ra[d];
     fe.ra[d].ht_clear_words = 0;
-    fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + 3) / 4) + 3) / 4);
-    const size_t per = size_t(d == 0 ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8;
+    fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + CI_G - 1) / CI_G) + 3) / 4);
+    // egress with one descriptor per slot (udesc): only the block's slots' sets are staged
+    if (d == 1 && CYC_E_SPLIT && c->uni_desc) fe.ra[d].udesc = c->udesc.as<int32_t>();
+    const size_t per = size_t(d == 0 || fe.ra[d].udesc ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8;
     fe.ra[d].rpb = class_rpb(c, per);
     fe.nb[d] = blocks(uint64_t((fe.ra[d].WA + 255) / 256) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
-    lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
+    if (d == 1 && fe.ra[d].udesc) lds_uni = per * fe.ra[d].rpb;
+    else lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
   const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
   const bool bits = fa.nb[1] && port_bits_on(c);
@@ -4175,7 +4319,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
   if (CYC_E_SPLIT) {  // the directions' class rows as two launches, each at its own register budget
-    if (fe.nb[1]) k_class_rows_ido<true, E_KC><<<fe.nb[1], 256, lds, st>>>(fe.ra[1]);
+    if (fe.nb[1] && fe.ra[1].udesc) k_class_rows_ido<true, E_KC, true><<<fe.nb[1], 256, lds_uni, st>>>(fe.ra[1]);
+    else if (fe.nb[1]) k_class_rows_ido<true, E_KC><<<fe.nb[1], 256, lds, st>>>(fe.ra[1]);
     if (fe.nb[0]) k_class_rows_ido<false, E_KC><<<fe.nb[0], 256, lds, st>>>(fe.ra[0]);
   } else if (fe.nb[0] + fe.nb[1]) {
     k_front_e<<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);

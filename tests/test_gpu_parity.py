@@ -843,3 +843,27 @@ def test_duplicate_job_keys(gpu, block):
         elif not isinstance(o, Panicked):
             n_ok += 1
     assert n_dup >= 40 and n_ok >= 10, (n_dup, n_ok)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_uniform_descriptors_ido(gpu, seed):
+    """Every pod with the same containers (one VALID job descriptor per slot across the table, as in
+    configs #3 / #4): the egress class rows take the descriptor as a scalar and skip the per-word slot
+    words; equal to the oracle on IDO builds (deployment-style words) and PM builds, fused and DAG
+    fronts."""
+    pols, res, probes = _deployment_problem(seed)
+    conts = [{"Name": "c0", "Port": 80, "Protocol": "TCP", "PortName": "serve-80-tcp"},
+             {"Name": "c1", "Port": 53, "Protocol": "UDP", "PortName": "serve-53-udp"},
+             {"Name": "c2", "Port": 81, "Protocol": "SCTP", "PortName": "serve-81-sctp"}]
+    res = dict(res, Pods=[dict(p, Containers=conts) for p in res["Pods"]])
+    probes = [{"AllAvailable": True}, {"Port": 80, "Protocol": "TCP"}, {"Port": "serve-53-udp", "Protocol": "UDP"}]
+    if seed % 2 == 0:
+        probes = probes[:1]  # 3 slots: the PM build's wave-per-chunk class rows apply
+    want = Oracle(pols, res).probe(probes)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    eng.prepare(probes)
+    for pod_words, fused in ((1, 1), (1, 0), (0, 1), (0, 0)):  # IDO and PM builds (wave-per-chunk rows)
+        eng.set_option("pod_words", pod_words)
+        eng.set_option("front_fused", fused)
+        assert eng.get_option("pod_words") == pod_words
+        assert_same(want, eng.run_host(), f"seed {seed} pod_words {pod_words} fused {fused}")
