@@ -8,9 +8,10 @@ already resident in HBM: selector evaluation, peer rows, port tables, target mem
 class election, class rows, and the emit of both packed verdict planes (ingress keyed by
 destination, egress keyed by source) for this rank's rows.  N > 1 shards the pods across ranks
 (one process per GPU, torch.distributed over RCCL for the barrier / max-time reduce only; there is
-no collective on the data path): --partition source (north_star: rank r owns source pods, i.e.
-every cell Table.Get(from = s, *) of its sources) or target (rank r owns the target rows of both
-planes).  Rank 0 prints one JSON line.
+no collective on the data path): --partition target (the default, the faster of the two on one-GPU
+shard timings, DESIGN.md §6: rank r owns the target rows of both planes) or source (north_star:
+rank r owns source pods, i.e. every cell Table.Get(from = s, *) of its sources).  Rank 0 prints one
+JSON line.
 """
 from __future__ import annotations
 
@@ -103,7 +104,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-assemble", action="store_true", help="skip the N>1 all-gather timing")
-    ap.add_argument("--partition", default="source", choices=["source", "target"],
+    ap.add_argument("--partition", default="target", choices=["source", "target"],
                     help="row partition across ranks (include/cyclonus_hip.h cyc_rows; the same at N=1)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="cyc_set_option tuning knob (diagnostics; results never change)")

@@ -791,14 +791,19 @@ __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32
   // the chunk's own [min, max] per family (records W.. of `words`): a peer whose network misses
   // the whole chunk leaves all 64 words zero — the wave only clears the chunk's cnz mask
   const DWordIP ck = words[W + __builtin_amdgcn_readfirstlane(chunk)];
-  for (uint32_t r = 0; r < nr; r++) {
-    const DIPTest t = s_t[r];
-    const bool v4 = t.cidr.fam == 4;
-    if (t.cidr.valid && (v4 ? !ck.m4 || span_vs_cidr4(ck.min4, ck.max4, t.cidr) == 0
-                            : !ck.m6 || span_vs_cidr6(ck.min6, ck.max6, t.cidr) == 0)) {
-      if (lane == 0) cnz[uint64_t(t.peer) * ((W + 63) / 64) + chunk] = 0;
-      continue;
-    }
+  // the chunk test of the group's peers a lane each (lane x: peer r0 + x; grp <= 64): a peer whose
+  // network misses the chunk's addresses only gets its chunk mask cleared, here, by its lane — the
+  // wave then walks only the peers that touch the chunk (config #4: ~1 in 5)
+  bool touch = false;
+  if (lane < nr) {
+    const DIPTest& tx = s_t[lane];
+    const bool v4 = tx.cidr.fam == 4;
+    touch = !(tx.cidr.valid && (v4 ? !ck.m4 || span_vs_cidr4(ck.min4, ck.max4, tx.cidr) == 0
+                                   : !ck.m6 || span_vs_cidr6(ck.min6, ck.max6, tx.cidr) == 0));
+    if (!touch) cnz[uint64_t(tx.peer) * ((W + 63) / 64) + chunk] = 0;
+  }
+  for (uint64_t todo = __ballot(touch); todo; todo &= todo - 1) {
+    const DIPTest t = s_t[__builtin_amdgcn_readfirstlane(__ffsll((unsigned long long)todo) - 1)];
     ip_row_word(t, ex_lds ? s_ex + (t.exoff - ex0) : ip_ex + t.exoff, pod_ip, wd, valid, w, chunk, P, W, lane, PM, rng, cnz);
   }
 }
@@ -1773,6 +1778,11 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
   // the chunks holding the window's words (<= 64 chunks in all: pl_wave_ok)
   const uint32_t cend = (w0 + wa + 63) / 64;
   const PlLane g0 = pl_lane(a, sh.e, lane, m);  // entries 0..63, one per lane, for every chunk
+  uint32_t vslots = 0;  // ingress: the representative's VALID slots (loaded once, not per chunk)
+  if (!EGRESS)
+#pragma unroll
+    for (uint32_t k = 0; k < PL_NB; k++)
+      if (k < a.K && a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) vslots |= 1u << k;
   for (uint32_t c = w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cend; c += nwaves) {
     const uint32_t w = c * 64 + lane;
     const bool live = w >= w0 && w < w0 + wa;
@@ -1790,7 +1800,7 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
         } else if (EGRESS) {
           valid[k] = a.VALID[uint64_t(k) * a.W + wl];
           du[k] = a.DESCW[uint64_t(k) * a.W + wl];
-        } else if (a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) {
+        } else if ((vslots >> k) & 1u) {
           valid[k] = w == a.W - 1 ? lastmask : ~0ull;
         }
       }
@@ -1961,16 +1971,21 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     uint32_t m = 0;
     for (uint32_t t0 = 0; t0 < nt; t0 += PL_TGT) {  // targets in chunks: offsets, counts, prefix sums
       const uint32_t ntc = min(PL_TGT, nt - t0);
-      for (uint32_t t = threadIdx.x; t < ntc; t += blockDim.x) {
-        const DTarget tg = a.tgt[lst[t0 + t]];
-        sh.poff[t] = tg.poff;
-        sh.pre[t + 1] = tg.pcnt;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        sh.pre[0] = 0;
-        for (uint32_t t = 0; t < ntc; t++) sh.pre[t + 1] = acc += sh.pre[t + 1];
+      static_assert(PL_TGT == 64, "one wave scans a target chunk");
+      if (threadIdx.x < 64) {  // wave 0: the chunk's targets a lane each, peer counts prefix-summed in registers
+        uint32_t v = 0;
+        if (threadIdx.x < ntc) {
+          const DTarget tg = a.tgt[lst[t0 + threadIdx.x]];
+          sh.poff[threadIdx.x] = tg.poff;
+          v = tg.pcnt;
+        }
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_up(v, o);
+          if (threadIdx.x >= o) v += u;
+        }
+        if (threadIdx.x < ntc) sh.pre[threadIdx.x + 1] = v;
+        if (threadIdx.x == 0) sh.pre[0] = 0;
       }
       __syncthreads();
       const uint32_t mc = sh.pre[ntc];
@@ -2076,6 +2091,14 @@ __device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const Word
   return m;
 }
 
+constexpr uint32_t IDO_RPB_MAX = 64;  // class_rpb's upper bound
+constexpr uint32_t IDO_IPL = 16;      // IP peers per representative staged in LDS (row, span, port bits)
+template <int KC>
+struct RepHead {  // a class-row block's representative: identity, class-row index, IP-peer list, slot descriptors
+  uint32_t i, arow, m, ipoff;
+  int32_t du[KC];
+};
+
 // UNI (egress): every destination has the same VALID job descriptor in each slot (a.udesc[k]), so the
 // slot's descriptor is a scalar and its valid mask every pod: no per-word VALID / DESCW loads, and
 // only the block's KC descriptors' identity sets are staged (config #3 / #4: identical containers).
@@ -2113,6 +2136,24 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
       du[kk] = a.DESCW[uint64_t(k) * a.W + w];
     }
   }
+  // each representative's scalars (identity, class-row index, IP-peer list, ingress slot
+  // descriptors) are loaded once per block, before the barrier: the row loop below then reads them
+  // from LDS instead of walking reps -> identity -> list chains per representative after it
+  __shared__ RepHead<KC> s_rep[IDO_RPB_MAX];
+  if (threadIdx.x < nr) {
+    RepHead<KC> h;
+    h.i = a.reps[r0 + threadIdx.x];
+    h.arow = uint32_t(arow_of(a, h.i));
+    h.m = a.cnt[h.i] ? a.ip_cnt[h.i] : 0u;
+    h.ipoff = a.ip_off[h.i];
+#pragma unroll
+    for (int kk = 0; kk < KC; kk++) {
+      const uint32_t k = k0 + kk;
+      h.du[kk] = -2;
+      if (!EGRESS && k < a.K && a.id_status[uint64_t(h.i) * a.K + k] == CYC_JOB_VALID) h.du[kk] = a.id_desc[uint64_t(h.i) * a.K + k];
+    }
+    s_rep[threadIdx.x] = h;
+  }
   for (uint32_t q = 0; q < nr; q++) {
     if (EGRESS && UNI) {  // the sets of the block's slots' descriptors, one row each
       for (uint32_t x = threadIdx.x; x < rowsz; x += blockDim.x) {
@@ -2125,9 +2166,30 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     for (uint32_t x = threadIdx.x; x < rowsz; x += blockDim.x) sB[q * rowsz + x] = src[x];
   }
   __syncthreads();
+  // the first IDO_IPL IP peers of each representative, staged after the heads: (PM row, first
+  // word, last word, port bits — egress: the descriptor bit row; ingress: a bit per block slot), so
+  // the row loop issues only the PM loads (no list -> port table chain per batch)
+  uint4* s_il = reinterpret_cast<uint4*>(sB + ((nr * rowsz + 1) & ~1u));  // 16-byte aligned
+  const bool stage_ip = !EGRESS || a.portbits != nullptr;
+  if (stage_ip) {
+    for (uint32_t t = threadIdx.x; t < nr * IDO_IPL; t += blockDim.x) {
+      const RepHead<KC>& h = s_rep[t / IDO_IPL];
+      const uint32_t x = t % IDO_IPL;
+      if (x >= h.m) continue;
+      const uint4 jp = a.ip_list[h.ipoff + x];
+      uint32_t bits = 0;
+      if (EGRESS) bits = a.portbits[jp.y];
+      else
+#pragma unroll
+        for (int kk = 0; kk < KC; kk++)
+          if (h.du[kk] >= 0 && a.portok[uint64_t(jp.y) * a.D + h.du[kk]]) bits |= 1u << kk;
+      s_il[t] = make_uint4(jp.x, jp.z, jp.w, bits);
+    }
+    __syncthreads();
+  }
   if (!live) return;
   for (uint32_t q = 0; q < nr; q++) {
-    const uint32_t i = a.reps[r0 + q];
+    const RepHead<KC>& h = s_rep[q];
     const uint64_t* sb = sB + q * rowsz;
     uint64_t allow[KC];
 #pragma unroll
@@ -2136,9 +2198,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
       allow[kk] = 0;
       if (k < a.K) {
         if (!EGRESS) {  // the destination's slot: per representative (block-uniform)
-          const bool v = a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID;
-          valid[kk] = v ? wmask : 0ull;
-          du[kk] = v ? a.id_desc[uint64_t(i) * a.K + k] : -2;
+          du[kk] = h.du[kk];
+          valid[kk] = du[kk] >= 0 ? wmask : 0ull;
         }
         if (du[kk] >= 0) {
           allow[kk] = expand_runs(sb + uint64_t(EGRESS && !UNI ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wr);
@@ -2151,9 +2212,44 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     // IP peers (ippeermatcher.go:43-50): per pod word through the PM rows, PEER_BATCH peers' words
     // loaded at once (no panic in IDO builds: the OR is order-free; the undecided check only ends
     // the walk early, once per batch)
-    const uint32_t m = a.cnt[i] ? a.ip_cnt[i] : 0u;
-    const uint4* il = a.ip_list + a.ip_off[i];
-    for (uint32_t x0 = 0; x0 < m; x0 += PEER_BATCH) {
+    const uint32_t m = h.m, ms = stage_ip ? min(m, IDO_IPL) : 0u;
+    const uint4* sl = s_il + q * IDO_IPL;
+    uint64_t undecided = ms ? 0ull : ~0ull;
+    for (uint32_t x0 = 0; x0 < ms; x0 += PEER_BATCH) {
+      uint64_t pm[PEER_BATCH];
+      uint32_t pbits[PEER_BATCH];
+#pragma unroll
+      for (uint32_t u = 0; u < PEER_BATCH; u++) {
+        pm[u] = 0;
+        pbits[u] = 0;
+        if (x0 + u < ms) {
+          const uint4 e = sl[x0 + u];
+          pbits[u] = e.w;
+          if (w >= e.y && w <= e.z) pm[u] = a.PM[uint64_t(e.x) * a.W + w] & cnz_mask(a.ip_cnz, a.W, e.x, w);
+        }
+      }
+      undecided = 0;
+#pragma unroll
+      for (int kk = 0; kk < KC; kk++) {
+#pragma unroll
+        for (uint32_t u = 0; u < PEER_BATCH; u++) {
+          if (!pm[u]) continue;
+          if (!EGRESS) allow[kk] |= ((pbits[u] >> kk) & 1u) ? pm[u] : 0ull;
+          else if (du[kk] >= 0) allow[kk] |= ((pbits[u] >> du[kk]) & 1u) ? pm[u] : 0ull;
+          else if (!UNI && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
+            uint64_t okm = 0;
+            const uint64_t* dm = a.DM + uint64_t(k0 + kk) * a.D * a.W + w;
+            for (uint32_t d = 0; d < a.D; d++)
+              if ((pbits[u] >> d) & 1u) okm |= dm[uint64_t(d) * a.W];
+            allow[kk] |= pm[u] & okm;
+          }
+        }
+        undecided |= valid[kk] & ~allow[kk];
+      }
+      if (!undecided) break;
+    }
+    const uint4* il = a.ip_list + h.ipoff;
+    for (uint32_t x0 = ms; x0 < (undecided ? m : 0u); x0 += PEER_BATCH) {  // peers past the staged ones
       uint64_t pm[PEER_BATCH];
       uint32_t port[PEER_BATCH], pbits[PEER_BATCH];
 #pragma unroll
@@ -2188,7 +2284,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
       const uint32_t k = k0 + kk;
-      if (k < a.K) a.A[(arow_of(a, i) * a.K + k) * a.WA + (w - a.w0)] = allow[kk] & valid[kk];
+      if (k < a.K) a.A[(uint64_t(h.arow) * a.K + k) * a.WA + (w - a.w0)] = allow[kk] & valid[kk];
     }
   }
 }
@@ -3984,7 +4080,7 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     else k_class_ident<true, CI_G><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
     ra.ht_clear_words = 0;
     const uint32_t rows = d == 0 ? std::min<uint32_t>(4, K) : D;
-    const size_t per = size_t(rows) * ra.EW * 8;
+    const size_t per = size_t(rows) * ra.EW * 8 + IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
     ra.rpb = class_rpb(c, per);
     const unsigned gi = unsigned(uint64_t((ra.WA + 255) / 256) * ((K + 3) / 4) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
     if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
@@ -4289,7 +4385,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + CI_G - 1) / CI_G) + 3) / 4);
     // egress with one descriptor per slot (udesc): only the block's slots' sets are staged
     if (d == 1 && CYC_E_SPLIT && c->uni_desc) fe.ra[d].udesc = c->udesc.as<int32_t>();
-    const size_t per = size_t(d == 0 || fe.ra[d].udesc ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8;
+    const size_t per = size_t(d == 0 || fe.ra[d].udesc ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8 +
+                       IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
     fe.ra[d].rpb = class_rpb(c, per);
     fe.nb[d] = blocks(uint64_t((fe.ra[d].WA + 255) / 256) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
     if (d == 1 && fe.ra[d].udesc) lds_uni = per * fe.ra[d].rpb;

@@ -1,6 +1,7 @@
 """Build an A/B variant of libcyclonus_hip.so with extra -D flags (dev helper):
     python scripts/build_variant.py NAME -DCYC_PL_BATCH=16   -> cyclonus_amd/_build/var_NAME/libcyclonus_hip.so
     python scripts/build_variant.py NAME --rev HEAD           -> the engine.hip of a git revision
+    python scripts/build_variant.py NAME --src FILE           -> a patched copy of engine.hip (diagnostics)
 Run it with CYC_HIP_LIB=<that path> (cyclonus_amd/_lib.py)."""
 import os
 import subprocess
@@ -21,6 +22,9 @@ if "--rev" in defs:
     with open(src, "w") as f:
         f.write(subprocess.run(["git", "-C", ROOT, "show", f"{rev}:cyclonus_amd/csrc/engine.hip"], check=True,
                                capture_output=True, text=True).stdout)
+if "--src" in defs:
+    src = os.path.abspath(defs[defs.index("--src") + 1])
+    defs = [d for d in defs if d not in ("--src", src) and os.path.abspath(d) != src]
 common = ["-O3", "-std=c++17", "-fPIC", "-I", b.CSRC, "-I", b.INCLUDE, *defs]
 host = os.path.join(b.BUILD, "host.cpp.o")
 eng = os.path.join(out, "engine.hip.o")

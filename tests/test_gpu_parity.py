@@ -430,6 +430,54 @@ def test_pod_words_from_identity_runs(gpu, seed):
                                               f"fused {fused} member_wave {mw} rpb {rpb} run {rep}")
 
 
+def _many_ip_peers(seed):
+    """Deployment-style pods plus policies whose rules list 17-40 IPBlock peers each (more than the
+    IDO class rows stage per representative, IDO_IPL = 16), with mixed numbered / named / no ports,
+    over both directions: the staged and the global IP-peer walks both run."""
+    import random
+
+    r = random.Random(1000 + seed)
+    pols, res, probes = _deployment_problem(seed)
+    nss = sorted({p["Namespace"] for p in res["Pods"]})
+    ports = [None, [{"port": 80, "protocol": "TCP"}], [{"port": "serve-53-udp", "protocol": "UDP"}],
+             [{"port": 81, "protocol": "SCTP"}, {"port": 53, "protocol": "UDP"}]]
+    for i in range(6):
+        def peers():
+            out = []
+            for _ in range(r.randint(17, 40)):
+                plen = r.choice([16, 20, 24, 26, 28, 30, 32])
+                blk = {"cidr": f"10.1.{r.randint(0, 4)}.{r.randint(0, 249)}/{plen}"}
+                if plen <= 28 and r.random() < 0.3:
+                    blk["except"] = [f"10.1.{r.randint(0, 4)}.{r.randint(0, 249)}/32"]
+                out.append({"ipBlock": blk})
+            return out
+
+        ing, eg = {"from": peers()}, {"to": peers()}
+        pp = r.choice(ports)
+        if pp:
+            ing["ports"], eg["ports"] = pp, pp
+        pols.append({"apiVersion": "networking.k8s.io/v1", "kind": "NetworkPolicy",
+                     "metadata": {"name": f"many-ip-{i}", "namespace": r.choice(nss)},
+                     "spec": {"podSelector": {}, "policyTypes": ["Ingress", "Egress"], "ingress": [ing], "egress": [eg]}})
+    return pols, res, probes
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_ido_many_ip_peers(gpu, seed):
+    """IDO class rows with more IP peers per class than are staged in LDS: equal to the oracle for
+    one and several representatives per block, fused and DAG fronts."""
+    pols, res, probes = _many_ip_peers(seed)
+    want = Oracle(pols, res).probe(probes)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    eng.prepare(probes)
+    for fused, rpb in ((1, 4), (1, 1), (0, 3)):
+        eng.set_option("pod_words", 1)
+        eng.set_option("front_fused", fused)
+        eng.set_option("class_rpb", rpb)
+        assert eng.get_option("pod_words") == 1
+        assert_same(want, eng.run_host(), f"seed {seed} fused {fused} rpb {rpb}")
+
+
 def _wide_ports_problem(seed, n_pods=150):
     """Pods with many containers (AllAvailable: > 32 job slots per pod) over > 32 distinct job
     descriptors, so the descriptor bit rows (<= 32) and the slot-bit list entries (<= 32) do not
