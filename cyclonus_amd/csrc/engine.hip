@@ -1597,6 +1597,24 @@ constexpr uint32_t PL_LDS = 256, PL_TGT = 64, PL_BATCH = CYC_PL_BATCH, PL_THREAD
 constexpr uint32_t PL_SKIP = 0xFFFFFFFEu, PL_ONES = 0xFFFFFFFFu;  // entry rows: zero row / PortsForAllPeers
 constexpr uint32_t PL_IP = 0x80000000u;
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+// The neighbouring lane's (lane ^ 1) 8-byte value, by DPP quad permutation [1, 0, 3, 2].
+__device__ __forceinline__ uint64_t lane_pair_swap(uint64_t v) {
+  const uint32_t lo = uint32_t(__builtin_amdgcn_mov_dpp(int(uint32_t(v)), 0xB1, 0xF, 0xF, false));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_mov_dpp(int(uint32_t(v >> 32)), 0xB1, 0xF, 0xF, false));
+  return (uint64_t(hi) << 32) | lo;
+}
+// Words off, off ^ 1 (lanes 2j, 2j + 1 hold one word each) of two class-row slot rows as 16-byte
+// stores: the even lane writes row ra's pair, the odd lane row rb's — half the store instructions
+// of 8-byte stores (the class rows are store-issue bound: config #3 / #4 class rows 30 us faster
+// with their stores removed).  Rows 16-byte aligned, off even on even lanes, both lanes live.
+__device__ __forceinline__ void store_row_pair(uint64_t* ra, uint64_t* rb, uint64_t off, uint64_t va, uint64_t vb, bool odd) {
+  const uint64_t got = lane_pair_swap(odd ? va : vb);
+  if (!odd) *reinterpret_cast<u64x2*>(ra + off) = u64x2{va, got};
+  else *reinterpret_cast<u64x2*>(rb + off - 1) = u64x2{got, vb};
+}
+
 // PM word of list entry e for pod word w (0 outside the entry's span)
 __device__ __forceinline__ uint64_t pl_word(const RowArgs& a, const uint4& e, uint32_t w) {
   if (e.x == PL_ONES) return ~0ull;
@@ -1778,6 +1796,8 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
   // the chunks holding the window's words (<= 64 chunks in all: pl_wave_ok)
   const uint32_t cend = (w0 + wa + 63) / 64;
   const PlLane g0 = pl_lane(a, sh.e, lane, m);  // entries 0..63, one per lane, for every chunk
+  uint64_t* const rows = a.A + arow_of(a, i) * a.K * a.WA;  // the class row's slot 0
+  const bool pair = a.WA % 2 == 0 && w0 % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
   uint32_t vslots = 0;  // ingress: the representative's VALID slots (loaded once, not per chunk)
   if (!EGRESS)
 #pragma unroll
@@ -1837,11 +1857,12 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
       }
     }
     if (!live) continue;
+    uint64_t rr[PL_NB];
 #pragma unroll
     for (uint32_t k = 0; k < PL_NB; k++) {
-      if (k >= a.K) break;
       uint64_t r = 0;
-      if (!EGRESS) r = acc[k] & valid[k];
+      if (k >= a.K) {
+      } else if (!EGRESS) r = acc[k] & valid[k];
       else if (du[k] >= 0) {
 #pragma unroll
         for (uint32_t d = 0; d < PL_NB; d++) r = uint32_t(du[k]) == d ? acc[d] : r;
@@ -1853,8 +1874,19 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
           if (d < a.D) r |= acc[d] & dm[uint64_t(d) * a.W];
         r &= valid[k];
       }
-      a.A[(arow_of(a, i) * a.K + k) * a.WA + (w - w0)] = r;
+      rr[k] = r;
     }
+    const uint64_t off = w - w0;
+    uint32_t k = 0;
+    if (pair)
+#pragma unroll
+      for (; k + 1 < PL_NB; k += 2) {
+        if (k + 1 >= a.K) break;
+        store_row_pair(rows + uint64_t(k) * a.WA, rows + uint64_t(k + 1) * a.WA, off, rr[k], rr[k + 1], lane & 1);
+      }
+#pragma unroll
+    for (uint32_t kk = 0; kk < PL_NB; kk++)
+      if (kk >= k && kk < a.K) rows[uint64_t(kk) * a.WA + off] = rr[kk];
   }
 }
 
@@ -2188,6 +2220,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     __syncthreads();
   }
   if (!live) return;
+  // 16-byte stores of word pairs (store_row_pair): even rows of the class rows' window, aligned base
+  const bool pair = a.WA % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
   for (uint32_t q = 0; q < nr; q++) {
     const RepHead<KC>& h = s_rep[q];
     const uint64_t* sb = sB + q * rowsz;
@@ -2281,11 +2315,19 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
       }
       if (!undecided) break;
     }
+    uint64_t* const rows = a.A + (uint64_t(h.arow) * a.K + k0) * a.WA;  // slot k0 of the class row
+    const uint64_t off = w - a.w0;
+    int kk = 0;
+    if (pair)
 #pragma unroll
-    for (int kk = 0; kk < KC; kk++) {
-      const uint32_t k = k0 + kk;
-      if (k < a.K) a.A[(uint64_t(h.arow) * a.K + k) * a.WA + (w - a.w0)] = allow[kk] & valid[kk];
-    }
+      for (; kk + 1 < KC; kk += 2) {
+        if (k0 + kk + 1 >= a.K) break;
+        store_row_pair(rows + uint64_t(kk) * a.WA, rows + uint64_t(kk + 1) * a.WA, off, allow[kk] & valid[kk],
+                       allow[kk + 1] & valid[kk + 1], threadIdx.x & 1);
+      }
+#pragma unroll
+    for (int x = 0; x < KC; x++)
+      if (x >= kk && k0 + x < a.K) rows[uint64_t(x) * a.WA + off] = allow[x] & valid[x];
   }
 }
 template <bool EGRESS, int KC, bool UNI = false>
@@ -2577,7 +2619,6 @@ __device__ __forceinline__ void emit_status(const EmitArgs& a) {
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.st_dst[i] = a.st_src[i];
 }
 
-typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 // Rows of an odd word count or planes not 16-byte aligned: 8-byte copies, one block per row.
 __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
