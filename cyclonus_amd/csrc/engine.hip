@@ -232,6 +232,53 @@ __device__ __forceinline__ uint32_t sel_at(const SelView& v, uint32_t s, uint32_
   if (d.x != SEL_WALK) return req_holds(d.x & 0xFFu, v.LVT[uint64_t(d.y) * v.L + l], d.z, d.w, d.x >> 8) ? 1u : 0u;
   return sel_eval(v, v.LVT, v.L, s, l);
 }
+// N selectors on label set l with every load of the batch in flight together: the one-requirement
+// records first, then each one's label-table load, unconditionally (a load inside a divergent branch
+// is waited for at the branch's end); only a selector of several requirements walks them.
+template <uint32_t N>
+__device__ __forceinline__ void sel_at_n(const SelView& v, const uint32_t (&s)[N], uint32_t l, uint8_t (&r)[N]) {
+  if (v.selres) {
+#pragma unroll
+    for (uint32_t x = 0; x < N; x++) r[x] = v.selres[uint64_t(s[x]) * v.L + l];
+    return;
+  }
+  uint4 d[N];
+  uint32_t xv[N];
+#pragma unroll
+  for (uint32_t x = 0; x < N; x++) d[x] = v.one[s[x]];
+#pragma unroll
+  for (uint32_t x = 0; x < N; x++) xv[x] = v.LVT[uint64_t(d[x].x < SEL_ALL ? d[x].y : 0u) * v.L + l];
+#pragma unroll
+  for (uint32_t x = 0; x < N; x++) {
+    if (d[x].x == SEL_ALL) r[x] = 1;
+    else if (d[x].x != SEL_WALK) r[x] = req_holds(d[x].x & 0xFFu, xv[x], d[x].z, d[x].w, d[x].x >> 8) ? 1 : 0;
+    else r[x] = uint8_t(sel_eval(v, v.LVT, v.L, s[x], l));
+  }
+}
+// Mixes identity i's ingress slot descriptors into its class hash (status and descriptor of every
+// slot), 8 slots' loads in flight at once.
+__device__ __forceinline__ uint64_t hash_slots(uint64_t h, const uint8_t* __restrict__ id_status, const int32_t* __restrict__ id_desc,
+                                               uint32_t i, uint32_t K) {
+  for (uint32_t k0 = 0; k0 < K; k0 += 8) {
+    uint8_t st[8];
+    int32_t ds[8];
+#pragma unroll
+    for (uint32_t x = 0; x < 8; x++) {
+      const uint64_t ik = uint64_t(i) * K + min(k0 + x, K - 1);
+      st[x] = id_status[ik];
+      ds[x] = id_desc[ik];
+    }
+#pragma unroll
+    for (uint32_t x = 0; x < 8; x++) {
+      if (k0 + x >= K) break;
+      const uint64_t sk = st[x];
+      const int32_t d = sk == CYC_JOB_VALID ? ds[x] : -1;
+      h = mix64(h ^ ((sk << 40) | uint32_t(d + 1)) ^ (uint64_t(k0 + x) << 48));
+    }
+  }
+  return h;
+}
+
 // Pod selector s on pod q's own labels through PLVT: one coalesced load per requirement for a wave
 // of consecutive pods, instead of a pod -> label set -> table gather chain.
 __device__ __forceinline__ uint32_t sel_at_pod(const SelView& v, uint32_t s, uint32_t q) { return sel_eval(v, v.PLVT, v.P, s, q); }
@@ -264,14 +311,17 @@ __device__ __forceinline__ bool cidr_contains(const DCidr& c, const DIP& ip) {
 // namespace matcher first, pod matcher only if it matched.
 __device__ __forceinline__ uint32_t pod_peer_outcome(const DPeer& pr, const uint8_t* __restrict__ selres, uint32_t L,
                                                      uint32_t ns, uint32_t nsls, uint32_t ls) {
+  // both matchers' table bytes are loaded up front (byte 0 when a matcher needs none), so neither
+  // load waits inside a branch; the outcome still follows the matchers' order
+  const bool nsel = pr.nskind == 2, psel = pr.podsel != CYC_ALL;
+  const uint8_t rn = selres[nsel ? uint64_t(pr.nsval) * L + nsls : 0u];
+  const uint8_t rp = selres[psel ? uint64_t(pr.podsel) * L + ls : 0u];
   if (pr.nskind == 0) {
     if (ns != pr.nsval) return 0;
-  } else if (pr.nskind == 2) {
-    uint8_t r = selres[uint64_t(pr.nsval) * L + nsls];
-    if (r != 1) return r == 2 ? 2u : 0u;
+  } else if (nsel && rn != 1) {
+    return rn == 2 ? 2u : 0u;
   }
-  if (pr.podsel == CYC_ALL) return 1;
-  return selres[uint64_t(pr.podsel) * L + ls];
+  return psel ? rp : 1u;
 }
 
 // IP peer outcome for one pod IP: ippeermatcher.go:43-50 -> ipaddress.go:22-40 (CIDR parse,
@@ -348,11 +398,9 @@ __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uin
   const uint32_t j = pod_peers[p];
   const DPeer pr = peers[j];
   const uint32_t q = w * 64 + lane;
-  uint32_t o = 0;
-  if (q < P) {
-    const uint32_t e = pod_eid[q];
-    o = pod_peer_outcome(pr, selres, L, id_ns[e], id_nsls[e], id_ls[e]);
-  }
+  const uint32_t e = pod_eid[min(q, P - 1)];  // (clamped: no load inside a branch)
+  uint32_t o = pod_peer_outcome(pr, selres, L, id_ns[e], id_nsls[e], id_ls[e]);
+  if (q >= P) o = 0;
   const uint64_t m = __ballot(o == 1);
   const uint64_t er = ERR ? __ballot(o == 2) : 0ull;
   if (lane == 0) {
@@ -701,19 +749,15 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
         mixed &= mixed - 1;
       }
       const uint32_t q = (chunk * 64 + wl[u]) * 64 + lane;
-      fam[u] = 0;
-      a[u][0] = a[u][1] = a[u][2] = a[u][3] = 0;
-      if (wl[u] < 64 && q < P) {
-        const DIP* ip = pod_ip + q;
-        fam[u] = ip->fam;
-        if (v4net) a[u][3] = ip->w[3];
-        else {
-          a[u][0] = ip->w[0];
-          a[u][1] = ip->w[1];
-          a[u][2] = ip->w[2];
-          a[u][3] = ip->w[3];
-        }
-      }
+      // loaded unconditionally (a clamped pod), so the batch's loads are in flight together
+      const DIP* ip = pod_ip + min(q, P - 1);
+      const bool live = wl[u] < 64 && q < P;
+      const uint32_t f = ip->fam;
+      a[u][3] = ip->w[3];
+      a[u][0] = v4net ? 0u : ip->w[0];
+      a[u][1] = v4net ? 0u : ip->w[1];
+      a[u][2] = v4net ? 0u : ip->w[2];
+      fam[u] = live ? f : 0u;
     }
 #pragma unroll
     for (uint32_t u = 0; u < IP_MIXB; u++) {
@@ -777,6 +821,14 @@ __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32
   const uint32_t r0 = (bid_ / cb) * grp;
   if (r0 >= Ri) return;  // whole block
   const uint32_t nr = min(Ri - r0, grp), chunk = c0 + (bid_ % cb) * 4 + (threadIdx.x >> 6);
+  // the wave's word records are loaded first (clamped, unconditionally): their latency overlaps the
+  // staging below instead of following its barrier
+  const uint32_t w = chunk * 64 + lane;
+  const bool valid = w < W && chunk < c0 + nch;
+  const DWordIP wd = words[min(w, W - 1)];
+  // the chunk's own [min, max] per family (records W.. of `words`): a peer whose network misses
+  // the whole chunk leaves all 64 words zero — the wave only clears the chunk's cnz mask
+  const DWordIP ck = words[W + min(uint32_t(__builtin_amdgcn_readfirstlane(chunk)), (W + 63) / 64 - 1)];
   const uint32_t ex0 = tests[r0].exoff, nex = tests[r0 + nr - 1].exoff + tests[r0 + nr - 1].excnt - ex0;
   const bool ex_lds = nex <= IP_EX_LDS;
   for (uint32_t x = threadIdx.x; x < nr; x += blockDim.x) s_t[x] = tests[r0 + x];
@@ -784,13 +836,6 @@ __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32
     for (uint32_t x = threadIdx.x; x < nex; x += blockDim.x) s_ex[x] = ip_ex[ex0 + x];
   __syncthreads();
   if (chunk >= c0 + nch) return;
-  const uint32_t w = chunk * 64 + lane;
-  const bool valid = w < W;
-  DWordIP wd{};
-  if (valid) wd = words[w];
-  // the chunk's own [min, max] per family (records W.. of `words`): a peer whose network misses
-  // the whole chunk leaves all 64 words zero — the wave only clears the chunk's cnz mask
-  const DWordIP ck = words[W + __builtin_amdgcn_readfirstlane(chunk)];
   // the chunk test of the group's peers a lane each (lane x: peer r0 + x; grp <= 64): a peer whose
   // network misses the chunk's addresses only gets its chunk mask cleared, here, by its lane — the
   // wave then walks only the peers that touch the chunk (config #4: ~1 in 5)
@@ -977,9 +1022,10 @@ __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t
     uint32_t sel[MB];
     uint8_t r[MB];
 #pragma unroll
-    for (uint32_t x = 0; x < MB; x++) sel[x] = t0 + x < hi ? a.tgt[t0 + x].sel : 0u;
+    for (uint32_t x = 0; x < MB; x++) sel[x] = a.tgt[min(t0 + x, hi - 1)].sel;
+    sel_at_n<MB>(a.sv, sel, ls, r);
 #pragma unroll
-    for (uint32_t x = 0; x < MB; x++) r[x] = t0 + x < hi ? uint8_t(sel_at(a.sv, sel[x], ls)) : 0;
+    for (uint32_t x = 0; x < MB; x++) r[x] = t0 + x < hi ? r[x] : uint8_t(0);
 #pragma unroll
     for (uint32_t x = 0; x < MB; x++) {
       const uint32_t t = t0 + x;
@@ -990,13 +1036,7 @@ __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t
       }
     }
   }
-  if (a.id_desc) {
-    for (uint32_t k = 0; k < a.K; k++) {
-      uint64_t st = a.id_status[uint64_t(i) * a.K + k];
-      int32_t d = st == CYC_JOB_VALID ? a.id_desc[uint64_t(i) * a.K + k] : -1;
-      h = mix64(h ^ ((st << 40) | uint32_t(d + 1)) ^ (uint64_t(k) << 48));
-    }
-  }
+  if (a.id_desc) h = hash_slots(h, a.id_status, a.id_desc, i, a.K);
   if (a.id_blk) h = mix64(h ^ (uint64_t(a.id_blk[i]) << 24) ^ 0xB10Cull);  // a class row covers one block's words
   h &= 0x7FFFFFFFFFFFFFFFull;  // never the empty key (~0)
   a.cnt[i] = n;
@@ -1041,13 +1081,7 @@ __device__ __forceinline__ void member_wave_blk(MemberArgs a, uint32_t bid_, uin
     for (uint64_t mm = m; mm; mm &= mm - 1) h = mix64(h ^ (uint64_t(t0 + __ffsll((unsigned long long)mm) - 1) + 1));
     n += __popcll(m);
   }
-  if (a.id_desc) {
-    for (uint32_t k = 0; k < a.K; k++) {
-      uint64_t st = a.id_status[uint64_t(i) * a.K + k];
-      int32_t d = st == CYC_JOB_VALID ? a.id_desc[uint64_t(i) * a.K + k] : -1;
-      h = mix64(h ^ ((st << 40) | uint32_t(d + 1)) ^ (uint64_t(k) << 48));
-    }
-  }
+  if (a.id_desc) h = hash_slots(h, a.id_status, a.id_desc, i, a.K);
   if (a.id_blk) h = mix64(h ^ (uint64_t(a.id_blk[i]) << 24) ^ 0xB10Cull);  // a class row covers one block's words
   h &= 0x7FFFFFFFFFFFFFFFull;  // never the empty key (~0)
   if (lane == 0) {
@@ -1139,7 +1173,9 @@ struct RowArgs {
   // pod peers are folded per class into identity-space sets B by k_class_ident, and the class
   // rows expand B through each word's runs; only IP peers are walked per pod word.
   const uint64_t* IDOB;      // [pod peers][EW] u64: pod peer matches egress identity e (bit e)
+  const uint64_t* zero;      // 256 zero bytes: the target of branch-free loads for absent items
   const uint32_t* peer_ido;  // peer id -> IDOB row
+  const uint32_t* prow;      // peer id -> its PM / ER row and IP word-span record (IP peers of one IPBlock share one)
   const struct WordRuns* runs;  // [W] each 64-pod word's identity runs (<= IDO_MAX_RUNS)
   uint64_t* B;               // [n_ident][NB][EW]; NB = K (ingress, per slot) or D (egress, per descriptor)
   const uint32_t* ip_off;    // [n_ident] host upper bound: IP peers of the identity's namespace's targets
@@ -1318,13 +1354,20 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
   if (r >= *a.rep_cnt + 1u) return;
   const uint32_t i = a.reps[r];
   int32_t du[G];
+  {  // ingress: the slots' status and descriptor, all G pairs loaded at once
+    uint8_t st[G];
+    int32_t ds[G];
 #pragma unroll
-  for (uint32_t x = 0; x < uint32_t(G); x++) {
-    const uint32_t nb = nb0 + x;
-    du[x] = -1;
-    if (nb < a.NB) {
-      if (EGRESS) du[x] = int32_t(nb);
-      else if (a.id_status[uint64_t(i) * a.K + nb] == CYC_JOB_VALID) du[x] = a.id_desc[uint64_t(i) * a.K + nb];
+    for (uint32_t x = 0; x < uint32_t(G); x++) {
+      const uint64_t ik = EGRESS ? 0u : uint64_t(i) * a.K + min(nb0 + x, a.K - 1);
+      st[x] = EGRESS ? uint8_t(0) : a.id_status[ik];
+      ds[x] = EGRESS ? 0 : a.id_desc[ik];
+    }
+#pragma unroll
+    for (uint32_t x = 0; x < uint32_t(G); x++) {
+      const uint32_t nb = nb0 + x;
+      du[x] = -1;
+      if (nb < a.NB) du[x] = EGRESS ? int32_t(nb) : (st[x] == CYC_JOB_VALID ? ds[x] : -1);
     }
   }
   const uint32_t n = a.cnt[i];
@@ -1356,31 +1399,49 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
     for (uint32_t x = 0; x < uint32_t(G); x++) b[x] = (n == 0 && du[x] >= 0) ? ~0ull : 0ull;  // no target: allowed (policy.go:158-160)
     if (flat) {
       // no panic on this path: the OR over peers is order-free (AllPeersMatcher: every valid cell)
+      // a batch's loads in three levels, each issued for every peer of the batch whatever its kind
+      // (absent peers / other kinds read a zero word): peer record + identity-set row id, then the
+      // identity-set word and the port test (descriptor bit row, or the byte table per slot)
       for (uint32_t x0 = 0; x0 < m; x0 += CI_BATCH) {
         uint32_t kind[CI_BATCH], port[CI_BATCH], pid[CI_BATCH];
 #pragma unroll
         for (uint32_t u = 0; u < CI_BATCH; u++) {
-          kind[u] = 3;
-          port[u] = 0;
-          pid[u] = 0;
-          if (x0 + u < m) {
-            const uint32_t j = __builtin_amdgcn_readfirstlane(sj[x0 + u]);
-            kind[u] = a.peers[j].kind;
-            port[u] = a.peers[j].port;
-            pid[u] = a.peer_ido[j];
-          }
+          const uint32_t j = __builtin_amdgcn_readfirstlane(sj[min(x0 + u, m - 1)]);
+          const DPeer pr = a.peers[j];
+          pid[u] = a.peer_ido[j];
+          kind[u] = x0 + u < m ? pr.kind : 3u;
+          port[u] = pr.kind == 0 ? 0u : pr.port;
         }
         uint64_t v[CI_BATCH];
+        uint32_t ok[CI_BATCH];  // bit x: the peer's port matcher passes slot / descriptor du[x]
 #pragma unroll
-        for (uint32_t u = 0; u < CI_BATCH; u++)
-          v[u] = kind[u] == 0 || kind[u] == 1 ? ~0ull : (kind[u] == 2 && ew < a.EW ? a.IDOB[uint64_t(pid[u]) * a.EW + ew] : 0ull);
+        for (uint32_t u = 0; u < CI_BATCH; u++) {
+          const uint64_t iv = *(kind[u] == 2 && ew < a.EW ? a.IDOB + uint64_t(pid[u]) * a.EW + ew : a.zero);
+          v[u] = kind[u] == 0 || kind[u] == 1 ? ~0ull : iv;
+          const bool live = kind[u] != 3;
+          if (a.portbits) {  // uniform
+            const uint32_t pb = *(live ? a.portbits + port[u] : reinterpret_cast<const uint32_t*>(a.zero));
+            ok[u] = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < uint32_t(G); x++)
+              if (du[x] >= 0 && ((pb >> du[x]) & 1u)) ok[u] |= 1u << x;
+          } else {
+            uint8_t pk[G];
+#pragma unroll
+            for (uint32_t x = 0; x < uint32_t(G); x++)
+              pk[x] = *(live ? a.portok + uint64_t(port[u]) * a.D + uint32_t(max(du[x], 0)) : reinterpret_cast<const uint8_t*>(a.zero));
+            ok[u] = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < uint32_t(G); x++)
+              if (du[x] >= 0 && pk[x]) ok[u] |= 1u << x;
+          }
+        }
 #pragma unroll
         for (uint32_t u = 0; u < CI_BATCH; u++) {
           if (kind[u] == 3) continue;  // IP peers: per pod word, in the class rows
-          const uint8_t* pok = a.portok + uint64_t(port[u]) * a.D;
 #pragma unroll
           for (uint32_t x = 0; x < uint32_t(G); x++)
-            if (du[x] >= 0 && (kind[u] == 0 || pok[du[x]])) b[x] |= v[u];
+            if (du[x] >= 0 && (kind[u] == 0 || ((ok[u] >> x) & 1u))) b[x] |= v[u];
         }
       }
     } else {
@@ -1420,12 +1481,15 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
       if (e < m) {
         j = sj[e];
         kind = a.peers[j].kind;
-        if (kind == 3) r0 = a.ip_rng[4 * j];
+        if (kind == 3) r0 = a.ip_rng[4 * a.prow[j]];
       }
       all |= __ballot(e < m && kind == 0) != 0;
       const bool keep = e < m && kind == 3 && r0 != 0xFFFFFFFFu;
       const uint64_t bm = __ballot(keep);
-      if (keep && !all) il[mm + __popcll(bm & ((1ull << lane) - 1))] = make_uint4(j, a.peers[j].port, r0, ~a.ip_rng[4 * j + 1]);
+      if (keep && !all) {
+        const uint32_t row = a.prow[j];
+        il[mm + __popcll(bm & ((1ull << lane) - 1))] = make_uint4(row, a.peers[j].port, r0, ~a.ip_rng[4 * row + 1]);
+      }
       mm += __popcll(bm);
     }
     if (lane == 0) a.ip_cnt[i] = all ? 0u : mm;
@@ -1438,7 +1502,9 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
       for (uint32_t j = tg.poff; j < tg.poff + tg.pcnt; j++) {
         const DPeer pr = a.peers[j];
         if (pr.kind == 0) break;  // AllPeers: the identity sets already allow everything
-        if (pr.kind == 3 && a.ip_rng[4 * j] != 0xFFFFFFFFu) il[mm++] = make_uint4(j, pr.port, a.ip_rng[4 * j], ~a.ip_rng[4 * j + 1]);
+        if (pr.kind != 3) continue;
+        const uint32_t row = a.prow[j];
+        if (a.ip_rng[4 * row] != 0xFFFFFFFFu) il[mm++] = make_uint4(row, pr.port, a.ip_rng[4 * row], ~a.ip_rng[4 * row + 1]);
       }
     }
     a.ip_cnt[i] = mm;
@@ -1512,10 +1578,11 @@ __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uin
           break;
         }
         uint64_t pm = ~0ull, er = 0;
-        if (!ERR && pr.kind == 3 && (w < a.ip_rng[4 * j] || w > ~a.ip_rng[4 * j + 1])) continue;  // zero word
+        const uint32_t row = pr.kind == 3 ? a.prow[j] : j;
+        if (!ERR && pr.kind == 3 && (w < a.ip_rng[4 * row] || w > ~a.ip_rng[4 * row + 1])) continue;  // zero word
         if (pr.kind >= 2) {
-          pm = a.PM[uint64_t(j) * a.W + w];
-          if (ERR) er = a.ER[uint64_t(j) * a.W + w];
+          pm = a.PM[uint64_t(row) * a.W + w];
+          if (ERR) er = a.ER[uint64_t(row) * a.W + w];
         }
         const uint8_t* pok = a.portok + uint64_t(pr.port) * a.D;
         uint64_t alldec = ~0ull;
@@ -1628,6 +1695,7 @@ struct PlShared {  // one per block, shared by both directions' instantiations o
   uint32_t bits[PL_LDS];  // port test bits
   uint32_t pre[PL_TGT + 1], poff[PL_TGT];
   uint32_t all;
+  int32_t rdu[32];  // ingress, K <= 32: the representative's job descriptor per slot (-1: slot not VALID)
 };
 
 #ifndef CYC_PL_ITEMS
@@ -1768,6 +1836,9 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
 #ifndef CYC_PL_WBATCH
 #define CYC_PL_WBATCH 8
 #endif
+#ifndef CYC_PL_PIPE
+#define CYC_PL_PIPE 1  // classes of <= 64 entries: pl_wave_chunks_pipe
+#endif
 constexpr uint32_t PL_WBATCH = CYC_PL_WBATCH, PL_NB = 4;
 // An entry's lane fields for the wave-per-chunk rows: row, port bits, mask of the 64-word chunks
 // holding a nonzero PM word of it (IP rows: from the IP-row pass; other rows: all)
@@ -1781,11 +1852,136 @@ __device__ __forceinline__ PlLane pl_lane(const RowArgs& a, const uint4* src, ui
     const uint4 e = src[x];  // (row, port bits, first word | PL_IP, last word)
     l.row = e.x;
     l.bits = e.y;
+    // the chunk mask is loaded whatever the entry (a zero word for the others): no wait in a branch
+    const bool sparse = e.x < PL_SKIP && (e.z & PL_IP);
+    const uint64_t nm = *(sparse ? reinterpret_cast<const uint64_t*>(a.ip_rng) + 2 * e.x + 1 : a.zero);
     if (e.x == PL_SKIP || !e.y) l.cm = 0;
-    else if (e.x != PL_ONES && (e.z & PL_IP)) l.cm = ~reinterpret_cast<const uint64_t*>(a.ip_rng)[2 * e.x + 1];
+    else if (sparse) l.cm = ~nm;
     else l.cm = ~0ull;
   }
   return l;
+}
+
+// Pops up to PL_WBATCH entries of `todo` (lanes of the wave's entry group g) and loads their PM words
+// of pod word wl, branch-free: all of the batch's loads are in flight together.
+__device__ __forceinline__ void pl_load_batch(const RowArgs& a, const PlLane& g, uint64_t& todo, uint32_t wl,
+                                              uint64_t (&v)[PL_WBATCH], uint32_t (&bits)[PL_WBATCH]) {
+#pragma unroll
+  for (uint32_t u = 0; u < PL_WBATCH; u++) {
+    uint32_t row = PL_SKIP;
+    bits[u] = 0;
+    if (todo) {  // wave-uniform
+      const uint32_t src = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      row = __builtin_amdgcn_readlane(g.row, src);
+      bits[u] = __builtin_amdgcn_readlane(g.bits, src);
+    }
+    const uint64_t x = *(row < PL_SKIP ? a.PM + uint64_t(row) * a.W + wl : a.zero);
+    v[u] = row == PL_ONES ? ~0ull : x;
+  }
+}
+
+// pl_wave_chunks for classes of at most 64 entries (one lane group), software-pipelined: the first
+// batch of the wave's NEXT chunk (and its slot words) is loaded before this chunk's class-row stores
+// are issued.  On gfx9 a wave's loads and stores share one in-order counter, so a batch loaded after
+// the stores would wait for them too; loaded before, the wait leaves the stores in flight and the
+// wave's store traffic overlaps its next chunk's PM loads.
+template <bool EGRESS, bool UNI = false>
+__device__ __forceinline__ void pl_wave_chunks_pipe(const RowArgs& a, const PlShared& sh, uint32_t i, uint32_t m,
+                                                    uint64_t lastmask, uint32_t w0, uint32_t wa) {
+  const uint32_t lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+  const uint32_t cend = (w0 + wa + 63) / 64;
+  uint32_t c = w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (c >= cend) return;
+  const PlLane g = pl_lane(a, sh.e, lane, m);
+  uint64_t* const rows = a.A + arow_of(a, i) * a.K * a.WA;  // the class row's slot 0
+  const bool pair = a.WA % 2 == 0 && w0 % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
+  uint32_t vslots = 0;  // ingress: the representative's VALID slots (class_rows_pl_blk staged them)
+  if (!EGRESS)
+#pragma unroll
+    for (uint32_t k = 0; k < PL_NB; k++)
+      if (k < a.K && sh.rdu[k] >= 0) vslots |= 1u << k;
+  // the slot words of chunk c (egress with per-destination descriptors: VALID / DESCW loads)
+  auto slot_words = [&](uint32_t cc, uint64_t (&valid)[PL_NB], int32_t (&du)[PL_NB]) {
+    const uint32_t w = cc * 64 + lane, wl = min(max(w, w0), w0 + wa - 1);
+#pragma unroll
+    for (uint32_t k = 0; k < PL_NB; k++) {
+      valid[k] = 0;
+      du[k] = -2;
+      if (k < a.K) {  // block-uniform
+        if (EGRESS && UNI) {
+          valid[k] = w == a.W - 1 ? lastmask : ~0ull;
+          du[k] = a.udesc[k];
+        } else if (EGRESS) {
+          valid[k] = a.VALID[uint64_t(k) * a.W + wl];
+          du[k] = a.DESCW[uint64_t(k) * a.W + wl];
+        } else if ((vslots >> k) & 1u) {
+          valid[k] = w == a.W - 1 ? lastmask : ~0ull;
+        }
+      }
+    }
+  };
+  uint64_t v[PL_WBATCH], valid[PL_NB];
+  uint32_t bits[PL_WBATCH];
+  int32_t du[PL_NB];
+  uint64_t todo = __ballot((g.cm >> c) & 1ull);
+  pl_load_batch(a, g, todo, min(max(c * 64 + lane, w0), w0 + wa - 1), v, bits);
+  slot_words(c, valid, du);
+  for (; c < cend; c += nwaves) {
+    const uint32_t w = c * 64 + lane;
+    const bool live = w >= w0 && w < w0 + wa;
+    const uint32_t wl = live ? w : min(max(w, w0), w0 + wa - 1);
+    uint64_t acc[PL_NB];
+#pragma unroll
+    for (uint32_t d = 0; d < PL_NB; d++) acc[d] = 0;
+    while (true) {  // the prefetched batch, then (entries past PL_WBATCH in this chunk) further ones
+#pragma unroll
+      for (uint32_t u = 0; u < PL_WBATCH; u++)
+#pragma unroll
+        for (uint32_t d = 0; d < PL_NB; d++)
+          if ((bits[u] >> d) & 1u) acc[d] |= v[u];
+      if (!todo) break;
+      pl_load_batch(a, g, todo, wl, v, bits);
+    }
+    uint64_t rr[PL_NB];
+#pragma unroll
+    for (uint32_t k = 0; k < PL_NB; k++) {
+      uint64_t r = 0;
+      if (k >= a.K) {
+      } else if (!EGRESS) r = acc[k] & valid[k];
+      else if (du[k] >= 0) {
+#pragma unroll
+        for (uint32_t d = 0; d < PL_NB; d++) r = uint32_t(du[k]) == d ? acc[d] : r;
+        r &= valid[k];
+      } else if (du[k] == -1) {  // destinations with mixed job descriptors (rare)
+        const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + wl;
+#pragma unroll
+        for (uint32_t d = 0; d < PL_NB; d++)
+          if (d < a.D) r |= acc[d] & dm[uint64_t(d) * a.W];
+        r &= valid[k];
+      }
+      rr[k] = r;
+    }
+    // the next chunk's first batch and slot words, before this chunk's stores
+    const uint32_t cn = c + nwaves;
+    if (cn < cend) {
+      todo = __ballot((g.cm >> cn) & 1ull);
+      pl_load_batch(a, g, todo, min(max(cn * 64 + lane, w0), w0 + wa - 1), v, bits);
+      slot_words(cn, valid, du);
+    }
+    if (!live) continue;
+    const uint64_t off = w - w0;
+    uint32_t k = 0;
+    if (pair)
+#pragma unroll
+      for (; k + 1 < PL_NB; k += 2) {
+        if (k + 1 >= a.K) break;
+        store_row_pair(rows + uint64_t(k) * a.WA, rows + uint64_t(k + 1) * a.WA, off, rr[k], rr[k + 1], lane & 1);
+      }
+#pragma unroll
+    for (uint32_t kk = 0; kk < PL_NB; kk++)
+      if (kk >= k && kk < a.K) rows[uint64_t(kk) * a.WA + off] = rr[kk];
+  }
 }
 
 template <bool EGRESS, bool UNI = false>
@@ -1798,11 +1994,11 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
   const PlLane g0 = pl_lane(a, sh.e, lane, m);  // entries 0..63, one per lane, for every chunk
   uint64_t* const rows = a.A + arow_of(a, i) * a.K * a.WA;  // the class row's slot 0
   const bool pair = a.WA % 2 == 0 && w0 % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
-  uint32_t vslots = 0;  // ingress: the representative's VALID slots (loaded once, not per chunk)
+  uint32_t vslots = 0;  // ingress: the representative's VALID slots (class_rows_pl_blk staged them)
   if (!EGRESS)
 #pragma unroll
     for (uint32_t k = 0; k < PL_NB; k++)
-      if (k < a.K && a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) vslots |= 1u << k;
+      if (k < a.K && sh.rdu[k] >= 0) vslots |= 1u << k;
   for (uint32_t c = w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cend; c += nwaves) {
     const uint32_t w = c * 64 + lane;
     const bool live = w >= w0 && w < w0 + wa;
@@ -2000,6 +2196,14 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     const uint32_t* lst = a.list + a.list_off[i];
     uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
     if (threadIdx.x == 0) sh.all = 0;
+    // ingress (K <= 32): the representative's descriptor per slot, read by the peers' slot bits below
+    // and by the chunk walk (the first barrier of the target loop, or the one after it, publishes it)
+    if (!EGRESS && threadIdx.x < min(a.K, 32u)) {
+      const uint64_t ik = uint64_t(i) * a.K + threadIdx.x;
+      const uint8_t st = a.id_status[ik];
+      const int32_t ds = a.id_desc[ik];
+      sh.rdu[threadIdx.x] = st == CYC_JOB_VALID ? ds : -1;
+    }
     uint32_t m = 0;
     for (uint32_t t0 = 0; t0 < nt; t0 += PL_TGT) {  // targets in chunks: offsets, counts, prefix sums
       const uint32_t ntc = min(PL_TGT, nt - t0);
@@ -2029,7 +2233,13 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
           else hi = mid;
         }
         const uint32_t j = sh.poff[lo] + (e - sh.pre[lo]);
+        // every lane issues the same loads in two levels (peer + its row id, then the row's word span
+        // and the port bits), whatever the peer's kind: no load waits inside a divergent branch
         const DPeer pr = a.peers[j];
+        const uint32_t prj = a.prow[j];
+        const uint32_t row = pr.kind == 3 ? prj : j;
+        const uint32_t rlo = a.ip_rng[4 * row], rhi = a.ip_rng[4 * row + 1];
+        const uint32_t pbits = a.portbits ? a.portbits[pr.kind == 0 ? 0u : pr.port] : 0u;
         uint4 en = make_uint4(PL_SKIP, 0u, 1u, 0u);
         uint32_t bits = 0;
         if (pr.kind == 0) {
@@ -2038,21 +2248,19 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
           // PortsForAllPeers, and a pod peer of every pod in every namespace (podpeermatcher.go with
           // AllNamespaceMatcher + AllPodMatcher): all-ones rows, never loaded (nor built, sparse rows)
           const bool ones = pr.kind == 1 || (pr.kind == 2 && pr.nskind == 1 && pr.podsel == CYC_ALL);
-          en = make_uint4(ones ? PL_ONES : j, pr.port, 0u, a.W - 1);
+          en = make_uint4(ones ? PL_ONES : row, pr.port, 0u, a.W - 1);
           if (!ones && (pr.kind == 3 || (pr.kind == 2 && a.pod_sparse))) {  // bit 31 of z: a sparse row (only the cnz-marked words were written)
-            en.z = a.ip_rng[4 * j] | PL_IP;
-            en.w = ~a.ip_rng[4 * j + 1];
-            if (a.ip_rng[4 * j] == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
+            en.z = rlo | PL_IP;
+            en.w = ~rhi;
+            if (rlo == 0xFFFFFFFFu) en.x = PL_SKIP;  // an all-zero row
           }
           if (EGRESS) {
-            if (a.portbits) bits = a.portbits[pr.port];
+            bits = pbits;
           } else if (a.K <= 32) {  // a bit per job slot of this representative
-            const uint32_t pb = a.portbits ? a.portbits[pr.port] : 0u;
             for (uint32_t k = 0; k < a.K; k++) {
-              const uint64_t ik = uint64_t(i) * a.K + k;
-              if (a.id_status[ik] != CYC_JOB_VALID) continue;
-              const int32_t du = a.id_desc[ik];
-              if (a.portbits ? ((pb >> du) & 1u) : a.portok[uint64_t(pr.port) * a.D + du]) bits |= 1u << k;
+              const int32_t du = sh.rdu[k];
+              if (du < 0) continue;
+              if (a.portbits ? ((pbits >> du) & 1u) : a.portok[uint64_t(pr.port) * a.D + du]) bits |= 1u << k;
             }
           }
           // spilled entries (and every entry of the wave-per-chunk rows) carry the bits themselves
@@ -2091,6 +2299,10 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     rep_window(a, i, w0, wa);
     if (WAVE && CYC_PL_PAIR) {
       pl_wave_chunk_pairs<EGRESS>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
+    } else if (WAVE && CYC_PL_PIPE && !allow_all && m <= 64 && EGRESS && a.udesc) {
+      pl_wave_chunks_pipe<EGRESS, true>(a, sh, i, m, lastmask, w0, wa);
+    } else if (WAVE && CYC_PL_PIPE && !allow_all && m <= 64) {
+      pl_wave_chunks_pipe<EGRESS>(a, sh, i, m, lastmask, w0, wa);
     } else if (WAVE && EGRESS && a.udesc) {
       pl_wave_chunks<EGRESS, true>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
     } else if (WAVE) {
@@ -2125,6 +2337,39 @@ __device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const Word
 
 constexpr uint32_t IDO_RPB_MAX = 64;  // class_rpb's upper bound
 constexpr uint32_t IDO_IPL = 16;      // IP peers per representative staged in LDS (row, span, port bits)
+#ifndef CYC_IDO_CPB
+#define CYC_IDO_CPB 1  // IDO class rows: 256-word chunks per block (the block's staging is done once for all)
+#endif
+constexpr uint32_t IDO_CPB = CYC_IDO_CPB;
+// Grid rows of the IDO class rows per (slot chunk, representative group): groups of IDO_CPB chunks.
+__host__ __device__ inline uint32_t ido_chunk_groups(uint32_t WA) { return ((WA + 255) / 256 + IDO_CPB - 1) / IDO_CPB; }
+#ifndef CYC_IDO_PF
+#define CYC_IDO_PF 0  // IDO class rows: the next (chunk, representative)'s first IP batch loaded one item ahead
+#endif
+constexpr bool IDO_PF = CYC_IDO_PF != 0;
+// The PM words (and chunk marks) of staged IP peers x0 .. x0 + N - 1 of a representative for pod word w.
+// Branch-free: every lane issues every load (a zero word where the peer is absent or w is outside its
+// span), so the batch's loads are in flight together — a load under a divergent branch is waited
+// for at the branch's end, which serialises a batch into one memory round trip per peer.
+template <uint32_t N>
+__device__ __forceinline__ void ido_ip_loads(const RowArgs& a, const uint4* sl, uint32_t x0, uint32_t ms, uint32_t w,
+                                             uint64_t (&pm)[N], uint32_t (&pbits)[N]) {
+  const uint32_t cw = (a.W + 63) / 64;
+  uint64_t v[N];
+  uint32_t cm[N];
+#pragma unroll
+  for (uint32_t u = 0; u < N; u++) {
+    const uint4 e = sl[min(x0 + u, IDO_IPL - 1)];
+    const bool in = x0 + u < ms;
+    const bool ok = in && w >= e.y && w <= e.z;
+    pbits[u] = in ? e.w : 0u;
+    v[u] = *(ok ? a.PM + uint64_t(e.x) * a.W + w : a.zero);
+    cm[u] = *(ok ? a.ip_cnz + uint64_t(e.x) * cw + w / 64 : reinterpret_cast<const uint32_t*>(a.zero));
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < N; u++) pm[u] = cm[u] ? v[u] : 0ull;
+}
+
 template <int KC>
 struct RepHead {  // a class-row block's representative: identity, class-row index, IP-peer list, slot descriptors
   uint32_t i, arow, m, ipoff;
@@ -2137,21 +2382,113 @@ struct RepHead {  // a class-row block's representative: identity, class-row ind
 template <bool EGRESS, int KC, bool UNI = false>
 __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   extern __shared__ uint64_t sB[];
-  // block = (a.rpb consecutive class representatives, KC job slots, 256 pod words): the word's
-  // runs and slot words are loaded once for all its representatives
-  const uint32_t chunks = (a.WA + 255) / 256, nkc = (a.K + KC - 1) / KC;
-  const uint32_t kc = (bid_ / chunks) % nkc;
-  const uint32_t r0 = (bid_ / (chunks * nkc)) * a.rpb, n_reps = *a.rep_cnt + 1u;
+  // block = (a.rpb consecutive class representatives, KC job slots, IDO_CPB chunks of 256 pod
+  // words): the representatives' staging is done once for the block's chunks, and each word's runs
+  // and slot words are loaded once for all its representatives
+  const uint32_t cg = ido_chunk_groups(a.WA), nkc = (a.K + KC - 1) / KC;
+  const uint32_t kc = (bid_ / cg) % nkc;
+  const uint32_t r0 = (bid_ / (cg * nkc)) * a.rpb, n_reps = *a.rep_cnt + 1u;
   if (r0 >= n_reps) return;  // whole block
   const uint32_t nr = min(a.rpb, n_reps - r0), k0 = kc * KC;
   const uint32_t nrow = EGRESS && !UNI ? a.NB : min(uint32_t(KC), a.K - k0), rowsz = nrow * a.EW;
-  // the word's own loads (runs, slot words) are issued before the staging barrier, so their
-  // latency overlaps the staging loads instead of following them
-  const uint32_t w = a.w0 + (bid_ % chunks) * 256 + threadIdx.x;
-  const bool live = w < a.w0 + a.WA;
-  WordRuns wr{};
-  if (live) wr = a.runs[w];
+  const uint32_t wend = a.w0 + a.WA, c0 = (bid_ % cg) * IDO_CPB;
+  // the first word's own loads (runs) are issued before the staging barrier, so their latency
+  // overlaps the staging loads instead of following them; each later chunk's runs are loaded one
+  // chunk ahead
+  uint32_t w = a.w0 + c0 * 256 + threadIdx.x;
+  WordRuns wr = a.runs[min(w, wend - 1)];  // (lanes past the window load a valid record and store nothing)
   const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
+  // Staging in two dependency levels, every load of a level issued unconditionally (clamped
+  // indices, zero words) so a level is one memory round trip: (1) each representative's scalars —
+  // identity, class-row index, IP-peer list, ingress slot descriptors — a thread each; (2) after a
+  // barrier, its identity sets (B) and its first IDO_IPL IP peers with their port bits.  The row
+  // loop then reads them from LDS instead of walking reps -> identity -> list chains.
+  __shared__ RepHead<KC> s_rep[IDO_RPB_MAX];
+  if (threadIdx.x < nr) {
+    RepHead<KC> h;
+    h.i = a.reps[r0 + threadIdx.x];
+    h.arow = uint32_t(arow_of(a, h.i));
+    const uint32_t cn = a.cnt[h.i], ipc = a.ip_cnt[h.i];
+    h.ipoff = a.ip_off[h.i];
+    uint8_t st[KC];
+    int32_t ds[KC];
+#pragma unroll
+    for (int kk = 0; kk < KC; kk++) {
+      const uint64_t ik = uint64_t(h.i) * a.K + min(k0 + kk, a.K - 1);
+      st[kk] = EGRESS ? uint8_t(0) : a.id_status[ik];
+      ds[kk] = EGRESS ? 0 : a.id_desc[ik];
+    }
+    h.m = cn ? ipc : 0u;
+#pragma unroll
+    for (int kk = 0; kk < KC; kk++) h.du[kk] = !EGRESS && k0 + kk < a.K && st[kk] == CYC_JOB_VALID ? ds[kk] : -2;
+    s_rep[threadIdx.x] = h;
+  }
+  int32_t ud[KC];  // egress UNI: the block's slots' descriptors (block-uniform)
+#pragma unroll
+  for (int kk = 0; kk < KC; kk++) ud[kk] = EGRESS && UNI ? a.udesc[min(k0 + kk, a.K - 1)] : 0;
+  __syncthreads();
+  {  // identity sets: nr x rowsz words, 4 loads per thread in flight at once
+    const uint32_t tot = nr * rowsz;
+    for (uint32_t x0 = threadIdx.x; x0 < tot; x0 += 4 * blockDim.x) {
+      uint64_t v[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t x = min(x0 + u * blockDim.x, tot - 1), q = x / rowsz, r = x - q * rowsz;
+        const uint64_t i = s_rep[q].i;
+        const uint64_t* src;
+        if (EGRESS && UNI) {  // the sets of the block's slots' descriptors, one row each
+          const uint32_t kk = r / a.EW;
+          int32_t d = ud[0];
+#pragma unroll
+          for (int y = 1; y < KC; y++) d = uint32_t(y) == kk ? ud[y] : d;
+          src = a.B + (i * a.NB + uint32_t(d)) * a.EW + (r - kk * a.EW);
+        } else {
+          src = a.B + (i * a.NB + (EGRESS ? 0u : k0)) * a.EW + r;
+        }
+        v[u] = *src;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++)
+        if (x0 + u * blockDim.x < tot) sB[x0 + u * blockDim.x] = v[u];
+    }
+  }
+  // the first IDO_IPL IP peers of each representative: (PM row, first word, last word, port bits —
+  // egress: the descriptor bit row; ingress: a bit per block slot), so the row loop issues only the
+  // PM loads (no list -> port table chain per batch)
+  uint4* s_il = reinterpret_cast<uint4*>(sB + ((nr * rowsz + 1) & ~1u));  // 16-byte aligned
+  const bool stage_ip = !EGRESS || a.portbits != nullptr;
+  if (stage_ip) {
+    for (uint32_t t = threadIdx.x; t < nr * IDO_IPL; t += blockDim.x) {
+      const RepHead<KC>& h = s_rep[t / IDO_IPL];
+      const uint32_t x = t % IDO_IPL;
+      const bool ok = x < h.m;
+      const uint4 jp = *(ok ? a.ip_list + h.ipoff + x : reinterpret_cast<const uint4*>(a.zero));
+      uint32_t bits = 0;
+      if (EGRESS) {
+        bits = *(ok ? a.portbits + jp.y : reinterpret_cast<const uint32_t*>(a.zero));
+      } else {
+        uint8_t pk[KC];
+#pragma unroll
+        for (int kk = 0; kk < KC; kk++)
+          pk[kk] = *(ok ? a.portok + uint64_t(jp.y) * a.D + uint32_t(max(h.du[kk], 0)) : reinterpret_cast<const uint8_t*>(a.zero));
+#pragma unroll
+        for (int kk = 0; kk < KC; kk++)
+          if (h.du[kk] >= 0 && pk[kk]) bits |= 1u << kk;
+      }
+      if (ok) s_il[t] = make_uint4(jp.x, jp.z, jp.w, bits);
+    }
+  }
+  __syncthreads();
+  // 16-byte stores of word pairs (store_row_pair): even rows of the class rows' window, aligned base
+  const bool pair = a.WA % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
+  const uint32_t cend = min(c0 + IDO_CPB, (a.WA + 255) / 256);
+  uint64_t pf_pm[PEER_BATCH];
+  uint32_t pf_bits[PEER_BATCH];
+  if (IDO_PF) ido_ip_loads(a, s_il, 0u, w < wend && stage_ip ? min(s_rep[0].m, IDO_IPL) : 0u, w, pf_pm, pf_bits);
+  for (uint32_t c = c0; c < cend; c++, w += 256) {  // no barrier below: lanes leave independently
+  if (w >= wend) break;
+  const WordRuns wcur = wr;
+  if (c + 1 < cend && w + 256 < wend) wr = a.runs[w + 256];  // the next chunk's runs, in flight meanwhile
   const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
   uint64_t valid[KC];
   int32_t du[KC];
@@ -2161,70 +2498,29 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     valid[kk] = 0;
     du[kk] = -2;
     if (EGRESS && UNI && k < a.K) {
-      valid[kk] = live ? wmask : 0ull;
+      valid[kk] = wmask;
       du[kk] = a.udesc[k];
-    } else if (EGRESS && k < a.K && live) {
+    } else if (EGRESS && k < a.K) {
       valid[kk] = a.VALID[uint64_t(k) * a.W + w];
       du[kk] = a.DESCW[uint64_t(k) * a.W + w];
     }
   }
-  // each representative's scalars (identity, class-row index, IP-peer list, ingress slot
-  // descriptors) are loaded once per block, before the barrier: the row loop below then reads them
-  // from LDS instead of walking reps -> identity -> list chains per representative after it
-  __shared__ RepHead<KC> s_rep[IDO_RPB_MAX];
-  if (threadIdx.x < nr) {
-    RepHead<KC> h;
-    h.i = a.reps[r0 + threadIdx.x];
-    h.arow = uint32_t(arow_of(a, h.i));
-    h.m = a.cnt[h.i] ? a.ip_cnt[h.i] : 0u;
-    h.ipoff = a.ip_off[h.i];
-#pragma unroll
-    for (int kk = 0; kk < KC; kk++) {
-      const uint32_t k = k0 + kk;
-      h.du[kk] = -2;
-      if (!EGRESS && k < a.K && a.id_status[uint64_t(h.i) * a.K + k] == CYC_JOB_VALID) h.du[kk] = a.id_desc[uint64_t(h.i) * a.K + k];
-    }
-    s_rep[threadIdx.x] = h;
-  }
-  for (uint32_t q = 0; q < nr; q++) {
-    if (EGRESS && UNI) {  // the sets of the block's slots' descriptors, one row each
-      for (uint32_t x = threadIdx.x; x < rowsz; x += blockDim.x) {
-        const uint32_t kk = x / a.EW;
-        sB[q * rowsz + x] = a.B[(uint64_t(a.reps[r0 + q]) * a.NB + uint32_t(a.udesc[k0 + kk])) * a.EW + (x - kk * a.EW)];
-      }
-      continue;
-    }
-    const uint64_t* src = a.B + (uint64_t(a.reps[r0 + q]) * a.NB + (EGRESS ? 0u : k0)) * a.EW;
-    for (uint32_t x = threadIdx.x; x < rowsz; x += blockDim.x) sB[q * rowsz + x] = src[x];
-  }
-  __syncthreads();
-  // the first IDO_IPL IP peers of each representative, staged after the heads: (PM row, first
-  // word, last word, port bits — egress: the descriptor bit row; ingress: a bit per block slot), so
-  // the row loop issues only the PM loads (no list -> port table chain per batch)
-  uint4* s_il = reinterpret_cast<uint4*>(sB + ((nr * rowsz + 1) & ~1u));  // 16-byte aligned
-  const bool stage_ip = !EGRESS || a.portbits != nullptr;
-  if (stage_ip) {
-    for (uint32_t t = threadIdx.x; t < nr * IDO_IPL; t += blockDim.x) {
-      const RepHead<KC>& h = s_rep[t / IDO_IPL];
-      const uint32_t x = t % IDO_IPL;
-      if (x >= h.m) continue;
-      const uint4 jp = a.ip_list[h.ipoff + x];
-      uint32_t bits = 0;
-      if (EGRESS) bits = a.portbits[jp.y];
-      else
-#pragma unroll
-        for (int kk = 0; kk < KC; kk++)
-          if (h.du[kk] >= 0 && a.portok[uint64_t(jp.y) * a.D + h.du[kk]]) bits |= 1u << kk;
-      s_il[t] = make_uint4(jp.x, jp.z, jp.w, bits);
-    }
-    __syncthreads();
-  }
-  if (!live) return;
-  // 16-byte stores of word pairs (store_row_pair): even rows of the class rows' window, aligned base
-  const bool pair = a.WA % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
   for (uint32_t q = 0; q < nr; q++) {
     const RepHead<KC>& h = s_rep[q];
     const uint64_t* sb = sB + q * rowsz;
+    uint64_t cur_pm[PEER_BATCH];
+    uint32_t cur_bits[PEER_BATCH];
+    if (IDO_PF) {  // this item's first IP batch (loaded one item ahead); the next item's, in flight meanwhile
+#pragma unroll
+      for (uint32_t u = 0; u < PEER_BATCH; u++) {
+        cur_pm[u] = pf_pm[u];
+        cur_bits[u] = pf_bits[u];
+      }
+      const bool same = q + 1 < nr;
+      const uint32_t nq = same ? q + 1 : 0u, nw = same ? w : w + 256;
+      const bool more = same || (c + 1 < cend && nw < wend);
+      ido_ip_loads(a, s_il + nq * IDO_IPL, 0u, more && stage_ip ? min(s_rep[nq].m, IDO_IPL) : 0u, nw, pf_pm, pf_bits);
+    }
     uint64_t allow[KC];
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
@@ -2236,10 +2532,10 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
           valid[kk] = du[kk] >= 0 ? wmask : 0ull;
         }
         if (du[kk] >= 0) {
-          allow[kk] = expand_runs(sb + uint64_t(EGRESS && !UNI ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wr);
+          allow[kk] = expand_runs(sb + uint64_t(EGRESS && !UNI ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wcur);
         } else if (EGRESS && !UNI && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
           const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
-          for (uint32_t d = 0; d < a.D; d++) allow[kk] |= expand_runs(sb + uint64_t(d) * a.EW, wr) & dm[uint64_t(d) * a.W];
+          for (uint32_t d = 0; d < a.D; d++) allow[kk] |= expand_runs(sb + uint64_t(d) * a.EW, wcur) & dm[uint64_t(d) * a.W];
         }
       }
     }
@@ -2252,15 +2548,14 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     for (uint32_t x0 = 0; x0 < ms; x0 += PEER_BATCH) {
       uint64_t pm[PEER_BATCH];
       uint32_t pbits[PEER_BATCH];
+      if (IDO_PF && x0 == 0) {
 #pragma unroll
-      for (uint32_t u = 0; u < PEER_BATCH; u++) {
-        pm[u] = 0;
-        pbits[u] = 0;
-        if (x0 + u < ms) {
-          const uint4 e = sl[x0 + u];
-          pbits[u] = e.w;
-          if (w >= e.y && w <= e.z) pm[u] = a.PM[uint64_t(e.x) * a.W + w] & cnz_mask(a.ip_cnz, a.W, e.x, w);
+        for (uint32_t u = 0; u < PEER_BATCH; u++) {
+          pm[u] = cur_pm[u];
+          pbits[u] = cur_bits[u];
         }
+      } else {
+        ido_ip_loads(a, sl, x0, ms, w, pm, pbits);
       }
       undecided = 0;
 #pragma unroll
@@ -2328,6 +2623,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
 #pragma unroll
     for (int x = 0; x < KC; x++)
       if (x >= kk && k0 + x < a.K) rows[uint64_t(x) * a.WA + off] = allow[x] & valid[x];
+  }
   }
 }
 template <bool EGRESS, int KC, bool UNI = false>
@@ -3120,7 +3416,8 @@ struct cyc_ctx {
   // peer-row stage: pod peers in identity space + per-word identity runs; IP peers per pod
   DevBuf pod_peers_u;  // identity-set (IDOB) rows: the needed pod peers, one per distinct
                        // (namespace matcher, pod selector) of a direction (peer_ido maps every peer)
-  DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, idob, runs, ip_rng, lvt, dreqs;
+  DevBuf pod_peers, ip_peers, ip_tests, ip_ex, id_nsls, word_off, run_e, run_mask, ido, ip_words, peer_ido, peer_row, zeros, idob, runs, ip_rng, lvt, dreqs;
+  std::vector<uint32_t> prow_host;  // peer_row on the host (the panic describer reads PM / ER rows by it)
   DevBuf udesc;     // per slot the one VALID descriptor every pod has, when all slots are so (uni_desc)
   bool uni_desc = false;
   DevBuf plvt;      // LVT per pod (SelView::PLVT), built by ensure_plvt when it fits PLVT_MAX_BYTES
@@ -3587,6 +3884,10 @@ static void prepare_device(cyc_ctx* c) {
     dd.err.alloc(std::max<uint64_t>(dd.n, 16));
     dd.ht_key.alloc(uint64_t(dd.ht_cap) * 12 + 16);  // [cap] u64 keys (empty = ~0), [cap] u32 reps, counter
     HIPCHK(hipMemset(dd.ht_key.p, 0xFF, dd.ht_key.bytes));  // empty; afterwards every run's class rows empty it
+    if (!c->zeros.p) {
+      c->zeros.alloc(256);
+      HIPCHK(hipMemset(c->zeros.p, 0, 256));
+    }
     dd.reps.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.class_of.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.A.alloc(std::max<uint64_t>(uint64_t(dd.n) * K * W * 8, 16));
@@ -3826,17 +4127,36 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   upload(c->sel_list, sl);
   std::vector<uint32_t> pp, ip;
   std::vector<DIPTest> tests;
+  // An IP peer's row depends only on its IPBlock (ippeermatcher.go:43-50; the port is tested by the
+  // class rows): peers of one direction whose (cidr, except) strings are equal share the row of
+  // the first (config #4: the 0.0.0.0/0-style blocks of ~2,500 peers are 5 rows).  prow maps every
+  // peer to its row; only the first of each IPBlock gets an IP-row test.
+  std::vector<uint32_t> prow(std::max<size_t>(pb.peers.size(), 1));
+  for (uint32_t j = 0; j < prow.size(); j++) prow[j] = j;
   for (int d = 0; d < 2; d++) {  // ingress peers first, then egress: one sub-list per branch
     c->rp_off[d] = uint32_t(pp.size());
     c->ri_off[d] = uint32_t(ip.size());
     for (uint32_t j : c->plan.pod_peers)
       if (peer_needed[j] && peer_dir[j] == d) pp.push_back(j);
-    for (size_t r = 0; r < c->plan.ip_peers.size(); r++)
-      if (peer_needed[c->plan.ip_peers[r]] && peer_dir[c->plan.ip_peers[r]] == d) {
-        ip.push_back(c->plan.ip_peers[r]);
-        tests.push_back(c->plan.ip_tests[r]);
+    std::map<std::vector<uint32_t>, uint32_t> ipb_row;
+    std::vector<uint32_t> key;
+    for (size_t r = 0; r < c->plan.ip_peers.size(); r++) {
+      const uint32_t j = c->plan.ip_peers[r];
+      if (!peer_needed[j] || peer_dir[j] != d) continue;
+      const DIPBlock& b = pb.ipbs[pb.peers[j].ipb];
+      key.assign(1, b.cidr);
+      key.insert(key.end(), pb.ipb_ex.begin() + b.exoff, pb.ipb_ex.begin() + b.exoff + b.excnt);
+      auto it = ipb_row.emplace(key, j);
+      if (!it.second) {
+        prow[j] = it.first->second;
+        continue;
       }
+      ip.push_back(j);
+      tests.push_back(c->plan.ip_tests[r]);
+    }
   }
+  upload(c->peer_row, prow);
+  c->prow_host = prow;
   c->rp_off[2] = uint32_t(pp.size());
   c->ri_off[2] = uint32_t(ip.size());
   c->Rp = uint32_t(pp.size());
@@ -4076,6 +4396,8 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.rep_cnt = dd.rep_cnt();
   ra.IDOB = c->idob.as<uint64_t>();
   ra.peer_ido = c->peer_ido.as<uint32_t>();
+  ra.prow = c->peer_row.as<uint32_t>();
+  ra.zero = c->zeros.as<uint64_t>();
   ra.runs = c->runs.as<WordRuns>();
   ra.B = dd.B.as<uint64_t>();
   ra.ip_off = dd.ip_off.as<uint32_t>();
@@ -4123,7 +4445,7 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     const uint32_t rows = d == 0 ? std::min<uint32_t>(4, K) : D;
     const size_t per = size_t(rows) * ra.EW * 8 + IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
     ra.rpb = class_rpb(c, per);
-    const unsigned gi = unsigned(uint64_t((ra.WA + 255) / 256) * ((K + 3) / 4) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
+    const unsigned gi = unsigned(uint64_t(ido_chunk_groups(ra.WA)) * ((K + 3) / 4) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
     if (d == 0) k_class_rows_ido<false, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
     else k_class_rows_ido<true, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
   } else {  // per-class flattened peer lists (the IP word spans are final here)
@@ -4429,7 +4751,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     const size_t per = size_t(d == 0 || fe.ra[d].udesc ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8 +
                        IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
     fe.ra[d].rpb = class_rpb(c, per);
-    fe.nb[d] = blocks(uint64_t((fe.ra[d].WA + 255) / 256) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
+    fe.nb[d] = blocks(uint64_t(ido_chunk_groups(fe.ra[d].WA)) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
     if (d == 1 && fe.ra[d].udesc) lds_uni = per * fe.ra[d].rpb;
     else lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
@@ -4789,8 +5111,9 @@ int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t id
           continue;
         }
         uint64_t pm, er;
-        HIPCHK(hipMemcpy(&pm, c->PM.as<uint64_t>() + size_t(j) * pb.W + peer / 64, 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&er, c->ER.as<uint64_t>() + size_t(j) * pb.W + peer / 64, 8, hipMemcpyDeviceToHost));
+        const size_t row = pr.kind == 3 && j < c->prow_host.size() ? c->prow_host[j] : j;  // IP peers share their IPBlock's row
+        HIPCHK(hipMemcpy(&pm, c->PM.as<uint64_t>() + row * pb.W + peer / 64, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&er, c->ER.as<uint64_t>() + row * pb.W + peer / 64, 8, hipMemcpyDeviceToHost));
         if ((er >> (peer % 64)) & 1) {
           if (pr.kind == 2) return fail(c, CYC_ERR_PANIC_SELECTOR, "invalid operator");
           std::string msg;
