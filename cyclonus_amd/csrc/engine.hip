@@ -232,29 +232,6 @@ __device__ __forceinline__ uint32_t sel_at(const SelView& v, uint32_t s, uint32_
   if (d.x != SEL_WALK) return req_holds(d.x & 0xFFu, v.LVT[uint64_t(d.y) * v.L + l], d.z, d.w, d.x >> 8) ? 1u : 0u;
   return sel_eval(v, v.LVT, v.L, s, l);
 }
-// N selectors on label set l with every load of the batch in flight together: the one-requirement
-// records first, then each one's label-table load, unconditionally (a load inside a divergent branch
-// is waited for at the branch's end); only a selector of several requirements walks them.
-template <uint32_t N>
-__device__ __forceinline__ void sel_at_n(const SelView& v, const uint32_t (&s)[N], uint32_t l, uint8_t (&r)[N]) {
-  if (v.selres) {
-#pragma unroll
-    for (uint32_t x = 0; x < N; x++) r[x] = v.selres[uint64_t(s[x]) * v.L + l];
-    return;
-  }
-  uint4 d[N];
-  uint32_t xv[N];
-#pragma unroll
-  for (uint32_t x = 0; x < N; x++) d[x] = v.one[s[x]];
-#pragma unroll
-  for (uint32_t x = 0; x < N; x++) xv[x] = v.LVT[uint64_t(d[x].x < SEL_ALL ? d[x].y : 0u) * v.L + l];
-#pragma unroll
-  for (uint32_t x = 0; x < N; x++) {
-    if (d[x].x == SEL_ALL) r[x] = 1;
-    else if (d[x].x != SEL_WALK) r[x] = req_holds(d[x].x & 0xFFu, xv[x], d[x].z, d[x].w, d[x].x >> 8) ? 1 : 0;
-    else r[x] = uint8_t(sel_eval(v, v.LVT, v.L, s[x], l));
-  }
-}
 // Mixes identity i's ingress slot descriptors into its class hash (status and descriptor of every
 // slot), 8 slots' loads in flight at once.
 __device__ __forceinline__ uint64_t hash_slots(uint64_t h, const uint8_t* __restrict__ id_status, const int32_t* __restrict__ id_desc,
@@ -1022,10 +999,9 @@ __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t
     uint32_t sel[MB];
     uint8_t r[MB];
 #pragma unroll
-    for (uint32_t x = 0; x < MB; x++) sel[x] = a.tgt[min(t0 + x, hi - 1)].sel;
-    sel_at_n<MB>(a.sv, sel, ls, r);
+    for (uint32_t x = 0; x < MB; x++) sel[x] = t0 + x < hi ? a.tgt[t0 + x].sel : 0u;
 #pragma unroll
-    for (uint32_t x = 0; x < MB; x++) r[x] = t0 + x < hi ? r[x] : uint8_t(0);
+    for (uint32_t x = 0; x < MB; x++) r[x] = t0 + x < hi ? uint8_t(sel_at(a.sv, sel[x], ls)) : 0;
 #pragma unroll
     for (uint32_t x = 0; x < MB; x++) {
       const uint32_t t = t0 + x;
@@ -1836,9 +1812,7 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
 #ifndef CYC_PL_WBATCH
 #define CYC_PL_WBATCH 8
 #endif
-#ifndef CYC_PL_PIPE
-#define CYC_PL_PIPE 1  // classes of <= 64 entries: pl_wave_chunks_pipe
-#endif
+
 constexpr uint32_t PL_WBATCH = CYC_PL_WBATCH, PL_NB = 4;
 // An entry's lane fields for the wave-per-chunk rows: row, port bits, mask of the 64-word chunks
 // holding a nonzero PM word of it (IP rows: from the IP-row pass; other rows: all)
@@ -1878,109 +1852,6 @@ __device__ __forceinline__ void pl_load_batch(const RowArgs& a, const PlLane& g,
     }
     const uint64_t x = *(row < PL_SKIP ? a.PM + uint64_t(row) * a.W + wl : a.zero);
     v[u] = row == PL_ONES ? ~0ull : x;
-  }
-}
-
-// pl_wave_chunks for classes of at most 64 entries (one lane group), software-pipelined: the first
-// batch of the wave's NEXT chunk (and its slot words) is loaded before this chunk's class-row stores
-// are issued.  On gfx9 a wave's loads and stores share one in-order counter, so a batch loaded after
-// the stores would wait for them too; loaded before, the wait leaves the stores in flight and the
-// wave's store traffic overlaps its next chunk's PM loads.
-template <bool EGRESS, bool UNI = false>
-__device__ __forceinline__ void pl_wave_chunks_pipe(const RowArgs& a, const PlShared& sh, uint32_t i, uint32_t m,
-                                                    uint64_t lastmask, uint32_t w0, uint32_t wa) {
-  const uint32_t lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
-  const uint32_t cend = (w0 + wa + 63) / 64;
-  uint32_t c = w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (c >= cend) return;
-  const PlLane g = pl_lane(a, sh.e, lane, m);
-  uint64_t* const rows = a.A + arow_of(a, i) * a.K * a.WA;  // the class row's slot 0
-  const bool pair = a.WA % 2 == 0 && w0 % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
-  uint32_t vslots = 0;  // ingress: the representative's VALID slots (class_rows_pl_blk staged them)
-  if (!EGRESS)
-#pragma unroll
-    for (uint32_t k = 0; k < PL_NB; k++)
-      if (k < a.K && sh.rdu[k] >= 0) vslots |= 1u << k;
-  // the slot words of chunk c (egress with per-destination descriptors: VALID / DESCW loads)
-  auto slot_words = [&](uint32_t cc, uint64_t (&valid)[PL_NB], int32_t (&du)[PL_NB]) {
-    const uint32_t w = cc * 64 + lane, wl = min(max(w, w0), w0 + wa - 1);
-#pragma unroll
-    for (uint32_t k = 0; k < PL_NB; k++) {
-      valid[k] = 0;
-      du[k] = -2;
-      if (k < a.K) {  // block-uniform
-        if (EGRESS && UNI) {
-          valid[k] = w == a.W - 1 ? lastmask : ~0ull;
-          du[k] = a.udesc[k];
-        } else if (EGRESS) {
-          valid[k] = a.VALID[uint64_t(k) * a.W + wl];
-          du[k] = a.DESCW[uint64_t(k) * a.W + wl];
-        } else if ((vslots >> k) & 1u) {
-          valid[k] = w == a.W - 1 ? lastmask : ~0ull;
-        }
-      }
-    }
-  };
-  uint64_t v[PL_WBATCH], valid[PL_NB];
-  uint32_t bits[PL_WBATCH];
-  int32_t du[PL_NB];
-  uint64_t todo = __ballot((g.cm >> c) & 1ull);
-  pl_load_batch(a, g, todo, min(max(c * 64 + lane, w0), w0 + wa - 1), v, bits);
-  slot_words(c, valid, du);
-  for (; c < cend; c += nwaves) {
-    const uint32_t w = c * 64 + lane;
-    const bool live = w >= w0 && w < w0 + wa;
-    const uint32_t wl = live ? w : min(max(w, w0), w0 + wa - 1);
-    uint64_t acc[PL_NB];
-#pragma unroll
-    for (uint32_t d = 0; d < PL_NB; d++) acc[d] = 0;
-    while (true) {  // the prefetched batch, then (entries past PL_WBATCH in this chunk) further ones
-#pragma unroll
-      for (uint32_t u = 0; u < PL_WBATCH; u++)
-#pragma unroll
-        for (uint32_t d = 0; d < PL_NB; d++)
-          if ((bits[u] >> d) & 1u) acc[d] |= v[u];
-      if (!todo) break;
-      pl_load_batch(a, g, todo, wl, v, bits);
-    }
-    uint64_t rr[PL_NB];
-#pragma unroll
-    for (uint32_t k = 0; k < PL_NB; k++) {
-      uint64_t r = 0;
-      if (k >= a.K) {
-      } else if (!EGRESS) r = acc[k] & valid[k];
-      else if (du[k] >= 0) {
-#pragma unroll
-        for (uint32_t d = 0; d < PL_NB; d++) r = uint32_t(du[k]) == d ? acc[d] : r;
-        r &= valid[k];
-      } else if (du[k] == -1) {  // destinations with mixed job descriptors (rare)
-        const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + wl;
-#pragma unroll
-        for (uint32_t d = 0; d < PL_NB; d++)
-          if (d < a.D) r |= acc[d] & dm[uint64_t(d) * a.W];
-        r &= valid[k];
-      }
-      rr[k] = r;
-    }
-    // the next chunk's first batch and slot words, before this chunk's stores
-    const uint32_t cn = c + nwaves;
-    if (cn < cend) {
-      todo = __ballot((g.cm >> cn) & 1ull);
-      pl_load_batch(a, g, todo, min(max(cn * 64 + lane, w0), w0 + wa - 1), v, bits);
-      slot_words(cn, valid, du);
-    }
-    if (!live) continue;
-    const uint64_t off = w - w0;
-    uint32_t k = 0;
-    if (pair)
-#pragma unroll
-      for (; k + 1 < PL_NB; k += 2) {
-        if (k + 1 >= a.K) break;
-        store_row_pair(rows + uint64_t(k) * a.WA, rows + uint64_t(k + 1) * a.WA, off, rr[k], rr[k + 1], lane & 1);
-      }
-#pragma unroll
-    for (uint32_t kk = 0; kk < PL_NB; kk++)
-      if (kk >= k && kk < a.K) rows[uint64_t(kk) * a.WA + off] = rr[kk];
   }
 }
 
@@ -2033,18 +1904,7 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
       while (todo) {
         uint32_t bits[PL_WBATCH];
         uint64_t v[PL_WBATCH];
-#pragma unroll
-        for (uint32_t u = 0; u < PL_WBATCH; u++) {
-          bits[u] = 0;
-          v[u] = 0;
-          if (todo) {
-            const uint32_t src = __ffsll((unsigned long long)todo) - 1;
-            todo &= todo - 1;
-            const uint32_t row = __builtin_amdgcn_readlane(g.row, src);
-            bits[u] = __builtin_amdgcn_readlane(g.bits, src);
-            v[u] = row == PL_ONES ? ~0ull : a.PM[uint64_t(row) * a.W + wl];
-          }
-        }
+        pl_load_batch(a, g, todo, wl, v, bits);
 #pragma unroll
         for (uint32_t u = 0; u < PL_WBATCH; u++)
 #pragma unroll
@@ -2299,10 +2159,6 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     rep_window(a, i, w0, wa);
     if (WAVE && CYC_PL_PAIR) {
       pl_wave_chunk_pairs<EGRESS>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
-    } else if (WAVE && CYC_PL_PIPE && !allow_all && m <= 64 && EGRESS && a.udesc) {
-      pl_wave_chunks_pipe<EGRESS, true>(a, sh, i, m, lastmask, w0, wa);
-    } else if (WAVE && CYC_PL_PIPE && !allow_all && m <= 64) {
-      pl_wave_chunks_pipe<EGRESS>(a, sh, i, m, lastmask, w0, wa);
     } else if (WAVE && EGRESS && a.udesc) {
       pl_wave_chunks<EGRESS, true>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
     } else if (WAVE) {
@@ -2338,15 +2194,12 @@ __device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const Word
 constexpr uint32_t IDO_RPB_MAX = 64;  // class_rpb's upper bound
 constexpr uint32_t IDO_IPL = 16;      // IP peers per representative staged in LDS (row, span, port bits)
 #ifndef CYC_IDO_CPB
-#define CYC_IDO_CPB 1  // IDO class rows: 256-word chunks per block (the block's staging is done once for all)
+#define CYC_IDO_CPB 1  // IDO class rows: 256-word chunks per block (the block's staging is done once for all;
+                       // 2 / 4 / 7 measured slower on config #3: profiles/r03_ido_rows_ab.txt)
 #endif
 constexpr uint32_t IDO_CPB = CYC_IDO_CPB;
 // Grid rows of the IDO class rows per (slot chunk, representative group): groups of IDO_CPB chunks.
 __host__ __device__ inline uint32_t ido_chunk_groups(uint32_t WA) { return ((WA + 255) / 256 + IDO_CPB - 1) / IDO_CPB; }
-#ifndef CYC_IDO_PF
-#define CYC_IDO_PF 0  // IDO class rows: the next (chunk, representative)'s first IP batch loaded one item ahead
-#endif
-constexpr bool IDO_PF = CYC_IDO_PF != 0;
 // The PM words (and chunk marks) of staged IP peers x0 .. x0 + N - 1 of a representative for pod word w.
 // Branch-free: every lane issues every load (a zero word where the peer is absent or w is outside its
 // span), so the batch's loads are in flight together — a load under a divergent branch is waited
@@ -2482,9 +2335,6 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   // 16-byte stores of word pairs (store_row_pair): even rows of the class rows' window, aligned base
   const bool pair = a.WA % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
   const uint32_t cend = min(c0 + IDO_CPB, (a.WA + 255) / 256);
-  uint64_t pf_pm[PEER_BATCH];
-  uint32_t pf_bits[PEER_BATCH];
-  if (IDO_PF) ido_ip_loads(a, s_il, 0u, w < wend && stage_ip ? min(s_rep[0].m, IDO_IPL) : 0u, w, pf_pm, pf_bits);
   for (uint32_t c = c0; c < cend; c++, w += 256) {  // no barrier below: lanes leave independently
   if (w >= wend) break;
   const WordRuns wcur = wr;
@@ -2508,19 +2358,6 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   for (uint32_t q = 0; q < nr; q++) {
     const RepHead<KC>& h = s_rep[q];
     const uint64_t* sb = sB + q * rowsz;
-    uint64_t cur_pm[PEER_BATCH];
-    uint32_t cur_bits[PEER_BATCH];
-    if (IDO_PF) {  // this item's first IP batch (loaded one item ahead); the next item's, in flight meanwhile
-#pragma unroll
-      for (uint32_t u = 0; u < PEER_BATCH; u++) {
-        cur_pm[u] = pf_pm[u];
-        cur_bits[u] = pf_bits[u];
-      }
-      const bool same = q + 1 < nr;
-      const uint32_t nq = same ? q + 1 : 0u, nw = same ? w : w + 256;
-      const bool more = same || (c + 1 < cend && nw < wend);
-      ido_ip_loads(a, s_il + nq * IDO_IPL, 0u, more && stage_ip ? min(s_rep[nq].m, IDO_IPL) : 0u, nw, pf_pm, pf_bits);
-    }
     uint64_t allow[KC];
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) {
@@ -2548,15 +2385,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     for (uint32_t x0 = 0; x0 < ms; x0 += PEER_BATCH) {
       uint64_t pm[PEER_BATCH];
       uint32_t pbits[PEER_BATCH];
-      if (IDO_PF && x0 == 0) {
-#pragma unroll
-        for (uint32_t u = 0; u < PEER_BATCH; u++) {
-          pm[u] = cur_pm[u];
-          pbits[u] = cur_bits[u];
-        }
-      } else {
-        ido_ip_loads(a, sl, x0, ms, w, pm, pbits);
-      }
+      ido_ip_loads(a, sl, x0, ms, w, pm, pbits);
       undecided = 0;
 #pragma unroll
       for (int kk = 0; kk < KC; kk++) {
