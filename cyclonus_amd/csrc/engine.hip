@@ -355,6 +355,12 @@ __global__ __launch_bounds__(256) void k_pod_rows(uint32_t Rp, uint32_t E, uint3
   if (ERR) ER[j * W + w] = e;
 }
 
+struct DWordNS {
+  uint32_t lo, hi;  // namespace string ids of the word's (chunk's) pods: min, max
+  uint32_t nsls;    // their namespace label set when lo == hi
+  uint32_t pad;
+};
+
 // Pod-peer rows straight from each pod's egress identity: one wave per (pod peer, 64-pod word),
 // lane = pod, one ballot per word.  Used when identities are about as many as pods (every pod
 // labelled apart, e.g. a `pod: <name>` label): then the identity-space outcomes cost as much as
@@ -366,16 +372,32 @@ __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uin
                                                          const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres,
                                                          uint32_t L, const uint32_t* __restrict__ pod_eid,
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
-                                                         const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
-                                                         uint64_t* __restrict__ ER, uint32_t bid_, uint32_t nblk_, uint32_t w0,
-                                                         uint32_t nw) {
+                                                         const uint32_t* __restrict__ id_ls, const DWordNS* __restrict__ nsw,
+                                                         uint64_t* __restrict__ PM, uint64_t* __restrict__ ER, uint32_t bid_,
+                                                         uint32_t nblk_, uint32_t w0, uint32_t nw) {
   const uint32_t lane = threadIdx.x & 63, gw = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6));  // wave-uniform
   const uint32_t p = gw / nw, w = w0 + (gw - p * nw);
   if (p >= Rp) return;
   const uint32_t j = pod_peers[p];
   const DPeer pr = peers[j];
+  // the namespace matcher first (podpeermatcher.go:21-28), on the word's namespace record: an exact
+  // namespace outside the word's namespace range, or a namespace selector that rejects the word's
+  // only namespace, rejects every pod of the word before its pod matcher runs (no panic possible
+  // either) — a zero word, without the pods' identity and selector loads (config #2: most words)
+  // (the pods' identity loads are issued first, with the record's: a word that is not skipped
+  // pays no extra round trip)
   const uint32_t q = w * 64 + lane;
   const uint32_t e = pod_eid[min(q, P - 1)];  // (clamped: no load inside a branch)
+  const DWordNS wn = nsw[w];
+  const uint8_t rns = selres[pr.nskind == 2 && wn.lo == wn.hi ? uint64_t(pr.nsval) * L + wn.nsls : 0u];
+  const bool none = pr.nskind == 0 ? (pr.nsval < wn.lo || pr.nsval > wn.hi) : (pr.nskind == 2 && wn.lo == wn.hi && rns == 0);
+  if (none) {
+    if (lane == 0) {
+      PM[uint64_t(j) * W + w] = 0;
+      if (ERR) ER[uint64_t(j) * W + w] = 0;
+    }
+    return;
+  }
   uint32_t o = pod_peer_outcome(pr, selres, L, id_ns[e], id_nsls[e], id_ls[e]);
   if (q >= P) o = 0;
   const uint64_t m = __ballot(o == 1);
@@ -391,8 +413,10 @@ __global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P
                                                          const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres,
                                                          uint32_t L, const uint32_t* __restrict__ pod_eid,
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
-                                                         const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
-                                                         uint64_t* __restrict__ ER, uint32_t w0, uint32_t nw) { pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, PM, ER, blockIdx.x, gridDim.x, w0, nw); }
+                                                         const uint32_t* __restrict__ id_ls, const DWordNS* __restrict__ nsw,
+                                                         uint64_t* __restrict__ PM, uint64_t* __restrict__ ER, uint32_t w0, uint32_t nw) {
+  pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, nsw, PM, ER, blockIdx.x, gridDim.x, w0, nw);
+}
 
 // Pod-peer rows of the fused front on PM builds (no panic possible), stored sparse, 64-word chunks
 // at a time with lane = pod word (block shapes: pod_rows_sparse_blk).  The namespace
@@ -404,11 +428,6 @@ __global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P
 // (their loads in flight together).  Rows are stored chunk-dense with their nonzero word span and chunk masks,
 // exactly like the IP rows (ip_row_word), so the class rows skip their zero chunks: with every pod
 // labelled apart (identities ~ pods) most pod-peer rows are a namespace's worth of words.
-struct DWordNS {
-  uint32_t lo, hi;  // namespace string ids of the word's (chunk's) pods: min, max
-  uint32_t nsls;    // their namespace label set when lo == hi
-  uint32_t pad;
-};
 #ifndef CYC_PR_WB
 #define CYC_PR_WB 8
 #endif
@@ -675,7 +694,7 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
 // together and drop the PM word of an all-zero chunk, so the zero chunks — most of a row — cost
 // no HBM writes.
 #ifndef CYC_IP_MIXB
-#define CYC_IP_MIXB 2  // straddling words of an IP row whose pod addresses are loaded at once
+#define CYC_IP_MIXB 1  // straddling words of an IP row whose pod addresses are loaded at once (2: config #4 launch B +4 us)
 #endif
 constexpr uint32_t IP_MIXB = CYC_IP_MIXB;
 __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
@@ -1810,7 +1829,7 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
 // bit.  The accumulators become the class rows through each word's slot descriptor (DESCW; the DM
 // masks for mixed words).
 #ifndef CYC_PL_WBATCH
-#define CYC_PL_WBATCH 8
+#define CYC_PL_WBATCH 4  // PM words in flight per wave-per-chunk batch (8: 78 VGPRs, config #4 class rows +7 us: profiles/r03_front_b_d_ab.txt)
 #endif
 
 constexpr uint32_t PL_WBATCH = CYC_PL_WBATCH, PL_NB = 4;
@@ -1946,104 +1965,6 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
   }
 }
 
-// The same with two chunks per step of a wave (c and c + nwaves): the batches take the entries of
-// both chunks, so one memory round trip serves two chunks (CYC_PL_PAIR).
-#ifndef CYC_PL_PAIR
-#define CYC_PL_PAIR 0
-#endif
-template <bool EGRESS>
-__device__ __forceinline__ void pl_wave_chunk_pairs(const RowArgs& a, const PlShared& sh, const uint4* spill, uint32_t i,
-                                                    uint32_t m, bool allow_all, uint64_t lastmask, uint32_t w0, uint32_t wa) {
-  const uint32_t lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
-  const uint32_t cend = (w0 + wa + 63) / 64;
-  const PlLane g0 = pl_lane(a, sh.e, lane, m);
-  for (uint32_t c = w0 / 64 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < cend; c += 2 * nwaves) {
-    const uint32_t cc[2] = {c, c + nwaves};
-    uint32_t wv[2], wl[2];
-    bool live[2];
-    uint64_t valid[2][PL_NB], acc[2][PL_NB];
-    int32_t du[2][PL_NB];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      wv[h] = cc[h] * 64 + lane;
-      live[h] = cc[h] < cend && wv[h] >= w0 && wv[h] < w0 + wa;
-      wl[h] = live[h] ? wv[h] : w0;
-#pragma unroll
-      for (uint32_t k = 0; k < PL_NB; k++) {
-        valid[h][k] = 0;
-        du[h][k] = -2;
-        if (k < a.K) {
-          if (EGRESS) {
-            valid[h][k] = a.VALID[uint64_t(k) * a.W + wl[h]];
-            du[h][k] = a.DESCW[uint64_t(k) * a.W + wl[h]];
-          } else if (a.id_status[uint64_t(i) * a.K + k] == CYC_JOB_VALID) {
-            valid[h][k] = wv[h] == a.W - 1 ? lastmask : ~0ull;
-          }
-        }
-        acc[h][k] = allow_all ? ~0ull : 0ull;
-      }
-    }
-    const bool second = cc[1] < cend;
-    for (uint32_t x0 = 0; x0 < (allow_all ? 0u : m); x0 += 64) {
-      PlLane g = g0;
-      if (x0 >= PL_LDS) g = pl_lane(a, spill, x0 + lane, m);
-      else if (x0) g = pl_lane(a, sh.e, x0 + lane, m);
-      uint64_t todo0 = __ballot((g.cm >> cc[0]) & 1ull);
-      uint64_t todo1 = second ? __ballot((g.cm >> cc[1]) & 1ull) : 0ull;
-      while (todo0 | todo1) {
-        uint32_t bits[PL_WBATCH], hh[PL_WBATCH];
-        uint64_t v[PL_WBATCH];
-#pragma unroll
-        for (uint32_t u = 0; u < PL_WBATCH; u++) {
-          bits[u] = 0;
-          v[u] = 0;
-          hh[u] = 0;
-          if (todo0 | todo1) {
-            const uint32_t h = todo0 ? 0u : 1u;  // wave-uniform
-            uint64_t& t = h ? todo1 : todo0;
-            const uint32_t src = __ffsll((unsigned long long)t) - 1;
-            t &= t - 1;
-            const uint32_t row = __builtin_amdgcn_readlane(g.row, src);
-            bits[u] = __builtin_amdgcn_readlane(g.bits, src);
-            hh[u] = h;
-            v[u] = row == PL_ONES ? ~0ull : a.PM[uint64_t(row) * a.W + (h ? wl[1] : wl[0])];
-          }
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < PL_WBATCH; u++)
-#pragma unroll
-          for (uint32_t d = 0; d < PL_NB; d++)
-            if ((bits[u] >> d) & 1u) {
-              if (hh[u]) acc[1][d] |= v[u];
-              else acc[0][d] |= v[u];
-            }
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      if (!live[h]) continue;
-#pragma unroll
-      for (uint32_t k = 0; k < PL_NB; k++) {
-        if (k >= a.K) break;
-        uint64_t r = 0;
-        if (!EGRESS) r = acc[h][k] & valid[h][k];
-        else if (du[h][k] >= 0) {
-#pragma unroll
-          for (uint32_t d = 0; d < PL_NB; d++) r = uint32_t(du[h][k]) == d ? acc[h][d] : r;
-          r &= valid[h][k];
-        } else if (du[h][k] == -1) {  // destinations with mixed job descriptors (rare)
-          const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + wv[h];
-#pragma unroll
-          for (uint32_t d = 0; d < PL_NB; d++)
-            if (d < a.D) r |= acc[h][d] & dm[uint64_t(d) * a.W];
-          r &= valid[h][k];
-        }
-        a.A[(arow_of(a, i) * a.K + k) * a.WA + (wv[h] - w0)] = r;
-      }
-    }
-  }
-}
-
 template <bool EGRESS, bool WAVE>
 __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
@@ -2157,9 +2078,7 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     // the class's (slot chunk, word) items, PL_ITEMS per thread at once (their loads overlap)
     uint32_t w0, wa;
     rep_window(a, i, w0, wa);
-    if (WAVE && CYC_PL_PAIR) {
-      pl_wave_chunk_pairs<EGRESS>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
-    } else if (WAVE && EGRESS && a.udesc) {
+    if (WAVE && EGRESS && a.udesc) {
       pl_wave_chunks<EGRESS, true>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
     } else if (WAVE) {
       pl_wave_chunks<EGRESS>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
@@ -2510,6 +2429,7 @@ struct FrontB {
   const uint32_t* plist[2];
   uint32_t pw0[2], pnw[2];  // per-pod pod-peer rows: word window per segment
   const uint32_t* pod_eid;
+  const DWordNS* nsw;  // per 64-pod word: namespace range (direct pod-peer rows)
   uint32_t M, D;
   const uint8_t* portok;
   uint32_t* portbits;
@@ -2547,7 +2467,7 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
     if (b < f.nb[2 + x]) {
       if (f.pod_direct)
         return pod_rows_direct_blk<false>(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls,
-                                          f.id_ls, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
+                                          f.id_ls, f.nsw, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
       return peer_bits_blk(f.Ru_[x], f.E, f.EW, f.pod_peers_u_[x], f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob_[x], b,
                            f.nb[2 + x], f.ew0[x], f.new_[x]);
     }
@@ -4112,11 +4032,13 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
     if (pb.may_err)
       k_pod_rows_direct<true><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
                                                  c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(),
-                                                 c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
+                                                 c->dir[1].id_ls.as<uint32_t>(), c->ns_words.as<DWordNS>(), c->PM.as<uint64_t>(),
+                                                 c->ER.as<uint64_t>(), w0, nw);
     else
       k_pod_rows_direct<false><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
                                                   c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(),
-                                                  c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
+                                                  c->dir[1].id_ls.as<uint32_t>(), c->ns_words.as<DWordNS>(), c->PM.as<uint64_t>(),
+                                                  c->ER.as<uint64_t>(), w0, nw);
   } else if (Rp && E && nw) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
     uint8_t* ido = c->ido.as<uint8_t>() + uint64_t(r0) * E;
@@ -4509,6 +4431,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (!ido && !pod_sparse(c)) {  // PM builds, few pod-peer words: full rows, a wave per (pod peer, word)
     fb.pod_direct = 1;
     fb.pod_eid = c->dir[1].pod_id.as<uint32_t>();
+    fb.nsw = c->ns_words.as<DWordNS>();
     for (int x = 0; x < 2; x++) {
       const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
       fb.Rp[x] = one_win && x ? 0u : c->rp_off[dhi] - c->rp_off[dlo];
