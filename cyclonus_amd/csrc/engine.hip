@@ -372,32 +372,16 @@ __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uin
                                                          const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres,
                                                          uint32_t L, const uint32_t* __restrict__ pod_eid,
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
-                                                         const uint32_t* __restrict__ id_ls, const DWordNS* __restrict__ nsw,
-                                                         uint64_t* __restrict__ PM, uint64_t* __restrict__ ER, uint32_t bid_,
-                                                         uint32_t nblk_, uint32_t w0, uint32_t nw) {
+                                                         const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
+                                                         uint64_t* __restrict__ ER, uint32_t bid_, uint32_t nblk_, uint32_t w0,
+                                                         uint32_t nw) {
   const uint32_t lane = threadIdx.x & 63, gw = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6));  // wave-uniform
   const uint32_t p = gw / nw, w = w0 + (gw - p * nw);
   if (p >= Rp) return;
   const uint32_t j = pod_peers[p];
   const DPeer pr = peers[j];
-  // the namespace matcher first (podpeermatcher.go:21-28), on the word's namespace record: an exact
-  // namespace outside the word's namespace range, or a namespace selector that rejects the word's
-  // only namespace, rejects every pod of the word before its pod matcher runs (no panic possible
-  // either) — a zero word, without the pods' identity and selector loads (config #2: most words)
-  // (the pods' identity loads are issued first, with the record's: a word that is not skipped
-  // pays no extra round trip)
   const uint32_t q = w * 64 + lane;
   const uint32_t e = pod_eid[min(q, P - 1)];  // (clamped: no load inside a branch)
-  const DWordNS wn = nsw[w];
-  const uint8_t rns = selres[pr.nskind == 2 && wn.lo == wn.hi ? uint64_t(pr.nsval) * L + wn.nsls : 0u];
-  const bool none = pr.nskind == 0 ? (pr.nsval < wn.lo || pr.nsval > wn.hi) : (pr.nskind == 2 && wn.lo == wn.hi && rns == 0);
-  if (none) {
-    if (lane == 0) {
-      PM[uint64_t(j) * W + w] = 0;
-      if (ERR) ER[uint64_t(j) * W + w] = 0;
-    }
-    return;
-  }
   uint32_t o = pod_peer_outcome(pr, selres, L, id_ns[e], id_nsls[e], id_ls[e]);
   if (q >= P) o = 0;
   const uint64_t m = __ballot(o == 1);
@@ -413,9 +397,9 @@ __global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P
                                                          const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres,
                                                          uint32_t L, const uint32_t* __restrict__ pod_eid,
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
-                                                         const uint32_t* __restrict__ id_ls, const DWordNS* __restrict__ nsw,
-                                                         uint64_t* __restrict__ PM, uint64_t* __restrict__ ER, uint32_t w0, uint32_t nw) {
-  pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, nsw, PM, ER, blockIdx.x, gridDim.x, w0, nw);
+                                                         const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
+                                                         uint64_t* __restrict__ ER, uint32_t w0, uint32_t nw) {
+  pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, PM, ER, blockIdx.x, gridDim.x, w0, nw);
 }
 
 // Pod-peer rows of the fused front on PM builds (no panic possible), stored sparse, 64-word chunks
@@ -2429,7 +2413,6 @@ struct FrontB {
   const uint32_t* plist[2];
   uint32_t pw0[2], pnw[2];  // per-pod pod-peer rows: word window per segment
   const uint32_t* pod_eid;
-  const DWordNS* nsw;  // per 64-pod word: namespace range (direct pod-peer rows)
   uint32_t M, D;
   const uint8_t* portok;
   uint32_t* portbits;
@@ -2467,7 +2450,7 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
     if (b < f.nb[2 + x]) {
       if (f.pod_direct)
         return pod_rows_direct_blk<false>(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls,
-                                          f.id_ls, f.nsw, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
+                                          f.id_ls, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
       return peer_bits_blk(f.Ru_[x], f.E, f.EW, f.pod_peers_u_[x], f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob_[x], b,
                            f.nb[2 + x], f.ew0[x], f.new_[x]);
     }
@@ -2665,6 +2648,14 @@ __device__ __forceinline__ void emit_status(const EmitArgs& a) {
 }
 
 
+#ifndef CYC_EMIT_NT
+#define CYC_EMIT_NT 1  // non-temporal plane stores (0: plain)
+#endif
+__device__ __forceinline__ void emit_store(u64x2 v, u64x2* p) {
+  if (CYC_EMIT_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // Rows of an odd word count or planes not 16-byte aligned: 8-byte copies, one block per row.
 __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
   emit_status(a);
@@ -2728,7 +2719,7 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++)
-      if (i0 + u * 256 < tot) __builtin_nontemporal_store(v[u], &s_dst[row[u]][col[u]]);
+      if (i0 + u * 256 < tot) emit_store(v[u], &s_dst[row[u]][col[u]]);
   }
 }
 
@@ -2755,7 +2746,59 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
       if (x0 + u * BS < n2) v[u] = si[x0 + u * BS];
 #pragma unroll
     for (int u = 0; u < UNROLL; u++)
-      if (x0 + u * BS < n2) __builtin_nontemporal_store(v[u], &di[x0 + u * BS]);
+      if (x0 + u * BS < n2) emit_store(v[u], &di[x0 + u * BS]);
+  }
+}
+
+// Groups of G rows of one plane per block (rows class-clustered, so consecutive rows of a plane
+// mostly share their class row): the class row is loaded into registers once per group and stored to
+// each of its rows, so the block's store stream is G rows long and the L2 reads of class rows fall
+// G-fold.  The group list: per plane ceil(n_rows / G) groups (interleaved planes: alternating
+// groups), cut into 8 XCD segments as the row list is.  Lanes 0..G-1 resolve the group's rows'
+// source / destination first, all at once.
+__host__ __device__ inline uint32_t emit_groups(const EmitArgs& a, uint32_t G) {
+  return a.interleave ? 2 * ((a.n_rows[0] + G - 1) / G) : (a.n_rows[0] + a.n_rows[1] + G - 1) / G;
+}
+template <int BS, int UNROLL, int G>
+__global__ __launch_bounds__(BS) void k_emit_group(EmitArgs a) {
+  emit_status(a);
+  const uint32_t b = blockIdx.x, x = b & 7, ng = emit_groups(a, G);
+  const uint32_t gi = x * a.per_xcd + (b >> 3);  // per_xcd counts groups here
+  if (gi >= min(ng, (x + 1) * a.per_xcd)) return;
+  const uint32_t lane = threadIdx.x & 63, n = a.n_rows[0] + a.n_rows[1];
+  uint64_t sp = 0, dp = 0;  // lane g < G: row g of the group (0: past the list / in place)
+  if (lane < G) {
+    uint32_t r = a.interleave ? 2 * ((gi >> 1) * G + lane) + (gi & 1) : gi * G + lane;
+    if (r < n) {
+      uint32_t pl, p;
+      emit_row_of(a, r, pl, p);
+      sp = reinterpret_cast<uint64_t>(emit_src(a, pl, p));
+      dp = reinterpret_cast<uint64_t>(a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.row_words);
+    }
+  }
+  const uint32_t n2 = uint32_t(a.row_words / 2);
+  u64x2 v[UNROLL];
+  uint64_t cur = 0;
+  for (int g = 0; g < G; g++) {
+    const uint64_t sg = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(sp >> 32), g))) << 32) |
+                        uint32_t(__builtin_amdgcn_readlane(int(uint32_t(sp)), g));
+    const uint64_t dg = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(dp >> 32), g))) << 32) |
+                        uint32_t(__builtin_amdgcn_readlane(int(uint32_t(dp)), g));
+    if (!dg) break;       // past the row list
+    if (!sg) continue;    // in-place class row: already written
+    const u64x2* si = reinterpret_cast<const u64x2*>(sg);
+    u64x2* di = reinterpret_cast<u64x2*>(dg);
+    for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS * UNROLL) {
+      if (sg != cur || n2 > BS * UNROLL) {  // a new class row (or rows longer than one pass)
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++)
+          if (x0 + u * BS < n2) v[u] = si[x0 + u * BS];
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++)
+        if (x0 + u * BS < n2) emit_store(v[u], &di[x0 + u * BS]);
+    }
+    cur = sg;
   }
 }
 
@@ -4032,13 +4075,11 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
     if (pb.may_err)
       k_pod_rows_direct<true><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
                                                  c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(),
-                                                 c->dir[1].id_ls.as<uint32_t>(), c->ns_words.as<DWordNS>(), c->PM.as<uint64_t>(),
-                                                 c->ER.as<uint64_t>(), w0, nw);
+                                                 c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
     else
       k_pod_rows_direct<false><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
                                                   c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(),
-                                                  c->dir[1].id_ls.as<uint32_t>(), c->ns_words.as<DWordNS>(), c->PM.as<uint64_t>(),
-                                                  c->ER.as<uint64_t>(), w0, nw);
+                                                  c->dir[1].id_ls.as<uint32_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
   } else if (Rp && E && nw) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
     uint8_t* ido = c->ido.as<uint8_t>() + uint64_t(r0) * E;
@@ -4213,6 +4254,9 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // shard's word window, egress rows of its sources over all words).  d_status (may be null): the
 // status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
 // in the plan; the caller then copies the status plane itself).
+#ifndef CYC_EMIT_GROUP
+#define CYC_EMIT_GROUP 0  // rows per block of the grouped emit (k_emit_group); 0: a block per row (k_emit_wide)
+#endif
 #ifndef CYC_EMIT_WIDE_MIN
 #define CYC_EMIT_WIDE_MIN 16384  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
 #endif
@@ -4226,6 +4270,24 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
+  if (row_bytes >= 16384 && CYC_EMIT_GROUP && !(ea.interleave && ea.n_rows[0] != ea.n_rows[1])) {
+    // groups of CYC_EMIT_GROUP rows per block, the class row held in registers (k_emit_group)
+    constexpr int G = CYC_EMIT_GROUP > 0 ? CYC_EMIT_GROUP : 1;
+    ea.per_xcd = (emit_groups(ea, G) + 7) / 8;
+    const unsigned gg = ea.per_xcd * 8;
+    if (row_bytes >= 65536) {
+      const uint64_t need = (ea.row_words / 2 + 511) / 512;
+      if (need <= 8) k_emit_group<512, 8, G><<<gg, 512, 0, st>>>(ea);
+      else if (need <= 13) k_emit_group<512, 13, G><<<gg, 512, 0, st>>>(ea);
+      else k_emit_group<512, 16, G><<<gg, 512, 0, st>>>(ea);
+    } else {
+      const uint64_t need = (ea.row_words / 2 + 255) / 256;
+      if (need <= 4) k_emit_group<256, 4, G><<<gg, 256, 0, st>>>(ea);
+      else if (need <= 8) k_emit_group<256, 8, G><<<gg, 256, 0, st>>>(ea);
+      else k_emit_group<256, 16, G><<<gg, 256, 0, st>>>(ea);
+    }
+    return;
+  }
   if (row_bytes >= 65536) {  // 512-thread single pass: smallest UNROLL covering the row (16 = two passes)
     const uint64_t need = (ea.row_words / 2 + 511) / 512;
     if (need <= 8) k_emit_wide<512, 8><<<g, 512, 0, st>>>(ea);
@@ -4431,7 +4493,6 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (!ido && !pod_sparse(c)) {  // PM builds, few pod-peer words: full rows, a wave per (pod peer, word)
     fb.pod_direct = 1;
     fb.pod_eid = c->dir[1].pod_id.as<uint32_t>();
-    fb.nsw = c->ns_words.as<DWordNS>();
     for (int x = 0; x < 2; x++) {
       const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
       fb.Rp[x] = one_win && x ? 0u : c->rp_off[dhi] - c->rp_off[dlo];

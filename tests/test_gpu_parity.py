@@ -341,6 +341,46 @@ def test_ip_interval_words(gpu, seed):
     assert_same(o, g, f"ip intervals seed {seed}")
 
 
+def _shared_ipblock_problem(seed, bad=False):
+    """Policies whose peers reuse a small pool of IPBlocks (equal cidr / except strings) on different
+    ports and in both directions: the run plan builds ONE IP row per IPBlock and direction, and every
+    peer (class rows, identity-set lists, the panic describer) reads it through peer_row.  bad: the
+    pool also holds an unparsable CIDR (ipaddress.go panics when a cell reaches it)."""
+    pols, res, probes = _ip_interval_problem(seed)
+    rng = np.random.default_rng(seed + 100)
+    pool = [p["ipBlock"] for pol in pols for p in pol["spec"]["ingress"][0]["from"]][:5]
+    pool.append({"cidr": "0.0.0.0/0"})
+    if bad:
+        pool.append({"cidr": "10.0.0.0/33"})
+    ports = [[{"port": 80, "protocol": "TCP"}], [{"port": 81, "protocol": "TCP"}], [{"port": "serve-80-tcp"}], None]
+    for i in range(10):
+        blocks = [pool[int(x)] for x in rng.integers(0, len(pool), 3)]
+        ing = {"from": [{"ipBlock": b} for b in blocks]}
+        eg = {"to": [{"ipBlock": b} for b in blocks[::-1]]}
+        pp = ports[i % len(ports)]
+        if pp:
+            ing["ports"] = pp
+            eg["ports"] = pp
+        spec = {"podSelector": {"matchLabels": {"i": str(i % 7)}}, "policyTypes": ["Ingress", "Egress"],
+                "ingress": [ing], "egress": [eg]}
+        pols.append({"metadata": {"name": f"shared{i}", "namespace": "x"}, "spec": spec})
+    return pols, res, probes
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_shared_ipblock_rows(gpu, seed):
+    for bad in (False, True):
+        pols, res, probes = _shared_ipblock_problem(seed, bad)
+        o, g = run_both(pols, res, probes)
+        assert_same(o, g, f"shared IPBlocks seed {seed} bad {bad}")
+        for opts in ({"front_fused": 0}, {"pod_words": 0}, {"pl_wave": 0}, {"graphs": 0}):
+            eng = Engine(0)
+            for k, v in opts.items():
+                eng.set_option(k, v)
+            o2, g2 = run_both(pols, res, probes, engine=eng)
+            assert_same(o2, g2, f"shared IPBlocks seed {seed} bad {bad} {opts}")
+
+
 def test_pm_class_rows_wave_and_items(gpu):
     """PM-build class rows (pod_words = 0) a wave per 64-word chunk (pl_wave = 1: <= 4 slots and
     descriptors) and a thread per item (pl_wave = 0), over sparse pod-peer rows built by either block
