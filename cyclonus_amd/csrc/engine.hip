@@ -2648,13 +2648,9 @@ __device__ __forceinline__ void emit_status(const EmitArgs& a) {
 }
 
 
-#ifndef CYC_EMIT_NT
-#define CYC_EMIT_NT 1  // non-temporal plane stores (0: plain)
-#endif
-__device__ __forceinline__ void emit_store(u64x2 v, u64x2* p) {
-  if (CYC_EMIT_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
+// Plane stores are non-temporal: they do not displace the class rows the emit re-reads from L2
+// (plain stores: config #4 emit +45 %, profiles/r03_emit_ab.txt).
+__device__ __forceinline__ void emit_store(u64x2 v, u64x2* p) { __builtin_nontemporal_store(v, p); }
 
 // Rows of an odd word count or planes not 16-byte aligned: 8-byte copies, one block per row.
 __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
@@ -2747,58 +2743,6 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
 #pragma unroll
     for (int u = 0; u < UNROLL; u++)
       if (x0 + u * BS < n2) emit_store(v[u], &di[x0 + u * BS]);
-  }
-}
-
-// Groups of G rows of one plane per block (rows class-clustered, so consecutive rows of a plane
-// mostly share their class row): the class row is loaded into registers once per group and stored to
-// each of its rows, so the block's store stream is G rows long and the L2 reads of class rows fall
-// G-fold.  The group list: per plane ceil(n_rows / G) groups (interleaved planes: alternating
-// groups), cut into 8 XCD segments as the row list is.  Lanes 0..G-1 resolve the group's rows'
-// source / destination first, all at once.
-__host__ __device__ inline uint32_t emit_groups(const EmitArgs& a, uint32_t G) {
-  return a.interleave ? 2 * ((a.n_rows[0] + G - 1) / G) : (a.n_rows[0] + a.n_rows[1] + G - 1) / G;
-}
-template <int BS, int UNROLL, int G>
-__global__ __launch_bounds__(BS) void k_emit_group(EmitArgs a) {
-  emit_status(a);
-  const uint32_t b = blockIdx.x, x = b & 7, ng = emit_groups(a, G);
-  const uint32_t gi = x * a.per_xcd + (b >> 3);  // per_xcd counts groups here
-  if (gi >= min(ng, (x + 1) * a.per_xcd)) return;
-  const uint32_t lane = threadIdx.x & 63, n = a.n_rows[0] + a.n_rows[1];
-  uint64_t sp = 0, dp = 0;  // lane g < G: row g of the group (0: past the list / in place)
-  if (lane < G) {
-    uint32_t r = a.interleave ? 2 * ((gi >> 1) * G + lane) + (gi & 1) : gi * G + lane;
-    if (r < n) {
-      uint32_t pl, p;
-      emit_row_of(a, r, pl, p);
-      sp = reinterpret_cast<uint64_t>(emit_src(a, pl, p));
-      dp = reinterpret_cast<uint64_t>(a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.row_words);
-    }
-  }
-  const uint32_t n2 = uint32_t(a.row_words / 2);
-  u64x2 v[UNROLL];
-  uint64_t cur = 0;
-  for (int g = 0; g < G; g++) {
-    const uint64_t sg = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(sp >> 32), g))) << 32) |
-                        uint32_t(__builtin_amdgcn_readlane(int(uint32_t(sp)), g));
-    const uint64_t dg = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(dp >> 32), g))) << 32) |
-                        uint32_t(__builtin_amdgcn_readlane(int(uint32_t(dp)), g));
-    if (!dg) break;       // past the row list
-    if (!sg) continue;    // in-place class row: already written
-    const u64x2* si = reinterpret_cast<const u64x2*>(sg);
-    u64x2* di = reinterpret_cast<u64x2*>(dg);
-    for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS * UNROLL) {
-      if (sg != cur || n2 > BS * UNROLL) {  // a new class row (or rows longer than one pass)
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++)
-          if (x0 + u * BS < n2) v[u] = si[x0 + u * BS];
-      }
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++)
-        if (x0 + u * BS < n2) emit_store(v[u], &di[x0 + u * BS]);
-    }
-    cur = sg;
   }
 }
 
@@ -4254,9 +4198,6 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // shard's word window, egress rows of its sources over all words).  d_status (may be null): the
 // status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
 // in the plan; the caller then copies the status plane itself).
-#ifndef CYC_EMIT_GROUP
-#define CYC_EMIT_GROUP 0  // rows per block of the grouped emit (k_emit_group); 0: a block per row (k_emit_wide)
-#endif
 #ifndef CYC_EMIT_WIDE_MIN
 #define CYC_EMIT_WIDE_MIN 16384  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
 #endif
@@ -4270,24 +4211,6 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
-  if (row_bytes >= 16384 && CYC_EMIT_GROUP && !(ea.interleave && ea.n_rows[0] != ea.n_rows[1])) {
-    // groups of CYC_EMIT_GROUP rows per block, the class row held in registers (k_emit_group)
-    constexpr int G = CYC_EMIT_GROUP > 0 ? CYC_EMIT_GROUP : 1;
-    ea.per_xcd = (emit_groups(ea, G) + 7) / 8;
-    const unsigned gg = ea.per_xcd * 8;
-    if (row_bytes >= 65536) {
-      const uint64_t need = (ea.row_words / 2 + 511) / 512;
-      if (need <= 8) k_emit_group<512, 8, G><<<gg, 512, 0, st>>>(ea);
-      else if (need <= 13) k_emit_group<512, 13, G><<<gg, 512, 0, st>>>(ea);
-      else k_emit_group<512, 16, G><<<gg, 512, 0, st>>>(ea);
-    } else {
-      const uint64_t need = (ea.row_words / 2 + 255) / 256;
-      if (need <= 4) k_emit_group<256, 4, G><<<gg, 256, 0, st>>>(ea);
-      else if (need <= 8) k_emit_group<256, 8, G><<<gg, 256, 0, st>>>(ea);
-      else k_emit_group<256, 16, G><<<gg, 256, 0, st>>>(ea);
-    }
-    return;
-  }
   if (row_bytes >= 65536) {  // 512-thread single pass: smallest UNROLL covering the row (16 = two passes)
     const uint64_t need = (ea.row_words / 2 + 511) / 512;
     if (need <= 8) k_emit_wide<512, 8><<<g, 512, 0, st>>>(ea);
