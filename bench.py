@@ -188,8 +188,14 @@ def main():
         ri, wi, re_, we, w0 = lays[rank]
         max_in = max(x[0] * x[1] for x in lays)
         max_eg = max(x[2] * x[3] for x in lays)
-        d_in = torch.empty((max(max_in, 1) * K,), dtype=torch.int64, device="cuda")
-        d_eg = torch.empty((max(max_eg, 1) * K,), dtype=torch.int64, device="cuda")
+        if os.environ.get("CYC_BENCH_ONE_BUFFER"):  # both planes carved from one allocation (layout A/B)
+            n_in, n_eg = max(max_in, 1) * K, max(max_eg, 1) * K
+            pad = int(os.environ.get("CYC_BENCH_PLANE_GAP", "0")) // 8
+            planes = torch.empty((n_in + pad + n_eg,), dtype=torch.int64, device="cuda")
+            d_in, d_eg = planes[:n_in], planes[n_in + pad:]
+        else:
+            d_in = torch.empty((max(max_in, 1) * K,), dtype=torch.int64, device="cuda")
+            d_eg = torch.empty((max(max_eg, 1) * K,), dtype=torch.int64, device="cuda")
         d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
 
         def step():

@@ -2111,16 +2111,28 @@ template <uint32_t N>
 __device__ __forceinline__ void ido_ip_loads(const RowArgs& a, const uint4* sl, uint32_t x0, uint32_t ms, uint32_t w,
                                              uint64_t (&pm)[N], uint32_t (&pbits)[N]) {
   const uint32_t cw = (a.W + 63) / 64;
+  uint4 e[N];
+  bool ok[N];
+  bool any = false;
+#pragma unroll
+  for (uint32_t u = 0; u < N; u++) {
+    e[u] = sl[min(x0 + u, IDO_IPL - 1)];
+    const bool in = x0 + u < ms;
+    ok[u] = in && w >= e[u].y && w <= e[u].z;
+    pbits[u] = in ? e[u].w : 0u;
+    pm[u] = 0;
+    any |= ok[u];
+  }
+  // most (representative, 256-word chunk) pairs lie outside every staged peer's nonzero word span
+  // (a CIDR covers a few namespaces' pods): then the wave issues no load and waits for none
+  // (config #3 class rows -6 us: profiles/r03_bench_variance_ipskip.txt)
+  if (!__ballot(any)) return;
   uint64_t v[N];
   uint32_t cm[N];
 #pragma unroll
   for (uint32_t u = 0; u < N; u++) {
-    const uint4 e = sl[min(x0 + u, IDO_IPL - 1)];
-    const bool in = x0 + u < ms;
-    const bool ok = in && w >= e.y && w <= e.z;
-    pbits[u] = in ? e.w : 0u;
-    v[u] = *(ok ? a.PM + uint64_t(e.x) * a.W + w : a.zero);
-    cm[u] = *(ok ? a.ip_cnz + uint64_t(e.x) * cw + w / 64 : reinterpret_cast<const uint32_t*>(a.zero));
+    v[u] = *(ok[u] ? a.PM + uint64_t(e[u].x) * a.W + w : a.zero);
+    cm[u] = *(ok[u] ? a.ip_cnz + uint64_t(e[u].x) * cw + w / 64 : reinterpret_cast<const uint32_t*>(a.zero));
   }
 #pragma unroll
   for (uint32_t u = 0; u < N; u++) pm[u] = cm[u] ? v[u] : 0ull;

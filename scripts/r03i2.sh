@@ -1,0 +1,8 @@
+set -e
+OUT=gpurun_out/r03i2; mkdir -p $OUT
+timeout -k 10 120 ./scripts/wbw 20 > $OUT/wbw.txt 2>&1
+for i in 1 2; do
+timeout -k 10 300 python -u bench.py --config config3 --no-cpu-baseline --steps 30 --warmup 10 > $OUT/bench_default_$i.log 2>&1
+CYC_BENCH_ONE_BUFFER=1 timeout -k 10 300 python -u bench.py --config config3 --no-cpu-baseline --steps 30 --warmup 10 > $OUT/bench_one_$i.log 2>&1
+CYC_BENCH_ONE_BUFFER=1 CYC_BENCH_PLANE_GAP=4096 timeout -k 10 300 python -u bench.py --config config3 --no-cpu-baseline --steps 30 --warmup 10 > $OUT/bench_onegap_$i.log 2>&1
+done

@@ -50,6 +50,23 @@ __global__ __launch_bounds__(BS) void k_rows(u64x2* p, size_t rows, size_t row16
   }
 }
 
+
+// the emit's two-plane row list: row r of the list -> plane r & 1 (interleaved) or r >= rows (plane-major),
+// plane row r >> 1 / r - rows; the list cut into 8 XCD segments
+template <int BS, int UNROLL>
+__global__ __launch_bounds__(BS) void k_rows2(u64x2* pa, u64x2* pb, size_t rows, size_t row16, size_t per_xcd, int inter) {
+  const size_t b = blockIdx.x, x = b & 7, r = x * per_xcd + (b >> 3);
+  if (r >= 2 * rows || r >= (x + 1) * per_xcd) return;
+  const size_t pl = inter ? (r & 1) : (r >= rows), pr = inter ? (r >> 1) : (r >= rows ? r - rows : r);
+  u64x2* d = (pl ? pb : pa) + pr * row16;
+  const u64x2 v = {0x5555555555555555ull, 0xAAAAAAAAAAAAAAAAull};
+  for (size_t x0 = threadIdx.x; x0 < row16; x0 += BS * UNROLL) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++)
+      if (x0 + u * BS < row16) __builtin_nontemporal_store(v, d + x0 + u * BS);
+  }
+}
+
 template <class F>
 static double time_ms(F f, int reps) {
   hipEvent_t a, b;
@@ -95,6 +112,20 @@ int main(int argc, char** argv) {
     report(nm, time_ms([&] { k_rows<512, 13, false><<<unsigned(per * 8), 512>>>(p, rows, row16, per); }, reps));
   }
   report("hipMemsetAsync", time_ms([&] { CHK(hipMemsetAsync(p, 0x5A, bytes)); }, reps));
-  CHK(hipFree(p));
+  {  // two planes of 100,032 B rows, as the emit writes them (config #3: 2 x 100,000 rows)
+    const size_t row = 100032, row16 = row / 16, rows = bytes / 2 / row, per = (2 * rows + 7) / 8;
+    u64x2* pa = p;
+    u64x2* pb = p + rows * row16;  // one allocation, planes back to back
+    report("2 planes, one buffer, interleaved rows", time_ms([&] { k_rows2<512, 13><<<unsigned(per * 8), 512>>>(pa, pb, rows, row16, per, 1); }, reps));
+    report("2 planes, one buffer, plane-major", time_ms([&] { k_rows2<512, 13><<<unsigned(per * 8), 512>>>(pa, pb, rows, row16, per, 0); }, reps));
+    CHK(hipFree(p));
+    u64x2 *qa, *qb;
+    CHK(hipMalloc(&qa, rows * row));
+    CHK(hipMalloc(&qb, rows * row));
+    report("2 planes, two buffers, interleaved rows", time_ms([&] { k_rows2<512, 13><<<unsigned(per * 8), 512>>>(qa, qb, rows, row16, per, 1); }, reps));
+    report("2 planes, two buffers, plane-major", time_ms([&] { k_rows2<512, 13><<<unsigned(per * 8), 512>>>(qa, qb, rows, row16, per, 0); }, reps));
+    CHK(hipFree(qa));
+    CHK(hipFree(qb));
+  }
   return 0;
 }
