@@ -2735,8 +2735,11 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
 // of BS x UNROLL 16-byte chunks covers the row (config #3: 100 KB rows, 512 x 13 x 16 B; config #4:
 // 25 KB rows, 256 x 7 x 16 B): every lane's loads are in flight before its stores and no second,
 // partly idle pass follows (profiles/r01_emit_wide_sweep.txt, r01_emit_medium_rows_ab.txt).
+#ifndef CYC_EMIT_WAVES
+#define CYC_EMIT_WAVES
+#endif
 template <int BS, int UNROLL>
-__global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
+__global__ __launch_bounds__(BS) CYC_EMIT_WAVES void k_emit_wide(EmitArgs a) {
   emit_status(a);
   const uint32_t b = blockIdx.x, n = a.n_rows[0] + a.n_rows[1], x = b & 7;
   const uint32_t r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
@@ -4210,6 +4213,9 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // shard's word window, egress rows of its sources over all words).  d_status (may be null): the
 // status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
 // in the plan; the caller then copies the status plane itself).
+#ifndef CYC_EMIT_CFG
+#define CYC_EMIT_CFG 0  // rows >= 64 KB: 0 = 512 threads one pass, 1 = 1024 x 7, 2 = 512 x 7 (A/B)
+#endif
 #ifndef CYC_EMIT_WIDE_MIN
 #define CYC_EMIT_WIDE_MIN 16384  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
 #endif
@@ -4223,7 +4229,11 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
-  if (row_bytes >= 65536) {  // 512-thread single pass: smallest UNROLL covering the row (16 = two passes)
+  if (row_bytes >= 65536 && CYC_EMIT_CFG == 1) {  // 1024-thread blocks, 7 chunks a thread (A/B)
+    k_emit_wide<1024, 7><<<g, 1024, 0, st>>>(ea);
+  } else if (row_bytes >= 65536 && CYC_EMIT_CFG == 2) {  // 512-thread blocks, 7 chunks a thread per pass (A/B)
+    k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
+  } else if (row_bytes >= 65536) {  // 512-thread single pass: smallest UNROLL covering the row (16 = two passes)
     const uint64_t need = (ea.row_words / 2 + 511) / 512;
     if (need <= 8) k_emit_wide<512, 8><<<g, 512, 0, st>>>(ea);
     else if (need <= 10) k_emit_wide<512, 10><<<g, 512, 0, st>>>(ea);
