@@ -348,8 +348,9 @@ def main():
     def kernel_of(words):  # the emit kernel the library picks by plane-row length (engine.hip enq_emit_launch)
         row_bytes = K * words * 8
         return ("k_emit_words (8-byte copies)" if (K * words) % 2 else
-                "k_emit_wide<512,U> (one single-pass block per row)" if row_bytes >= 65536 else
-                "k_emit_wide<256,U> (one single-pass block per row)" if row_bytes >= 16384 else
+                "k_emit_wide<1024,7> (a block per row, 7 x 16 B a thread per pass)" if row_bytes > 512 * 7 * 16 else
+                "k_emit_wide<512,7> (a block per row, one pass)" if row_bytes > 256 * 8 * 16 else
+                "k_emit_wide<256,U> (a block per row, one pass)" if row_bytes >= 16384 else
                 "k_emit_flat (multi-row blocks)")
     emit_kernel = kernel_of(we) if launches == 1 else f"ingress {kernel_of(wi)}; egress {kernel_of(we)}"
     if bt is not None:

@@ -4214,7 +4214,10 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
 // in the plan; the caller then copies the status plane itself).
 #ifndef CYC_EMIT_CFG
-#define CYC_EMIT_CFG 0  // rows >= 64 KB: 0 = 512 threads one pass, 1 = 1024 x 7, 2 = 512 x 7 (A/B)
+// rows >= 64 KB: 1 = 1024-thread blocks, 7 16-byte chunks a thread per pass (48 VGPRs: 32 waves a CU);
+// 0 = 512 threads, one pass (84 VGPRs: 5 waves a SIMD, 20 a CU); 2 = 512 x 7.  Config #3 on one box:
+// 3.66 (1) vs 3.79 (0) vs 3.89 (2) ms per step (profiles/r03_emit_ab.txt)
+#define CYC_EMIT_CFG 1
 #endif
 #ifndef CYC_EMIT_WIDE_MIN
 #define CYC_EMIT_WIDE_MIN 16384  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
@@ -4229,8 +4232,12 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
-  if (row_bytes >= 65536 && CYC_EMIT_CFG == 1) {  // 1024-thread blocks, 7 chunks a thread (A/B)
+  // 16-byte chunks per thread and pass <= 8 keeps a block at <= 48 VGPRs (8 waves a SIMD): 84 VGPRs for
+  // 512 x 13 held 5 (config #3 +3.5 % per step, profiles/r03_emit_ab.txt)
+  if (row_bytes > 512 * 7 * 16 && CYC_EMIT_CFG == 1) {  // > 56 KB: 1024 x 7 (config #3: 98 KB rows, one pass)
     k_emit_wide<1024, 7><<<g, 1024, 0, st>>>(ea);
+  } else if (row_bytes > 256 * 8 * 16 && CYC_EMIT_CFG == 1) {  // 32-56 KB: 512 x 7 (source shards at N = 2)
+    k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
   } else if (row_bytes >= 65536 && CYC_EMIT_CFG == 2) {  // 512-thread blocks, 7 chunks a thread per pass (A/B)
     k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
   } else if (row_bytes >= 65536) {  // 512-thread single pass: smallest UNROLL covering the row (16 = two passes)
