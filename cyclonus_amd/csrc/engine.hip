@@ -2598,6 +2598,17 @@ constexpr int E_KC = CYC_E_KC;
                        // budget: egress 101 VGPRs, ingress 61) instead of k_front_e (both at 101): config #3
                        // 189 -> 170 us (profiles/r03_e_split_ab.txt)
 #endif
+#ifndef CYC_E_UNI_FUSED
+#define CYC_E_UNI_FUSED 1  // egress with one descriptor per slot: both directions' class rows in one launch (k_front_e_uni;
+                           // config #3 132 -> 124 us, profiles/r03_ido_rows_ab.txt)
+#endif
+// Launch E as one kernel when the egress rows take the one-descriptor-per-slot form (UNI): both
+// bodies then stay near 60 VGPRs, so the fused launch keeps their occupancy and saves a launch.
+__global__ __launch_bounds__(256) void k_front_e_uni(FrontRows f) {
+  const uint32_t b = blockIdx.x;
+  if (b < f.nb[1]) class_rows_ido_blk<true, E_KC, true>(f.ra[1], b, f.nb[1]);
+  else class_rows_ido_blk<false, E_KC>(f.ra[0], b - f.nb[1], f.nb[0]);
+}
 __global__ __launch_bounds__(256) CYC_E_WAVES void k_front_e(FrontRows f) {
   const uint32_t b = blockIdx.x;
   if (b < f.nb[1]) class_rows_ido_blk<true, E_KC>(f.ra[1], b, f.nb[1]);
@@ -4543,7 +4554,9 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     return true;
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
-  if (CYC_E_SPLIT) {  // the directions' class rows as two launches, each at its own register budget
+  if (CYC_E_UNI_FUSED && fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
+    k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);
+  } else if (CYC_E_SPLIT) {  // the directions' class rows as two launches, each at its own register budget
     if (fe.nb[1] && fe.ra[1].udesc) k_class_rows_ido<true, E_KC, true><<<fe.nb[1], 256, lds_uni, st>>>(fe.ra[1]);
     else if (fe.nb[1]) k_class_rows_ido<true, E_KC><<<fe.nb[1], 256, lds, st>>>(fe.ra[1]);
     if (fe.nb[0]) k_class_rows_ido<false, E_KC><<<fe.nb[0], 256, lds, st>>>(fe.ra[0]);
