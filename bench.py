@@ -123,7 +123,9 @@ def main():
     torch.cuda.set_device(device)
     backend = os.environ.get("CYC_BENCH_BACKEND", "nccl")  # "gloo" = CPU rehearsal of the N>1 flow
     dist = None
-    if world > 1:
+    # CYC_BENCH_FORCE_DIST=1: the process group even for one rank (exercises the RCCL barrier /
+    # max-reduce / all-gather path on a one-GPU box; two ranks cannot share one GPU under RCCL)
+    if world > 1 or os.environ.get("CYC_BENCH_FORCE_DIST"):
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
