@@ -366,6 +366,16 @@ struct DWordNS {
 // labelled apart, e.g. a `pod: <name>` label): then the identity-space outcomes cost as much as
 // this and the run expansion above loops over up to 64 runs per word.
 // Words [w0, w0 + nw) of each row (a source shard's ingress peers: its word window).
+#ifndef CYC_PR_DIRECT_G
+#define CYC_PR_DIRECT_G 4  // pod peers per wave of the direct pod-peer rows
+#endif
+constexpr uint32_t PR_DIRECT_G = CYC_PR_DIRECT_G;
+// Wave = (PR_DIRECT_G pod peers, one 64-pod word), lane = pod: the word's pod identities (pod ->
+// identity -> namespace, namespace labels, labels) are loaded once for the group, then every
+// peer's two matcher bytes at once, one ballot per peer.
+__host__ __device__ inline uint64_t pod_direct_waves(uint32_t Rp, uint32_t nw) {
+  return uint64_t((Rp + PR_DIRECT_G - 1) / PR_DIRECT_G) * nw;
+}
 template <bool ERR>
 __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uint32_t W,
                                                          const uint32_t* __restrict__ pod_peers,
@@ -376,19 +386,31 @@ __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uin
                                                          uint64_t* __restrict__ ER, uint32_t bid_, uint32_t nblk_, uint32_t w0,
                                                          uint32_t nw) {
   const uint32_t lane = threadIdx.x & 63, gw = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6));  // wave-uniform
-  const uint32_t p = gw / nw, w = w0 + (gw - p * nw);
-  if (p >= Rp) return;
-  const uint32_t j = pod_peers[p];
-  const DPeer pr = peers[j];
+  const uint32_t g = gw / nw, w = w0 + (gw - g * nw), p0 = g * PR_DIRECT_G;
+  if (p0 >= Rp) return;
+  uint32_t j[PR_DIRECT_G];
+  DPeer pr[PR_DIRECT_G];
+#pragma unroll
+  for (uint32_t u = 0; u < PR_DIRECT_G; u++) {
+    j[u] = pod_peers[min(p0 + u, Rp - 1)];
+    pr[u] = peers[j[u]];
+  }
   const uint32_t q = w * 64 + lane;
   const uint32_t e = pod_eid[min(q, P - 1)];  // (clamped: no load inside a branch)
-  uint32_t o = pod_peer_outcome(pr, selres, L, id_ns[e], id_nsls[e], id_ls[e]);
-  if (q >= P) o = 0;
-  const uint64_t m = __ballot(o == 1);
-  const uint64_t er = ERR ? __ballot(o == 2) : 0ull;
-  if (lane == 0) {
-    PM[uint64_t(j) * W + w] = m;
-    if (ERR) ER[uint64_t(j) * W + w] = er;
+  const uint32_t ns = id_ns[e], nsls = id_nsls[e], ls = id_ls[e];
+  uint32_t o[PR_DIRECT_G];
+#pragma unroll
+  for (uint32_t u = 0; u < PR_DIRECT_G; u++) o[u] = pod_peer_outcome(pr[u], selres, L, ns, nsls, ls);
+#pragma unroll
+  for (uint32_t u = 0; u < PR_DIRECT_G; u++) {
+    if (p0 + u >= Rp) break;  // wave-uniform
+    const uint32_t ou = q < P ? o[u] : 0u;
+    const uint64_t m = __ballot(ou == 1);
+    const uint64_t er = ERR ? __ballot(ou == 2) : 0ull;
+    if (lane == 0) {
+      PM[uint64_t(j[u]) * W + w] = m;
+      if (ERR) ER[uint64_t(j[u]) * W + w] = er;
+    }
   }
 }
 template <bool ERR>
@@ -4040,7 +4062,7 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
     }
   } else if (Rp && E && nw && (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= P)) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
-    const unsigned g = unsigned((uint64_t(Rp) * nw + 3) / 4);
+    const unsigned g = unsigned((pod_direct_waves(Rp, nw) + 3) / 4);
     const uint32_t* eid = c->dir[1].pod_id.as<uint32_t>();
     if (pb.may_err)
       k_pod_rows_direct<true><<<g, 256, 0, st>>>(Rp, P, W, plist, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L, eid,
@@ -4461,7 +4483,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
       fb.Rp[x] = one_win && x ? 0u : c->rp_off[dhi] - c->rp_off[dlo];
       fb.plist[x] = c->pod_peers.as<uint32_t>() + c->rp_off[dlo];
       peer_window(c, one_win ? 1 : x, fb.pw0[x], fb.pnw[x]);
-      fb.nb[2 + x] = (fb.Rp[x] && E && fb.pnw[x]) ? blocks((uint64_t(fb.Rp[x]) * fb.pnw[x] + 3) / 4) : 0u;
+      fb.nb[2 + x] = (fb.Rp[x] && E && fb.pnw[x]) ? blocks((pod_direct_waves(fb.Rp[x], fb.pnw[x]) + 3) / 4) : 0u;
     }
   } else if (!ido) {  // PM builds: sparse pod-peer rows in launch C (k_front_c)
     fb.nb[2] = fb.nb[3] = 0;
