@@ -2118,13 +2118,9 @@ __device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const Word
 
 constexpr uint32_t IDO_RPB_MAX = 64;  // class_rpb's upper bound
 constexpr uint32_t IDO_IPL = 16;      // IP peers per representative staged in LDS (row, span, port bits)
-#ifndef CYC_IDO_CPB
-#define CYC_IDO_CPB 1  // IDO class rows: 256-word chunks per block (the block's staging is done once for all;
-                       // 2 / 4 / 7 measured slower on config #3: profiles/r03_ido_rows_ab.txt)
-#endif
-constexpr uint32_t IDO_CPB = CYC_IDO_CPB;
-// Grid rows of the IDO class rows per (slot chunk, representative group): groups of IDO_CPB chunks.
-__host__ __device__ inline uint32_t ido_chunk_groups(uint32_t WA) { return ((WA + 255) / 256 + IDO_CPB - 1) / IDO_CPB; }
+// Grid rows of the IDO class rows per (slot chunk, representative group): 256-word chunks (staging
+// once for 2 / 4 / 7 chunks per block measured slower on config #3: profiles/r03_ido_rows_ab.txt).
+__host__ __device__ inline uint32_t ido_chunk_groups(uint32_t WA) { return (WA + 255) / 256; }
 // The PM words (and chunk marks) of staged IP peers x0 .. x0 + N - 1 of a representative for pod word w.
 // Branch-free: every lane issues every load (a zero word where the peer is absent or w is outside its
 // span), so the batch's loads are in flight together — a load under a divergent branch is waited
@@ -2172,8 +2168,7 @@ struct RepHead {  // a class-row block's representative: identity, class-row ind
 template <bool EGRESS, int KC, bool UNI = false>
 __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   extern __shared__ uint64_t sB[];
-  // block = (a.rpb consecutive class representatives, KC job slots, IDO_CPB chunks of 256 pod
-  // words): the representatives' staging is done once for the block's chunks, and each word's runs
+  // block = (a.rpb consecutive class representatives, KC job slots, 256 pod words): each word's runs
   // and slot words are loaded once for all its representatives
   const uint32_t cg = ido_chunk_groups(a.WA), nkc = (a.K + KC - 1) / KC;
   const uint32_t kc = (bid_ / cg) % nkc;
@@ -2181,11 +2176,10 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   if (r0 >= n_reps) return;  // whole block
   const uint32_t nr = min(a.rpb, n_reps - r0), k0 = kc * KC;
   const uint32_t nrow = EGRESS && !UNI ? a.NB : min(uint32_t(KC), a.K - k0), rowsz = nrow * a.EW;
-  const uint32_t wend = a.w0 + a.WA, c0 = (bid_ % cg) * IDO_CPB;
-  // the first word's own loads (runs) are issued before the staging barrier, so their latency
-  // overlaps the staging loads instead of following them; each later chunk's runs are loaded one
-  // chunk ahead
-  uint32_t w = a.w0 + c0 * 256 + threadIdx.x;
+  const uint32_t wend = a.w0 + a.WA;
+  // the word's own loads (runs) are issued before the staging barrier, so their latency overlaps the
+  // staging loads instead of following them
+  const uint32_t w = a.w0 + (bid_ % cg) * 256 + threadIdx.x;
   WordRuns wr = a.runs[min(w, wend - 1)];  // (lanes past the window load a valid record and store nothing)
   const uint64_t lastmask = (a.P % 64) ? ((1ull << (a.P % 64)) - 1) : ~0ull;
   // Staging in two dependency levels, every load of a level issued unconditionally (clamped
@@ -2271,11 +2265,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   __syncthreads();
   // 16-byte stores of word pairs (store_row_pair): even rows of the class rows' window, aligned base
   const bool pair = a.WA % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
-  const uint32_t cend = min(c0 + IDO_CPB, (a.WA + 255) / 256);
-  for (uint32_t c = c0; c < cend; c++, w += 256) {  // no barrier below: lanes leave independently
-  if (w >= wend) break;
-  const WordRuns wcur = wr;
-  if (c + 1 < cend && w + 256 < wend) wr = a.runs[w + 256];  // the next chunk's runs, in flight meanwhile
+  if (w >= wend) return;  // no barrier below
+  const WordRuns& wcur = wr;
   const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
   uint64_t valid[KC];
   int32_t du[KC];
@@ -2389,7 +2380,6 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
 #pragma unroll
     for (int x = 0; x < KC; x++)
       if (x >= kk && k0 + x < a.K) rows[uint64_t(x) * a.WA + off] = allow[x] & valid[x];
-  }
   }
 }
 template <bool EGRESS, int KC, bool UNI = false>
@@ -2768,11 +2758,8 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
 // of BS x UNROLL 16-byte chunks covers the row (config #3: 100 KB rows, 512 x 13 x 16 B; config #4:
 // 25 KB rows, 256 x 7 x 16 B): every lane's loads are in flight before its stores and no second,
 // partly idle pass follows (profiles/r01_emit_wide_sweep.txt, r01_emit_medium_rows_ab.txt).
-#ifndef CYC_EMIT_WAVES
-#define CYC_EMIT_WAVES
-#endif
 template <int BS, int UNROLL>
-__global__ __launch_bounds__(BS) CYC_EMIT_WAVES void k_emit_wide(EmitArgs a) {
+__global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   emit_status(a);
   const uint32_t b = blockIdx.x, n = a.n_rows[0] + a.n_rows[1], x = b & 7;
   const uint32_t r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
@@ -4246,12 +4233,6 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // shard's word window, egress rows of its sources over all words).  d_status (may be null): the
 // status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
 // in the plan; the caller then copies the status plane itself).
-#ifndef CYC_EMIT_CFG
-// rows >= 64 KB: 1 = 1024-thread blocks, 7 16-byte chunks a thread per pass (48 VGPRs: 32 waves a CU);
-// 0 = 512 threads, one pass (84 VGPRs: 5 waves a SIMD, 20 a CU); 2 = 512 x 7.  Config #3 on one box:
-// 3.66 (1) vs 3.79 (0) vs 3.89 (2) ms per step (profiles/r03_emit_ab.txt)
-#define CYC_EMIT_CFG 1
-#endif
 #ifndef CYC_EMIT_WIDE_MIN
 #define CYC_EMIT_WIDE_MIN 16384  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
 #endif
@@ -4265,32 +4246,20 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
-  // 16-byte chunks per thread and pass <= 8 keeps a block at <= 48 VGPRs (8 waves a SIMD): 84 VGPRs for
-  // 512 x 13 held 5 (config #3 +3.5 % per step, profiles/r03_emit_ab.txt)
-  if (row_bytes > 512 * 7 * 16 && CYC_EMIT_CFG == 1) {  // > 56 KB: 1024 x 7 (config #3: 98 KB rows, one pass)
+  // 16-byte chunks per thread and pass <= 8 keeps a block at <= 48 VGPRs (8 waves a SIMD): a 512 x 13
+  // one-pass block held 84 VGPRs, 5 waves a SIMD, and ran config #3 3.5 % slower per step on a slow
+  // box (profiles/r03_emit_ab.txt; 512 x 7 in two passes was slower still)
+  if (row_bytes > 512 * 7 * 16) {  // > 56 KB: 1024 x 7 (config #3: 98 KB rows, one pass)
     k_emit_wide<1024, 7><<<g, 1024, 0, st>>>(ea);
-  } else if (row_bytes > 256 * 8 * 16 && CYC_EMIT_CFG == 1) {  // 32-56 KB: 512 x 7 (source shards at N = 2)
+  } else if (row_bytes > 256 * 8 * 16) {  // 32-56 KB: 512 x 7 (source shards at N = 2)
     k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
-  } else if (row_bytes >= 65536 && CYC_EMIT_CFG == 2) {  // 512-thread blocks, 7 chunks a thread per pass (A/B)
-    k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
-  } else if (row_bytes >= 65536) {  // 512-thread single pass: smallest UNROLL covering the row (16 = two passes)
-    const uint64_t need = (ea.row_words / 2 + 511) / 512;
-    if (need <= 8) k_emit_wide<512, 8><<<g, 512, 0, st>>>(ea);
-    else if (need <= 10) k_emit_wide<512, 10><<<g, 512, 0, st>>>(ea);
-    else if (need <= 12) k_emit_wide<512, 12><<<g, 512, 0, st>>>(ea);
-    else if (need <= 13) k_emit_wide<512, 13><<<g, 512, 0, st>>>(ea);
-    else if (need <= 14) k_emit_wide<512, 14><<<g, 512, 0, st>>>(ea);
-    else k_emit_wide<512, 16><<<g, 512, 0, st>>>(ea);
-  } else if (row_bytes >= CYC_EMIT_WIDE_MIN) {  // 256-thread single pass (16-64 KB rows)
+  } else if (row_bytes >= CYC_EMIT_WIDE_MIN) {  // 256-thread single pass (16-32 KB rows)
     const uint64_t need = (ea.row_words / 2 + 255) / 256;
     if (need <= 2) k_emit_wide<256, 2><<<g, 256, 0, st>>>(ea);
     else if (need <= 4) k_emit_wide<256, 4><<<g, 256, 0, st>>>(ea);
     else if (need <= 6) k_emit_wide<256, 6><<<g, 256, 0, st>>>(ea);
     else if (need <= 7) k_emit_wide<256, 7><<<g, 256, 0, st>>>(ea);
-    else if (need <= 8) k_emit_wide<256, 8><<<g, 256, 0, st>>>(ea);
-    else if (need <= 10) k_emit_wide<256, 10><<<g, 256, 0, st>>>(ea);
-    else if (need <= 12) k_emit_wide<256, 12><<<g, 256, 0, st>>>(ea);
-    else k_emit_wide<256, 16><<<g, 256, 0, st>>>(ea);
+    else k_emit_wide<256, 8><<<g, 256, 0, st>>>(ea);
   } else {  // flat multi-row sweep over ~32 KB per block
     ea.chunk = uint32_t(std::min<uint64_t>(EMIT_FLAT_MAX_ROWS, std::max<uint64_t>(1, 32768 / row_bytes)));
     k_emit_flat<8><<<(ea.per_xcd + ea.chunk - 1) / ea.chunk * 8, 256, 0, st>>>(ea);
