@@ -1347,7 +1347,6 @@ constexpr int CI_G = CYC_CI_G;
 template <bool EGRESS, int G>
 __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   __shared__ uint32_t s_j[4][CI_LDS];
-  __shared__ uint32_t s_pid[4][CI_LDS], s_pk[4][CI_LDS];  // per entry: identity-set row; kind << 16 | port-test bits
   ht_clear_slice(a, bid_, nblk_);
   // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
   const uint32_t wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wv = bid_ * 4 + wi, lane = threadIdx.x & 63;
@@ -1394,31 +1393,6 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the list is read back by other lanes
   const bool flat = m <= CI_LDS;
-  if (flat) {  // each entry's record, identity-set row and port test, a lane per entry: two load levels for all
-    for (uint32_t x = lane; x < m; x += 64) {
-      const uint32_t j = sj[x];
-      const DPeer pr = a.peers[j];
-      const uint32_t pid = a.peer_ido[j];
-      const uint32_t port = pr.kind == 0 ? 0u : pr.port;
-      uint32_t okb = 0;
-      if (a.portbits) {
-        const uint32_t pb = a.portbits[port];
-#pragma unroll
-        for (uint32_t y = 0; y < uint32_t(G); y++)
-          if (du[y] >= 0 && ((pb >> du[y]) & 1u)) okb |= 1u << y;
-      } else {
-        uint8_t pkb[G];
-#pragma unroll
-        for (uint32_t y = 0; y < uint32_t(G); y++) pkb[y] = a.portok[uint64_t(port) * a.D + uint32_t(max(du[y], 0))];
-#pragma unroll
-        for (uint32_t y = 0; y < uint32_t(G); y++)
-          if (du[y] >= 0 && pkb[y]) okb |= 1u << y;
-      }
-      s_pid[wi][x] = pid;
-      s_pk[wi][x] = (pr.kind << 16) | okb;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
   for (uint32_t ew0 = a.ew_lo; ew0 < a.ew_hi; ew0 += 64) {
     const uint32_t ew = ew0 + lane;
     uint64_t b[G];
@@ -1426,28 +1400,49 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
     for (uint32_t x = 0; x < uint32_t(G); x++) b[x] = (n == 0 && du[x] >= 0) ? ~0ull : 0ull;  // no target: allowed (policy.go:158-160)
     if (flat) {
       // no panic on this path: the OR over peers is order-free (AllPeersMatcher: every valid cell)
-      // entries staged once per wave (below, before this loop): only the identity-set words are
-      // loaded here, CI_WB at a time
-      constexpr uint32_t CI_WB = 8;
-      for (uint32_t x0 = 0; x0 < m; x0 += CI_WB) {
-        uint32_t pk[CI_WB];
-        uint64_t v[CI_WB];
+      // a batch's loads in three levels, each issued for every peer of the batch whatever its kind
+      // (absent peers / other kinds read a zero word): peer record + identity-set row id, then the
+      // identity-set word and the port test (descriptor bit row, or the byte table per slot)
+      for (uint32_t x0 = 0; x0 < m; x0 += CI_BATCH) {
+        uint32_t kind[CI_BATCH], port[CI_BATCH], pid[CI_BATCH];
 #pragma unroll
-        for (uint32_t u = 0; u < CI_WB; u++) {
-          const uint32_t x = min(x0 + u, m - 1);
-          const uint32_t pid = __builtin_amdgcn_readfirstlane(s_pid[wi][x]);
-          pk[u] = x0 + u < m ? __builtin_amdgcn_readfirstlane(s_pk[wi][x]) : (3u << 16);
-          const uint32_t kind = pk[u] >> 16;
-          const uint64_t iv = *(kind == 2 && ew < a.EW ? a.IDOB + uint64_t(pid) * a.EW + ew : a.zero);
-          v[u] = kind == 0 || kind == 1 ? ~0ull : iv;
+        for (uint32_t u = 0; u < CI_BATCH; u++) {
+          const uint32_t j = __builtin_amdgcn_readfirstlane(sj[min(x0 + u, m - 1)]);
+          const DPeer pr = a.peers[j];
+          pid[u] = a.peer_ido[j];
+          kind[u] = x0 + u < m ? pr.kind : 3u;
+          port[u] = pr.kind == 0 ? 0u : pr.port;
+        }
+        uint64_t v[CI_BATCH];
+        uint32_t ok[CI_BATCH];  // bit x: the peer's port matcher passes slot / descriptor du[x]
+#pragma unroll
+        for (uint32_t u = 0; u < CI_BATCH; u++) {
+          const uint64_t iv = *(kind[u] == 2 && ew < a.EW ? a.IDOB + uint64_t(pid[u]) * a.EW + ew : a.zero);
+          v[u] = kind[u] == 0 || kind[u] == 1 ? ~0ull : iv;
+          const bool live = kind[u] != 3;
+          if (a.portbits) {  // uniform
+            const uint32_t pb = *(live ? a.portbits + port[u] : reinterpret_cast<const uint32_t*>(a.zero));
+            ok[u] = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < uint32_t(G); x++)
+              if (du[x] >= 0 && ((pb >> du[x]) & 1u)) ok[u] |= 1u << x;
+          } else {
+            uint8_t pk[G];
+#pragma unroll
+            for (uint32_t x = 0; x < uint32_t(G); x++)
+              pk[x] = *(live ? a.portok + uint64_t(port[u]) * a.D + uint32_t(max(du[x], 0)) : reinterpret_cast<const uint8_t*>(a.zero));
+            ok[u] = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < uint32_t(G); x++)
+              if (du[x] >= 0 && pk[x]) ok[u] |= 1u << x;
+          }
         }
 #pragma unroll
-        for (uint32_t u = 0; u < CI_WB; u++) {
-          const uint32_t kind = pk[u] >> 16;
-          if (kind == 3) continue;  // IP peers: per pod word, in the class rows
+        for (uint32_t u = 0; u < CI_BATCH; u++) {
+          if (kind[u] == 3) continue;  // IP peers: per pod word, in the class rows
 #pragma unroll
           for (uint32_t x = 0; x < uint32_t(G); x++)
-            if (du[x] >= 0 && (kind == 0 || ((pk[u] >> x) & 1u))) b[x] |= v[u];
+            if (du[x] >= 0 && (kind[u] == 0 || ((ok[u] >> x) & 1u))) b[x] |= v[u];
         }
       }
     } else {
