@@ -8,9 +8,10 @@ already resident in HBM: selector evaluation, peer rows, port tables, target mem
 class election, class rows, and the emit of both packed verdict planes (ingress keyed by
 destination, egress keyed by source) for this rank's rows.  N > 1 shards the pods across ranks
 (one process per GPU, torch.distributed over RCCL for the barrier / max-time reduce only; there is
-no collective on the data path): --partition target (the default, the faster of the two on one-GPU
-shard timings, DESIGN.md §6: rank r owns the target rows of both planes) or source (north_star:
-rank r owns source pods, i.e. every cell Table.Get(from = s, *) of its sources).  Rank 0 prints one
+no collective on the data path): --partition source (the default, north_star's partition: rank r owns
+a contiguous share of the source pods, i.e. every cell Table.Get(from = s, *) of its sources, which it
+can answer alone — pkg/connectivity/probe/table.go:54-56, resources.go:286-287) or target (rank r owns
+the target rows of both planes; Get(from, to) then needs the ranks of both pods).  Rank 0 prints one
 JSON line.
 """
 from __future__ import annotations
@@ -104,7 +105,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-assemble", action="store_true", help="skip the N>1 all-gather timing")
-    ap.add_argument("--partition", default="target", choices=["source", "target"],
+    ap.add_argument("--partition", default="source", choices=["source", "target"],
                     help="row partition across ranks (include/cyclonus_hip.h cyc_rows; the same at N=1)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="cyc_set_option tuning knob (diagnostics; results never change)")
@@ -222,7 +223,8 @@ def main():
     # assembled table (not part of `value`): RCCL all-gather of both planes' row shards into the
     # full table on every rank, timed separately (max over ranks)
     assembled = None
-    if dist is not None and not args.no_assemble:
+    # (batched blocks: each rank holds its own problems' slabs, of rank-dependent sizes — nothing to assemble)
+    if dist is not None and not args.no_assemble and bt is None:
         try:
             dev = "cuda" if backend == "nccl" else "cpu"
             out_in = torch.empty((world * d_in.numel(),), dtype=torch.int64, device=dev)

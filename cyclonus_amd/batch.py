@@ -29,6 +29,24 @@ def _key(probe):
     return json.dumps(probe, sort_keys=True)
 
 
+def _field(obj, name):
+    """The keys of `obj` that decode into struct field `name` (encoding/json: exact or ASCII
+    case-insensitive), and the value that decides it: the last non-null one (a JSON null leaves a
+    string / struct field unchanged — cjson.hpp sval, the library's loader)."""
+    keys = [k for k in obj if k.lower() == name.lower()]
+    vals = [obj[k] for k in keys if obj[k] is not None]
+    return keys, (vals[-1] if vals else None)
+
+
+def _prefixed(obj, name, pre, default):
+    """A copy of `obj` whose field `name` is prefix + its decoded value (or `default` when absent or
+    null), held by ONE key: every case variant is dropped first, so no later variant overrides it."""
+    keys, v = _field(obj, name)
+    q = {k: x for k, x in obj.items() if k not in keys}
+    q[name] = pre + (v or default)
+    return q
+
+
 class Batch:
     def __init__(self, problems):
         """problems: list of {"policies": [...], "resources": {...}, "probe": {...}}."""
@@ -45,17 +63,17 @@ class Batch:
             pre = f"{b}~"
             for pol in p["policies"]:
                 q = copy.deepcopy(pol)
-                md = q.setdefault("metadata", {})
-                md["namespace"] = pre + (md.get("namespace") or "default")
+                mkeys, md = _field(q, "metadata")
+                q = {k: x for k, x in q.items() if k not in mkeys}
+                # the policy's namespace (builder.go: "" -> "default"), renamed into the block's
+                q["metadata"] = _prefixed(md if isinstance(md, dict) else {}, "namespace", pre, "default")
                 pols.append(q)
             for ns, labels in (p["resources"].get("Namespaces") or {}).items():
                 nss[pre + ns] = labels
             self.offsets.append(len(pods))
             self.sizes.append(len(p["resources"].get("Pods") or []))
             for pod in p["resources"].get("Pods") or []:
-                q = dict(pod)
-                q["Namespace"] = pre + pod.get("Namespace", "")
-                pods.append(q)
+                pods.append(_prefixed(pod, "Namespace", pre, ""))
             self.block_end.append(len(pods))
             self.block_config.append(self.probe_index[_key(p["probe"])])
         self.policies = pols

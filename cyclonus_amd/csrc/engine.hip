@@ -1339,7 +1339,7 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
 // identity-set words at once — one chain of dependent loads per batch instead of per peer (the
 // walk dominates this launch on row shards, where few classes leave the chip mostly idle).
 // Classes with more than CI_LDS peers walk the targets directly.
-constexpr uint32_t CI_LDS = 128, CI_BATCH = 4;
+constexpr uint32_t CI_LDS = 128;
 #ifndef CYC_CI_G
 #define CYC_CI_G 4  // identity sets: job slots (ingress) / descriptors (egress) per wave
 #endif
@@ -1347,6 +1347,7 @@ constexpr int CI_G = CYC_CI_G;
 template <bool EGRESS, int G>
 __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   __shared__ uint32_t s_j[4][CI_LDS];
+  __shared__ uint32_t s_pid[4][CI_LDS], s_pk[4][CI_LDS];  // per entry: identity-set row; kind << 16 | port-test bits
   ht_clear_slice(a, bid_, nblk_);
   // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
   const uint32_t wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wv = bid_ * 4 + wi, lane = threadIdx.x & 63;
@@ -1393,6 +1394,31 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the list is read back by other lanes
   const bool flat = m <= CI_LDS;
+  if (flat) {  // each entry's record, identity-set row and port test, a lane per entry: two load levels for all
+    for (uint32_t x = lane; x < m; x += 64) {
+      const uint32_t j = sj[x];
+      const DPeer pr = a.peers[j];
+      const uint32_t pid = a.peer_ido[j];
+      const uint32_t port = pr.kind == 0 ? 0u : pr.port;
+      uint32_t okb = 0;
+      if (a.portbits) {
+        const uint32_t pb = a.portbits[port];
+#pragma unroll
+        for (uint32_t y = 0; y < uint32_t(G); y++)
+          if (du[y] >= 0 && ((pb >> du[y]) & 1u)) okb |= 1u << y;
+      } else {
+        uint8_t pkb[G];
+#pragma unroll
+        for (uint32_t y = 0; y < uint32_t(G); y++) pkb[y] = a.portok[uint64_t(port) * a.D + uint32_t(max(du[y], 0))];
+#pragma unroll
+        for (uint32_t y = 0; y < uint32_t(G); y++)
+          if (du[y] >= 0 && pkb[y]) okb |= 1u << y;
+      }
+      s_pid[wi][x] = pid;
+      s_pk[wi][x] = (pr.kind << 16) | okb;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
   for (uint32_t ew0 = a.ew_lo; ew0 < a.ew_hi; ew0 += 64) {
     const uint32_t ew = ew0 + lane;
     uint64_t b[G];
@@ -1400,49 +1426,28 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
     for (uint32_t x = 0; x < uint32_t(G); x++) b[x] = (n == 0 && du[x] >= 0) ? ~0ull : 0ull;  // no target: allowed (policy.go:158-160)
     if (flat) {
       // no panic on this path: the OR over peers is order-free (AllPeersMatcher: every valid cell)
-      // a batch's loads in three levels, each issued for every peer of the batch whatever its kind
-      // (absent peers / other kinds read a zero word): peer record + identity-set row id, then the
-      // identity-set word and the port test (descriptor bit row, or the byte table per slot)
-      for (uint32_t x0 = 0; x0 < m; x0 += CI_BATCH) {
-        uint32_t kind[CI_BATCH], port[CI_BATCH], pid[CI_BATCH];
+      // entries staged once per wave (below, before this loop): only the identity-set words are
+      // loaded here, CI_WB at a time
+      constexpr uint32_t CI_WB = 8;
+      for (uint32_t x0 = 0; x0 < m; x0 += CI_WB) {
+        uint32_t pk[CI_WB];
+        uint64_t v[CI_WB];
 #pragma unroll
-        for (uint32_t u = 0; u < CI_BATCH; u++) {
-          const uint32_t j = __builtin_amdgcn_readfirstlane(sj[min(x0 + u, m - 1)]);
-          const DPeer pr = a.peers[j];
-          pid[u] = a.peer_ido[j];
-          kind[u] = x0 + u < m ? pr.kind : 3u;
-          port[u] = pr.kind == 0 ? 0u : pr.port;
-        }
-        uint64_t v[CI_BATCH];
-        uint32_t ok[CI_BATCH];  // bit x: the peer's port matcher passes slot / descriptor du[x]
-#pragma unroll
-        for (uint32_t u = 0; u < CI_BATCH; u++) {
-          const uint64_t iv = *(kind[u] == 2 && ew < a.EW ? a.IDOB + uint64_t(pid[u]) * a.EW + ew : a.zero);
-          v[u] = kind[u] == 0 || kind[u] == 1 ? ~0ull : iv;
-          const bool live = kind[u] != 3;
-          if (a.portbits) {  // uniform
-            const uint32_t pb = *(live ? a.portbits + port[u] : reinterpret_cast<const uint32_t*>(a.zero));
-            ok[u] = 0;
-#pragma unroll
-            for (uint32_t x = 0; x < uint32_t(G); x++)
-              if (du[x] >= 0 && ((pb >> du[x]) & 1u)) ok[u] |= 1u << x;
-          } else {
-            uint8_t pk[G];
-#pragma unroll
-            for (uint32_t x = 0; x < uint32_t(G); x++)
-              pk[x] = *(live ? a.portok + uint64_t(port[u]) * a.D + uint32_t(max(du[x], 0)) : reinterpret_cast<const uint8_t*>(a.zero));
-            ok[u] = 0;
-#pragma unroll
-            for (uint32_t x = 0; x < uint32_t(G); x++)
-              if (du[x] >= 0 && pk[x]) ok[u] |= 1u << x;
-          }
+        for (uint32_t u = 0; u < CI_WB; u++) {
+          const uint32_t x = min(x0 + u, m - 1);
+          const uint32_t pid = __builtin_amdgcn_readfirstlane(s_pid[wi][x]);
+          pk[u] = x0 + u < m ? __builtin_amdgcn_readfirstlane(s_pk[wi][x]) : (3u << 16);
+          const uint32_t kind = pk[u] >> 16;
+          const uint64_t iv = *(kind == 2 && ew < a.EW ? a.IDOB + uint64_t(pid) * a.EW + ew : a.zero);
+          v[u] = kind == 0 || kind == 1 ? ~0ull : iv;
         }
 #pragma unroll
-        for (uint32_t u = 0; u < CI_BATCH; u++) {
-          if (kind[u] == 3) continue;  // IP peers: per pod word, in the class rows
+        for (uint32_t u = 0; u < CI_WB; u++) {
+          const uint32_t kind = pk[u] >> 16;
+          if (kind == 3) continue;  // IP peers: per pod word, in the class rows
 #pragma unroll
           for (uint32_t x = 0; x < uint32_t(G); x++)
-            if (du[x] >= 0 && (kind[u] == 0 || ((ok[u] >> x) & 1u))) b[x] |= v[u];
+            if (du[x] >= 0 && (kind == 0 || ((pk[u] >> x) & 1u))) b[x] |= v[u];
         }
       }
     } else {
@@ -5099,6 +5104,7 @@ int cyc_probe_run_rows(cyc_ctx* c, void* stream, uint64_t* d_in, uint64_t* d_eg,
   if (!c->prepared) return fail(c, CYC_ERR_ARG, "cyc_probe_prepare first");
   if ((!d_in || !d_eg) && hi > lo) return fail(c, CYC_ERR_ARG, "null output plane");
   if (part != CYC_ROWS_TARGET && part != CYC_ROWS_SOURCE) return fail(c, CYC_ERR_ARG, "unknown partition");
+  if (!c->pb.blocks.empty()) return fail(c, CYC_ERR_ARG, "context prepared for blocks: use cyc_probe_run_blocks");
   return guarded(c, [&] {
     DeviceGuard dg(c->device);
     hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the HIP default (null) stream
@@ -5157,6 +5163,8 @@ struct cyc_table {
 // rows, words per egress row slot, first word of the ingress window.
 static bool rows_layout(const cyc_ctx* c, int part, int64_t lo, int64_t hi, int64_t v[5], std::string& why) {
   const int64_t P = c->pb.P, W = c->pb.W;
+  // a context prepared for batched blocks has per-block slabs, not row planes (cyc_probe_run_blocks)
+  if (!c->pb.blocks.empty()) return why = "context prepared for blocks: use cyc_probe_run_blocks", false;
   if (part != CYC_ROWS_TARGET && part != CYC_ROWS_SOURCE) return why = "unknown partition", false;
   if (lo < 0 || hi > P || lo > hi) return why = "row range out of bounds", false;
   if (part == CYC_ROWS_SOURCE && (lo % 64 || (hi % 64 && hi != P)))

@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from cyclonus_amd._lib import CyclonusPanic
+from cyclonus_amd._lib import CyclonusError, CyclonusPanic
 from cyclonus_amd.engine import Engine
 from oracle.oracle import Oracle, OraclePanic, combined_table
 from randgen import random_problem
@@ -731,6 +731,32 @@ def test_batch_cross_block_panic_isolated(gpu):
             want = Panicked(str(e))
         assert_same(want, Panicked(g.msg) if isinstance(g, CyclonusPanic) else g, blk["resources"]["Pods"][0]["Name"])
     assert isinstance(got[2], CyclonusPanic) and not isinstance(got[0], CyclonusPanic) and not isinstance(got[3], CyclonusPanic)
+
+
+def test_row_entry_points_refuse_block_contexts(gpu):
+    """A context prepared for batched blocks holds per-block slabs: the row-plane entry points
+    (cyc_probe_run_rows / run_host_rows / table_run_rows / table_wrap_rows / rows_layout) refuse it
+    with CYC_ERR_ARG instead of writing slabs sized by the row layout."""
+    import torch
+
+    from cyclonus_amd.batch import Batch
+
+    steps = []
+    for seed in (5, 6):
+        pols, res, probes = random_problem(310_000 + seed, n_pods=40)
+        steps.append({"policies": pols, "resources": res, "probe": probes[0]})
+    eng = Engine(0)
+    Batch(steps).prepare(eng)
+    for call in (lambda: eng.run_host(0, 10), lambda: eng.layout(0, 10), lambda: eng.table(0, 10),
+                 lambda: eng.run_host(0, 64, "source")):
+        with pytest.raises(CyclonusError, match="blocks"):
+            call()
+    buf = torch.zeros(1 << 16, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1 << 12, dtype=torch.uint8, device="cuda")
+    with pytest.raises(CyclonusError, match="blocks"):
+        eng.run_device(buf.data_ptr(), buf.data_ptr(), st.data_ptr(), torch.cuda.current_stream().cuda_stream, 0, 10)
+    with pytest.raises(CyclonusError, match="blocks"):
+        eng.wrap_table(buf.data_ptr(), buf.data_ptr(), st.data_ptr(), 0, 10)
 
 
 def _long_class_problem(seed, n_peers=300, n_pods=260):
