@@ -168,19 +168,31 @@ def main():
             eng.run_blocks_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), stream)
     else:
         # the drop-in's host cost (analyze --mode probe, pkg/cli/analyze.go:121, 232-243): policy build
-        # (BuildNetworkPolicies + Simplify), Resources load and cyc_probe_prepare (interning, job
-        # expansion, table upload) — paid once per probe model, outside `value`
-        pols_json, res_json = json.dumps(data["policies"]), json.dumps(data["resources"])
+        # (BuildNetworkPolicies + Simplify, from the k8s NetworkPolicy JSON), the probe model through
+        # the flat tables a cgo binding passes (cyc_resources_load: no JSON) and cyc_probe_prepare_configs
+        # (interning, job expansion, table upload) — paid once per probe model, outside `value`
+        from cyclonus_amd import flat
+
+        pols_json = json.dumps(data["policies"])
+        t_m = time.perf_counter()
+        res_tables = flat.ResourceTables(data["resources"])  # the binding's marshalling (Python here, Go there)
+        cfgs = flat.ProbeConfigs(data["probes"])
+        marshal_s = time.perf_counter() - t_m
         t_prep = time.perf_counter()
         eng.build_policies(pols_json)
         t_built = time.perf_counter()
-        eng.load_resources(res_json)
+        eng.load_resources_tables(res_tables)
         t_loaded = time.perf_counter()
-        shape = eng.prepare(data["probes"])
+        shape = eng.prepare_configs(cfgs)
         torch.cuda.synchronize()
         t_prepared = time.perf_counter()
         prepare_s = {"policy_build_s": t_built - t_prep, "resources_load_s": t_loaded - t_built,
-                     "probe_prepare_s": t_prepared - t_loaded, "total_s": t_prepared - t_prep}
+                     "probe_prepare_s": t_prepared - t_loaded, "total_s": t_prepared - t_prep,
+                     "path": "cyc_policy_build_json + cyc_resources_load (flat tables) + cyc_probe_prepare_configs",
+                     "tables_marshal_s": marshal_s,
+                     "note": "tables_marshal_s = building the flat tables in Python from the synthetic dicts (a Go "
+                             "binding fills them from its structs); not in total_s"}
+        del res_tables
         P, K, W = shape["pods"], shape["slots"], shape["words"]
         lo, hi = shard_range(P, world, rank, part)
         rows = hi - lo

@@ -59,7 +59,16 @@ EXPORTS = [
     "cyc_blocks_layout",
     "cyc_probe_run_blocks",
     "cyc_block_error",
+    "cyc_resources_load",
+    "cyc_policy_load",
+    "cyc_probe_prepare_configs",
+    "cyc_resources_json",
 ]
+
+# flat tables (cyc_policy_tables): cyc_peer_kind, cyc_ns_kind, cyc_port_kind
+PEER_ALL, PEER_PORTS, PEER_POD, PEER_IP = 0, 1, 2, 3
+NS_EXACT, NS_ALL, NS_LABEL = 0, 1, 2
+PORT_ANY, PORT_NUMBER, PORT_NAME = 0, 1, 2
 
 # cyc_rows (row partitions for one-process-per-GPU runs)
 ROWS_TARGET, ROWS_SOURCE = 0, 1
@@ -138,6 +147,11 @@ def lib():
         L.cyc_probe_run_blocks.argtypes = [vp, vp, vp, vp, vp, vp]
         L.cyc_block_error.argtypes = [vp, i64]
         L.cyc_block_error.restype = cp
+        L.cyc_resources_load.argtypes = [vp, vp]
+        L.cyc_policy_load.argtypes = [vp, vp]
+        L.cyc_probe_prepare_configs.argtypes = [vp, vp, i64, ctypes.POINTER(ProbeShape)]
+        L.cyc_resources_json.argtypes = [vp, cp, sz]
+        L.cyc_resources_json.restype = i64
         _lib = L
     return _lib
 

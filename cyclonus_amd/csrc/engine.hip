@@ -31,8 +31,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -3307,35 +3309,55 @@ static int guarded(cyc_ctx* c, F&& f) {
   }
 }
 
+static inline uint64_t hmix(uint64_t z) {  // splitmix64 finaliser (host)
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Pod identities per direction, numbered by first appearance in pod order: egress (namespace, label
+// set), ingress (namespace, label set, every slot's job status and descriptor).  Hashed into an
+// open-addressing table whose entries hold their first pod; a probe compares the pods' fields.
 static void build_identities(cyc_ctx* c) {
   Problem& pb = c->pb;
+  const uint32_t K = pb.K;
+  uint32_t cap = 2;
+  while (cap < 2 * std::max<uint32_t>(pb.P, 1)) cap <<= 1;
+  std::vector<uint32_t> slot_pod(cap), slot_id(cap);
   for (int d = 0; d < 2; d++) {
     Identities& I = c->ids[d];
     I = Identities{};
-    std::unordered_map<std::string, uint32_t> map;
     I.of_pod.resize(pb.P);
-    std::string key;
+    const bool slots = d == 0 && K;  // the ingress identity includes the pod's job descriptors
+    std::fill(slot_pod.begin(), slot_pod.end(), UINT32_MAX);
     for (uint32_t p = 0; p < pb.P; p++) {
-      key.assign(reinterpret_cast<const char*>(&pb.pod_ns[p]), 4);
-      key.append(reinterpret_cast<const char*>(&pb.pod_ls[p]), 4);
-      if (d == 0 && pb.K) {  // ingress identity includes the pod's job descriptors
-        key.append(reinterpret_cast<const char*>(&pb.slot_desc[size_t(p) * pb.K]), 4 * pb.K);
-        key.append(reinterpret_cast<const char*>(&pb.slot_status[size_t(p) * pb.K]), pb.K);
+      uint64_t h = hmix((uint64_t(pb.pod_ns[p]) << 32) | pb.pod_ls[p]);
+      if (slots)
+        for (uint32_t k = 0; k < K; k++)
+          h = hmix(h ^ (uint64_t(uint32_t(pb.slot_desc[size_t(p) * K + k])) << 8 | pb.slot_status[size_t(p) * K + k]));
+      uint32_t x = uint32_t(h) & (cap - 1);
+      for (;; x = (x + 1) & (cap - 1)) {
+        const uint32_t q = slot_pod[x];
+        if (q == UINT32_MAX) break;
+        if (pb.pod_ns[q] == pb.pod_ns[p] && pb.pod_ls[q] == pb.pod_ls[p] &&
+            (!slots || (memcmp(&pb.slot_desc[size_t(q) * K], &pb.slot_desc[size_t(p) * K], 4 * size_t(K)) == 0 &&
+                        memcmp(&pb.slot_status[size_t(q) * K], &pb.slot_status[size_t(p) * K], K) == 0)))
+          break;
       }
-      auto it = map.find(key);
-      if (it == map.end()) {
-        uint32_t id = uint32_t(I.ns.size());
+      if (slot_pod[x] == UINT32_MAX) {
+        slot_pod[x] = p;
+        slot_id[x] = uint32_t(I.ns.size());
         I.ns.push_back(pb.pod_ns[p]);
         I.ls.push_back(pb.pod_ls[p]);
         I.nsls.push_back(pb.pod_nsls[p]);
         if (d == 0)
-          for (uint32_t k = 0; k < pb.K; k++) {
-            I.desc.push_back(pb.slot_desc[size_t(p) * pb.K + k]);
-            I.status.push_back(pb.slot_status[size_t(p) * pb.K + k]);
+          for (uint32_t k = 0; k < K; k++) {
+            I.desc.push_back(pb.slot_desc[size_t(p) * K + k]);
+            I.status.push_back(pb.slot_status[size_t(p) * K + k]);
           }
-        it = map.emplace(key, id).first;
       }
-      I.of_pod[p] = it->second;
+      I.of_pod[p] = slot_id[x];
     }
     I.list_off.resize(I.ns.size());
     uint64_t tot = 0;
@@ -3345,9 +3367,9 @@ static void build_identities(cyc_ctx* c) {
       if (tot > 0xFFFFFFFFull) throw Panic{CYC_ERR_OOM, "membership lists exceed 2^32 entries"};
     }
     I.list_total = tot;
-    uint32_t cap = 2;
-    while (cap < 2 * I.ns.size()) cap <<= 1;
-    I.ht_cap = cap;
+    uint32_t hc = 2;
+    while (hc < 2 * I.ns.size()) hc <<= 1;
+    I.ht_cap = hc;
   }
 }
 
@@ -3462,6 +3484,7 @@ static void prepare_blocks_device(cyc_ctx* c) {
 
 static void prepare_device(cyc_ctx* c) {
   Problem& pb = c->pb;
+  PhaseClock clk("prepare_device");
   upload(c->ls_off, pb.ls_off);
   upload(c->ls_key, pb.ls_key);
   upload(c->ls_val, pb.ls_val);
@@ -3483,6 +3506,7 @@ static void prepare_device(cyc_ctx* c) {
   upload(c->slot_status, pb.slot_status);
   upload(c->slot_cfg, pb.slot_cfg);
   upload(c->slot_idx, pb.slot_idx);
+  clk.lap("uploads");
   uint64_t R = pb.peers.size(), W = pb.W, D = std::max<size_t>(pb.descs.size(), 1), K = pb.K;
   c->selres.alloc(std::max<uint64_t>(uint64_t(pb.S) * pb.L, 16));
   {  // dense label table for k_selectors_dense: label keys -> dense index kx, LVT[kx][l]
@@ -3554,6 +3578,7 @@ static void prepare_device(cyc_ctx* c) {
       upload(c->post_pods, pods);
     }
   }
+  clk.lap("label tables");
   c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
   c->ip_rng.alloc(std::max<uint64_t>(R * 16 + R * ((W + 63) / 64) * 4, 16));  // [R][4] word spans + chunk masks, then [R][W/64] cnz
   c->ER.alloc(pb.may_err ? std::max<uint64_t>(R * W * 8, 16) : 16);
@@ -3622,6 +3647,7 @@ static void prepare_device(cyc_ctx* c) {
     c->ido.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * c->ids[1].ns.size(), 16));
     c->idob.alloc(std::max<uint64_t>(uint64_t(pl.pod_peers.size()) * ((c->ids[1].ns.size() + 63) / 64) * 8, 16));
   }
+  clk.lap("peer plan");
   {  // one VALID descriptor per slot across all pods? (egress class rows then skip the per-word slot words)
     std::vector<int32_t> ud(std::max<uint32_t>(pb.K, 1), -1);
     bool uni = pb.P > 0 && pb.K > 0;
@@ -3680,6 +3706,7 @@ static void prepare_device(cyc_ctx* c) {
       dd.ip_list.alloc(std::max<uint64_t>(uint64_t(off[dd.n]) * 16, 16));
     }
   }
+  clk.lap("scratch");
   prepare_blocks_device(c);
   c->order_lo = c->order_hi = -1;
   c->order_src = false;
@@ -3791,6 +3818,7 @@ static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c
 static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   if (c->order_lo == lo && c->order_hi == hi && c->order_src == src) return;
   Problem& pb = c->pb;
+  PhaseClock clk("range plan");
   c->rl[0] = src ? 0 : lo;
   c->rh[0] = src ? int64_t(pb.P) : hi;
   c->rl[1] = lo;
@@ -3960,6 +3988,7 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   upload(c->ip_peers, ip);
   upload(c->ip_tests, tests);
   upload(c->ip_ex, c->plan.ip_ex);
+  clk.lap("done");
   c->order_lo = lo;
   c->order_hi = hi;
   c->order_src = src;
@@ -5012,8 +5041,40 @@ int cyc_resources_load_json(cyc_ctx* c, const char* js, size_t len) {
   });
 }
 
-static int probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* shape, const std::vector<ProbeBlock>* blocks) {
-  if (!c || !js) return CYC_ERR_ARG;
+int64_t cyc_resources_json(cyc_ctx* c, char* buf, size_t cap) {
+  if (!c || !c->have_res) return -1;
+  std::string s = dump_resources(c->res);
+  if (buf && cap > s.size()) {
+    memcpy(buf, s.data(), s.size());
+    buf[s.size()] = 0;
+  }
+  return int64_t(s.size()) + 1;
+}
+
+int cyc_resources_load(cyc_ctx* c, const cyc_resource_tables* t) {
+  if (!c || !t) return CYC_ERR_ARG;
+  return guarded(c, [&] {
+    c->res = load_resources_tables(*t);
+    c->have_res = true;
+    c->prepared = false;
+    return (int)CYC_OK;
+  });
+}
+
+int cyc_policy_load(cyc_ctx* c, const cyc_policy_tables* t) {
+  if (!c || !t) return CYC_ERR_ARG;
+  return guarded(c, [&] {
+    c->policy = load_policy_tables(*t);
+    c->have_policy = true;
+    c->prepared = false;
+    return (int)CYC_OK;
+  });
+}
+
+// `probes` decodes the probe configs (JSON or flat) inside the guarded call
+static int probe_prepare(cyc_ctx* c, const std::function<std::vector<ProbeConfig>()>& probes_of, cyc_probe_shape* shape,
+                         const std::vector<ProbeBlock>* blocks) {
+  if (!c) return CYC_ERR_ARG;
   if (!c->have_policy || !c->have_res) return fail(c, CYC_ERR_ARG, "load a policy and resources first");
   return guarded(c, [&] {
     DeviceGuard dg(c->device);
@@ -5022,12 +5083,16 @@ static int probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape
       for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
       HIPCHK(hipEventCreateWithFlags(&c->run_done, hipEventDisableTiming));
     }
-    auto probes = load_probes(json::parse(js, len));
+    const std::vector<ProbeConfig> probes = probes_of();
     c->prepared = false;
+    PhaseClock clk("prepare");
     c->pb = build_problem(c->policy, c->res, probes, blocks);
+    clk.lap("build_problem");
     drop_graph(c);
     build_identities(c);
+    clk.lap("identities");
     prepare_device(c);
+    clk.lap("device tables");
     c->prepared = true;
     if (shape) {
       shape->pods = c->pb.P;
@@ -5052,7 +5117,13 @@ static int probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape
 }
 
 int cyc_probe_prepare(cyc_ctx* c, const char* js, size_t len, cyc_probe_shape* shape) {
-  return probe_prepare(c, js, len, shape, nullptr);
+  if (!c || !js) return CYC_ERR_ARG;
+  return probe_prepare(c, [&] { return load_probes(json::parse(js, len)); }, shape, nullptr);
+}
+
+int cyc_probe_prepare_configs(cyc_ctx* c, const cyc_probe_config* cfgs, int64_t n, cyc_probe_shape* shape) {
+  if (!c || (n && !cfgs) || n < 0) return CYC_ERR_ARG;
+  return probe_prepare(c, [&] { return load_probe_configs(cfgs, n); }, shape, nullptr);
 }
 
 int cyc_probe_prepare_blocks(cyc_ctx* c, const char* js, size_t len, const int64_t* block_end, const int32_t* block_config,
@@ -5066,7 +5137,8 @@ int cyc_probe_prepare_blocks(cyc_ctx* c, const char* js, size_t len, const int64
     bl[size_t(b)] = ProbeBlock{uint32_t(at), uint32_t(block_end[b]), uint32_t(block_config[b])};
     at = block_end[b];
   }
-  return probe_prepare(c, js, len, shape, &bl);
+  if (!js) return CYC_ERR_ARG;
+  return probe_prepare(c, [&] { return load_probes(json::parse(js, len)); }, shape, &bl);
 }
 
 int cyc_blocks_layout(cyc_ctx* c, int64_t* out, int64_t n) {

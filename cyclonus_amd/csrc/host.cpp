@@ -14,6 +14,100 @@ namespace cyc {
 using json::Node;
 using json::quote;
 
+// ============================================================================ byte-string maps
+// Open-addressing map from byte strings to dense ids (first-insertion order), keys in one arena:
+// no allocation per key, one hash per lookup (the interning of 10^5-10^6 short strings and label maps
+// is the bulk of cyc_resources_load / cyc_probe_prepare's host time).
+static inline uint64_t bytes_hash(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xBF58476D1CE4E5B9ull);
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, p + i, 8);
+    h = (h ^ w) * 0x94D049BB133111EBull;
+    h ^= h >> 29;
+  }
+  uint64_t w = 0;
+  memcpy(&w, p + i, n - i);
+  h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 31;
+  h *= 0x94D049BB133111EBull;
+  return h ^ (h >> 32);
+}
+struct BytesMap {
+  std::vector<uint32_t> slot;  // id + 1; 0 = empty
+  std::vector<uint64_t> off{0};
+  std::string arena;
+  size_t size() const { return off.size() - 1; }
+  void reserve(size_t keys, size_t bytes) {
+    off.reserve(keys + 1);
+    arena.reserve(bytes);
+    size_t cap = 64;
+    while (cap < 2 * keys + 2) cap <<= 1;
+    if (cap > slot.size()) {
+      slot.assign(cap / 2, 0);  // grow() doubles it and re-inserts the (no) keys
+      grow();
+    }
+  }
+  std::string_view key(uint32_t id) const { return std::string_view(arena.data() + off[id], size_t(off[id + 1] - off[id])); }
+  // id of the key, adding it if absent (added = true)
+  uint32_t get(const char* p, size_t n, bool* added = nullptr) {
+    if (2 * (size() + 1) > slot.size()) grow();
+    const size_t mask = slot.size() - 1;
+    for (size_t x = bytes_hash(p, n) & mask;; x = (x + 1) & mask) {
+      const uint32_t s = slot[x];
+      if (!s) {
+        arena.append(p, n);
+        off.push_back(arena.size());
+        slot[x] = uint32_t(size());
+        if (added) *added = true;
+        return uint32_t(size() - 1);
+      }
+      const std::string_view k = key(s - 1);
+      if (k.size() == n && (n == 0 || memcmp(k.data(), p, n) == 0)) {
+        if (added) *added = false;
+        return s - 1;
+      }
+    }
+  }
+  void grow() {
+    std::vector<uint32_t> old(std::max<size_t>(slot.size() * 2, 64), 0);
+    old.swap(slot);
+    const size_t mask = slot.size() - 1;
+    for (uint32_t id = 0; id < size(); id++) {
+      const std::string_view k = key(id);
+      size_t x = bytes_hash(k.data(), k.size()) & mask;
+      while (slot[x]) x = (x + 1) & mask;
+      slot[x] = id + 1;
+    }
+  }
+};
+
+// Open-addressing map from 64-bit keys to 32-bit values (first insertion wins).
+struct U64Map {
+  std::vector<uint64_t> key;
+  std::vector<uint32_t> val;  // ~0 = empty slot
+  explicit U64Map(size_t n) {
+    size_t cap = 64;
+    while (cap < 2 * n + 2) cap <<= 1;
+    key.assign(cap, 0);
+    val.assign(cap, ~0u);
+  }
+  // the value stored under k, storing v first if k is absent
+  uint32_t emplace(uint64_t k, uint32_t v) {
+    const size_t mask = key.size() - 1;
+    uint64_t h = k * 0x9E3779B97F4A7C15ull;
+    for (size_t x = (h ^ (h >> 29)) & mask;; x = (x + 1) & mask) {
+      if (val[x] == ~0u) {
+        key[x] = k;
+        val[x] = v;
+        return v;
+      }
+      if (key[x] == k) return val[x];
+    }
+  }
+};
+
 // ============================================================================ selectors
 static std::string req_json(const Requirement& r) {
   std::string o = "{\"key\":" + quote(r.key) + ",\"operator\":" + quote(r.op);
@@ -632,6 +726,196 @@ PolicyIR load_policy_ir(const Node& root) {
   return ir;
 }
 
+// ============================================================================ IR flat tables
+// The already-built Go *matcher.Policy as cyc_policy_tables (include/cyclonus_hip.h): the same IR
+// load_policy_ir reads from json.Marshal(*Policy), without JSON.
+PolicyIR load_policy_tables(const cyc_policy_tables& t) {
+  const struct Check {
+    [[noreturn]] void bad(const std::string& m) const { throw Panic{CYC_ERR_ARG, "cyc_policy_tables: " + m}; }
+    void need(const void* p, const char* name) const {
+      if (!p) bad(std::string("null ") + name);
+    }
+    int64_t offsets(const int64_t* off, int64_t n, const char* name) const {
+      if (n < 0) bad(std::string("negative count for ") + name);
+      need(off, name);
+      if (off[0] < 0) bad(std::string(name) + "[0] < 0");
+      for (int64_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i]) bad(std::string(name) + " decreases at " + std::to_string(i));
+      return off[n];
+    }
+    void index(int64_t v, int64_t n, const char* name, int64_t at) const {
+      if (v < 0 || v >= n) bad(std::string(name) + "[" + std::to_string(at) + "] = " + std::to_string(v) + " out of range");
+    }
+  } ck;
+  // strings
+  ck.offsets(t.str.off, t.str.n, "str.off");
+  if (t.str.n && t.str.off[t.str.n] > t.str.off[0]) ck.need(t.str.bytes, "str.bytes");
+  auto S = [&](int64_t i, const char* name, int64_t at) {
+    ck.index(i, t.str.n, name, at);
+    return std::string(t.str.bytes + t.str.off[i], size_t(t.str.off[i + 1] - t.str.off[i]));
+  };
+  // selectors
+  const int64_t NS = t.n_selectors;
+  std::vector<Selector> sels(size_t(std::max<int64_t>(NS, 0)));
+  if (NS) {
+    const int64_t nl = ck.offsets(t.sel_label_off, NS, "sel_label_off");
+    const int64_t ne = ck.offsets(t.sel_expr_off, NS, "sel_expr_off");
+    if (nl > t.sel_label_off[0]) {
+      ck.need(t.sel_label_key, "sel_label_key");
+      ck.need(t.sel_label_val, "sel_label_val");
+    }
+    if (ne > t.sel_expr_off[0]) {
+      ck.need(t.expr_key, "expr_key");
+      ck.need(t.expr_op, "expr_op");
+      ck.need(t.expr_value_off, "expr_value_off");
+    }
+    for (int64_t i = 0; i < NS; i++) {
+      Selector& s = sels[size_t(i)];
+      for (int64_t j = t.sel_label_off[i]; j < t.sel_label_off[i + 1]; j++)
+        s.labels[S(t.sel_label_key[j], "sel_label_key", j)] = S(t.sel_label_val[j], "sel_label_val", j);
+      for (int64_t e = t.sel_expr_off[i]; e < t.sel_expr_off[i + 1]; e++) {
+        Requirement r;
+        r.key = S(t.expr_key[e], "expr_key", e);
+        r.op = S(t.expr_op[e], "expr_op", e);
+        if (t.expr_value_off[e + 1] < t.expr_value_off[e] || t.expr_value_off[e] < 0) ck.bad("expr_value_off decreases at " + std::to_string(e));
+        if (t.expr_value_off[e + 1] > t.expr_value_off[e]) ck.need(t.expr_value, "expr_value");
+        for (int64_t v = t.expr_value_off[e]; v < t.expr_value_off[e + 1]; v++) r.values.push_back(S(t.expr_value[v], "expr_value", v));
+        s.exprs.push_back(std::move(r));
+      }
+    }
+  }
+  auto sel = [&](int64_t i, const char* name, int64_t at) -> const Selector& {
+    ck.index(i, NS, name, at);
+    return sels[size_t(i)];
+  };
+  // port matchers (each keeps its own range array, as loaded from Go: aliasing already happened there)
+  PolicyIR ir;
+  const int64_t NM = t.n_port_matchers;
+  if (NM < 0) ck.bad("negative n_port_matchers");
+  if (NM) {
+    ck.need(t.pm_all, "pm_all");
+    const int64_t np = ck.offsets(t.pm_port_off, NM, "pm_port_off");
+    const int64_t nr = ck.offsets(t.pm_range_off, NM, "pm_range_off");
+    if (np > t.pm_port_off[0]) {
+      ck.need(t.port_kind, "port_kind");
+      ck.need(t.port_value, "port_value");
+      ck.need(t.port_proto, "port_proto");
+    }
+    if (nr > t.pm_range_off[0]) {
+      ck.need(t.range_from, "range_from");
+      ck.need(t.range_to, "range_to");
+      ck.need(t.range_proto, "range_proto");
+    }
+    for (int64_t m = 0; m < NM; m++) {
+      PortMatcher pm;
+      pm.all = t.pm_all[m] != 0;
+      if (!pm.all) {
+        pm.ports_nil = t.pm_ports_nil ? t.pm_ports_nil[m] != 0 : t.pm_port_off[m + 1] == t.pm_port_off[m];
+        for (int64_t j = t.pm_port_off[m]; j < t.pm_port_off[m + 1]; j++) {
+          PortEntry e;
+          e.proto = S(t.port_proto[j], "port_proto", j);
+          if (t.port_kind[j] == CYC_PORT_NUMBER) {
+            e.has_port = true;
+            e.port.i = t.port_value[j];
+          } else if (t.port_kind[j] == CYC_PORT_NAME) {
+            e.has_port = true;
+            e.port.is_str = true;
+            e.port.s = S(t.port_value[j], "port_value", j);
+          } else if (t.port_kind[j] != CYC_PORT_ANY) {
+            ck.bad("port_kind[" + std::to_string(j) + "] unknown");
+          }
+          pm.ports.push_back(std::move(e));
+          pm.ports_nil = false;
+        }
+        const bool rnil = t.pm_ranges_nil ? t.pm_ranges_nil[m] != 0 : t.pm_range_off[m + 1] == t.pm_range_off[m];
+        if (!rnil || t.pm_range_off[m + 1] > t.pm_range_off[m]) {
+          std::vector<PortRange> v;
+          for (int64_t j = t.pm_range_off[m]; j < t.pm_range_off[m + 1]; j++)
+            v.push_back(PortRange{t.range_from[j], t.range_to[j], S(t.range_proto[j], "range_proto", j)});
+          ir.range_arrays.push_back(v);
+          pm.ranges = RangeSlice{int(ir.range_arrays.size() - 1), uint32_t(v.size()), uint32_t(v.size())};
+        }
+      }
+      ir.pm.push_back(std::move(pm));
+    }
+  }
+  // targets and their ordered peers
+  if (t.n_targets[0] < 0 || t.n_targets[1] < 0) ck.bad("negative n_targets");
+  const int64_t NT = t.n_targets[0] + t.n_targets[1];
+  if (NT) {
+    ck.need(t.target_ns, "target_ns");
+    ck.need(t.target_sel, "target_sel");
+    const int64_t npeer = ck.offsets(t.target_peer_off, NT, "target_peer_off");
+    if (t.target_rule_off) {
+      const int64_t nrule = ck.offsets(t.target_rule_off, NT, "target_rule_off");
+      if (nrule > t.target_rule_off[0]) ck.need(t.rule_name, "rule_name");
+    }
+    if (npeer > t.target_peer_off[0]) {
+      ck.need(t.peer_kind, "peer_kind");
+      ck.need(t.peer_port, "peer_port");
+    }
+    for (int64_t x = 0; x < NT; x++) {
+      const int d = x < t.n_targets[0] ? 0 : 1;
+      Target tg;
+      tg.ns = S(t.target_ns[x], "target_ns", x);
+      tg.sel = sel(t.target_sel[x], "target_sel", x);
+      tg.pk = target_pk(tg.ns, tg.sel);
+      tg.peers_nil = t.target_peers_nil ? t.target_peers_nil[x] != 0 : t.target_peer_off[x + 1] == t.target_peer_off[x];
+      if (t.target_rule_off)
+        for (int64_t r = t.target_rule_off[x]; r < t.target_rule_off[x + 1]; r++) tg.rules.push_back(S(t.rule_name[r], "rule_name", r));
+      for (int64_t j = t.target_peer_off[x]; j < t.target_peer_off[x + 1]; j++) {
+        Peer p;
+        const uint8_t kind = t.peer_kind[j];
+        if (kind > CYC_PEER_IP) ck.bad("peer_kind[" + std::to_string(j) + "] unknown");
+        p.kind = PeerKind(kind);
+        if (kind != CYC_PEER_ALL) {
+          ck.index(t.peer_port[j], NM, "peer_port", j);
+          p.port = t.peer_port[j];
+        }
+        if (kind == CYC_PEER_POD) {
+          ck.need(t.peer_ns_kind, "peer_ns_kind");
+          ck.need(t.peer_pod_sel, "peer_pod_sel");
+          const uint8_t nk = t.peer_ns_kind[j];
+          if (nk == CYC_NS_EXACT) {
+            ck.need(t.peer_ns, "peer_ns");
+            p.ns_kind = NS_EXACT;
+            p.ns = S(t.peer_ns[j], "peer_ns", j);
+          } else if (nk == CYC_NS_LABEL) {
+            ck.need(t.peer_ns, "peer_ns");
+            p.ns_kind = NS_LABEL;
+            p.ns_sel = sel(t.peer_ns[j], "peer_ns", j);
+          } else if (nk == CYC_NS_ALL) {
+            p.ns_kind = NS_ALL;
+          } else {
+            ck.bad("peer_ns_kind[" + std::to_string(j) + "] unknown");
+          }
+          p.pod_all = t.peer_pod_sel[j] < 0;
+          if (!p.pod_all) p.pod_sel = sel(t.peer_pod_sel[j], "peer_pod_sel", j);
+        } else if (kind == CYC_PEER_IP) {
+          ck.need(t.peer_cidr, "peer_cidr");
+          ck.need(t.peer_except_off, "peer_except_off");
+          p.cidr = S(t.peer_cidr[j], "peer_cidr", j);
+          const int64_t e0 = t.peer_except_off[j], e1 = t.peer_except_off[j + 1];
+          if (e0 < 0 || e1 < e0) ck.bad("peer_except_off decreases at " + std::to_string(j));
+          if (e1 > e0) ck.need(t.except_cidr, "except_cidr");
+          for (int64_t e = e0; e < e1; e++) p.except.push_back(S(t.except_cidr[e], "except_cidr", e));
+          p.except_nil = t.peer_except_nil ? t.peer_except_nil[j] != 0 : e1 == e0;
+          if (e1 > e0) p.except_nil = false;
+        }
+        tg.peers.push_back(std::move(p));
+      }
+      if (!tg.peers.empty()) tg.peers_nil = false;
+      ir.dir[d].push_back(std::move(tg));
+    }
+  }
+  for (int d = 0; d < 2; d++) {  // Policy.Ingress / Egress are maps keyed by primary key: one target per key
+    std::sort(ir.dir[d].begin(), ir.dir[d].end(), [](const Target& a, const Target& b) { return a.pk < b.pk; });
+    for (size_t i = 1; i < ir.dir[d].size(); i++)
+      if (ir.dir[d][i].pk == ir.dir[d][i - 1].pk) ck.bad("two targets with primary key " + ir.dir[d][i].pk);
+  }
+  return ir;
+}
+
 // ============================================================================ probe model
 static void decode_labels(const Node* n, bool& nil, std::map<std::string, std::string>& out) {
   nil = !n || n->null();
@@ -639,39 +923,224 @@ static void decode_labels(const Node* n, bool& nil, std::map<std::string, std::s
   for (auto& kv : n->o) out[kv.first] = kv.second.null() ? "" : kv.second.str();
 }
 
+// Strings of the interned probe model: one table entry per distinct decoded string.
+namespace {
+struct StrTab {
+  Resources& r;
+  std::unordered_map<std::string, uint32_t> ids;
+  explicit StrTab(Resources& res) : r(res) {}
+  uint32_t operator()(const std::string& v) {
+    auto it = ids.find(v);
+    if (it != ids.end()) return it->second;
+    const uint32_t id = uint32_t(r.str.size());
+    r.str.push_back(v);
+    ids.emplace(v, id);
+    return id;
+  }
+};
+}  // namespace
+
 Resources load_resources(const Node& n) {
   Resources r;
-  if (auto ns = n.val("Namespaces"); ns && ns->is_obj())
-    for (auto& kv : ns->o) {
-      if (kv.second.null()) {
-        r.namespaces[kv.first] = std::nullopt;
-      } else {
-        std::map<std::string, std::string> l;
-        bool nil;
-        decode_labels(&kv.second, nil, l);
-        r.namespaces[kv.first] = l;
-      }
+  StrTab S(r);
+  const uint32_t empty = S("");
+  if (auto ns = n.val("Namespaces"); ns && ns->is_obj()) {
+    std::unordered_map<std::string, size_t> last;  // a repeated key: the last one wins (Go map decode)
+    for (size_t i = 0; i < ns->o.size(); i++) last[ns->o[i].first] = i;
+    for (size_t i = 0; i < ns->o.size(); i++) {
+      auto& kv = ns->o[i];
+      if (last[kv.first] != i) continue;
+      r.ns_name.push_back(S(kv.first));
+      r.ns_nil.push_back(kv.second.null() ? 1 : 0);
+      if (!kv.second.null())
+        for (auto& l : kv.second.o) {
+          r.ns_lab_key.push_back(S(l.first));
+          r.ns_lab_val.push_back(l.second.null() ? empty : S(l.second.str()));
+        }
+      r.ns_lab_off.push_back(uint32_t(r.ns_lab_key.size()));
     }
+  }
   if (auto pods = n.val("Pods"); pods && pods->is_arr()) {
-    r.pods.reserve(pods->a.size());
+    const size_t np = pods->a.size();
+    r.pod_ns.reserve(np);
+    r.pod_name.reserve(np);
+    r.pod_ip.reserve(np);
+    r.pod_lab_off.reserve(np + 1);
+    r.pod_cont_off.reserve(np + 1);
     for (auto& p : pods->a) {
-      Pod pod;
-      if (auto x = p.sval("Namespace")) pod.ns = x->str();
-      if (auto x = p.sval("Name")) pod.name = x->str();
-      if (auto x = p.sval("IP")) pod.ip = x->str();
-      decode_labels(p.val("Labels"), pod.labels_nil, pod.labels);
+      const Node* x;
+      r.pod_ns.push_back((x = p.sval("Namespace")) ? S(x->str()) : empty);
+      r.pod_name.push_back((x = p.sval("Name")) ? S(x->str()) : empty);
+      r.pod_ip.push_back((x = p.sval("IP")) ? S(x->str()) : empty);
+      if (auto ls = p.val("Labels"); ls && ls->is_obj())
+        for (auto& kv : ls->o) {
+          r.lab_key.push_back(S(kv.first));
+          r.lab_val.push_back(kv.second.null() ? empty : S(kv.second.str()));
+        }
+      r.pod_lab_off.push_back(uint32_t(r.lab_key.size()));
       if (auto cs = p.val("Containers"); cs && cs->is_arr())
         for (auto& c : cs->a) {
           Container ct;
-          if (auto x = c.sval("Name")) ct.name = x->str();
-          if (auto x = c.sval("Port")) ct.port = int32_t(x->i64());
-          if (auto x = c.sval("Protocol")) ct.proto = x->str();
-          if (auto x = c.sval("PortName")) ct.port_name = x->str();
-          pod.conts.push_back(ct);
+          ct.name = (x = c.sval("Name")) ? S(x->str()) : empty;
+          ct.port = (x = c.sval("Port")) ? int32_t(x->i64()) : 0;
+          ct.proto = (x = c.sval("Protocol")) ? S(x->str()) : empty;
+          ct.port_name = (x = c.sval("PortName")) ? S(x->str()) : empty;
+          r.conts.push_back(ct);
         }
-      r.pods.push_back(std::move(pod));
+      r.pod_cont_off.push_back(uint32_t(r.conts.size()));
     }
   }
+  return r;
+}
+
+// json.Marshal(*probe.Resources) of the fields the verdict path reads (Pod.ServiceIP and
+// Container.BatchJobs are not kept); map keys sorted as encoding/json writes them, a label map with
+// a repeated key as Go would hold it (last value).  Nil and empty label maps are one value here.
+std::string dump_resources(const Resources& r) {
+  auto labels = [&](const std::vector<uint32_t>& key, const std::vector<uint32_t>& val, uint32_t lo, uint32_t hi) {
+    std::map<std::string, std::string> m;
+    for (uint32_t j = lo; j < hi; j++) m[r.s(key[j])] = r.s(val[j]);
+    std::string o = "{";
+    for (auto& kv : m) o += (o.size() > 1 ? "," : "") + quote(kv.first) + ":" + quote(kv.second);
+    return o + "}";
+  };
+  std::map<std::string, std::string> nss;
+  for (size_t i = 0; i < r.ns_name.size(); i++)
+    nss[r.s(r.ns_name[i])] = r.ns_nil[i] ? "null" : labels(r.ns_lab_key, r.ns_lab_val, r.ns_lab_off[i], r.ns_lab_off[i + 1]);
+  std::string o = "{\"Namespaces\":{";
+  bool first = true;
+  for (auto& kv : nss) {
+    o += (first ? "" : ",") + quote(kv.first) + ":" + kv.second;
+    first = false;
+  }
+  o += "},\"Pods\":[";
+  for (size_t p = 0; p < r.pods(); p++) {
+    o += (p ? "," : "") + std::string("{\"Namespace\":") + quote(r.s(r.pod_ns[p])) + ",\"Name\":" + quote(r.s(r.pod_name[p])) +
+         ",\"Labels\":" + labels(r.lab_key, r.lab_val, r.pod_lab_off[p], r.pod_lab_off[p + 1]) + ",\"IP\":" + quote(r.s(r.pod_ip[p])) +
+         ",\"Containers\":[";
+    for (uint32_t i = 0; i < r.n_conts(p); i++) {
+      const Container& c = r.cont(p, i);
+      o += (i ? "," : "") + std::string("{\"Name\":") + quote(r.s(c.name)) + ",\"Port\":" + std::to_string(c.port) +
+           ",\"Protocol\":" + quote(r.s(c.proto)) + ",\"PortName\":" + quote(r.s(c.port_name)) + "}";
+    }
+    o += "]}";
+  }
+  return o + "]}";
+}
+
+// ---- flat tables (include/cyclonus_hip.h): validation helpers
+namespace {
+struct FlatCheck {
+  const char* what;
+  [[noreturn]] void bad(const std::string& m) const { throw Panic{CYC_ERR_ARG, std::string(what) + ": " + m}; }
+  void need(const void* p, const char* name) const {
+    if (!p) bad(std::string("null ") + name);
+  }
+  // offsets [n + 1], non-decreasing from >= 0: returns the element count they cover
+  int64_t offsets(const int64_t* off, int64_t n, const char* name) const {
+    if (n < 0) bad(std::string("negative count for ") + name);
+    need(off, name);
+    if (off[0] < 0) bad(std::string(name) + "[0] < 0");
+    for (int64_t i = 0; i < n; i++)
+      if (off[i + 1] < off[i]) bad(std::string(name) + " decreases at " + std::to_string(i));
+    return off[n];
+  }
+  uint32_t index(int64_t v, int64_t n, const char* name, int64_t at) const {
+    if (v < 0 || v >= n) bad(std::string(name) + "[" + std::to_string(at) + "] = " + std::to_string(v) + " out of range");
+    return uint32_t(v);
+  }
+};
+}  // namespace
+
+Resources load_resources_tables(const cyc_resource_tables& t) {
+  const FlatCheck ck{"cyc_resource_tables"};
+  PhaseClock clk("resources_load");
+  Resources r;
+  // the caller's string table may repeat a string: every index maps to one canonical entry, so equal
+  // ids <=> equal strings (Resources' invariant, which the name groups of the table build rely on)
+  ck.offsets(t.str.off, t.str.n, "str.off");
+  if (t.str.n && t.str.off[t.str.n] > t.str.off[0]) ck.need(t.str.bytes, "str.bytes");
+  std::vector<uint32_t> canon(size_t(t.str.n));
+  {
+    BytesMap seen;
+    seen.reserve(size_t(t.str.n), size_t(t.str.n ? t.str.off[t.str.n] - t.str.off[0] : 0));
+    for (int64_t i = 0; i < t.str.n; i++) canon[size_t(i)] = seen.get(t.str.bytes + t.str.off[i], size_t(t.str.off[i + 1] - t.str.off[i]));
+    r.str.resize(seen.size());
+    for (uint32_t k = 0; k < seen.size(); k++) r.str[k] = std::string(seen.key(k));
+  }
+  clk.lap("strings");
+  const int64_t n_str = t.str.n;
+  auto id = [&](int64_t v, const char* name, int64_t at) { return canon[ck.index(v, n_str, name, at)]; };
+  if (t.n_namespaces < 0 || t.n_pods < 0) ck.bad("negative count");
+  if (t.n_namespaces) {
+    ck.need(t.ns_name, "ns_name");
+    const int64_t nl = ck.offsets(t.ns_label_off, t.n_namespaces, "ns_label_off");
+    if (nl) {
+      ck.need(t.ns_label_key, "ns_label_key");
+      ck.need(t.ns_label_val, "ns_label_val");
+    }
+    // a repeated key: the last one wins (a Go map has none; this mirrors the JSON loader)
+    std::unordered_map<uint32_t, int64_t> last;
+    for (int64_t i = 0; i < t.n_namespaces; i++) last[id(t.ns_name[i], "ns_name", i)] = i;
+    for (int64_t i = 0; i < t.n_namespaces; i++) {
+      const uint32_t name = canon[uint32_t(t.ns_name[i])];
+      if (last[name] != i) continue;
+      r.ns_name.push_back(name);
+      r.ns_nil.push_back(t.ns_nil && t.ns_nil[i] ? 1 : 0);
+      for (int64_t j = t.ns_label_off[i]; j < t.ns_label_off[i + 1] && !r.ns_nil.back(); j++) {
+        r.ns_lab_key.push_back(id(t.ns_label_key[j], "ns_label_key", j));
+        r.ns_lab_val.push_back(id(t.ns_label_val[j], "ns_label_val", j));
+      }
+      r.ns_lab_off.push_back(uint32_t(r.ns_lab_key.size()));
+    }
+  }
+  const int64_t P = t.n_pods;
+  if (P) {
+    ck.need(t.pod_ns, "pod_ns");
+    ck.need(t.pod_name, "pod_name");
+    ck.need(t.pod_ip, "pod_ip");
+    const int64_t nl = ck.offsets(t.pod_label_off, P, "pod_label_off");
+    const int64_t nc = ck.offsets(t.pod_cont_off, P, "pod_cont_off");
+    const int64_t l0 = t.pod_label_off[0], c0 = t.pod_cont_off[0];
+    if (nl > l0) {
+      ck.need(t.label_key, "label_key");
+      ck.need(t.label_val, "label_val");
+    }
+    if (nc > c0) {
+      ck.need(t.cont_name, "cont_name");
+      ck.need(t.cont_port, "cont_port");
+      ck.need(t.cont_proto, "cont_proto");
+      ck.need(t.cont_port_name, "cont_port_name");
+    }
+    if (nl - l0 >= (int64_t(1) << 32) || nc - c0 >= (int64_t(1) << 32)) ck.bad("more than 2^32 labels or containers");
+    r.pod_ns.resize(size_t(P));
+    r.pod_name.resize(size_t(P));
+    r.pod_ip.resize(size_t(P));
+    r.pod_lab_off.assign(size_t(P) + 1, 0);
+    r.pod_cont_off.assign(size_t(P) + 1, 0);
+    for (int64_t p = 0; p < P; p++) {
+      r.pod_ns[size_t(p)] = id(t.pod_ns[p], "pod_ns", p);
+      r.pod_name[size_t(p)] = id(t.pod_name[p], "pod_name", p);
+      r.pod_ip[size_t(p)] = id(t.pod_ip[p], "pod_ip", p);
+      r.pod_lab_off[size_t(p) + 1] = uint32_t(t.pod_label_off[p + 1] - l0);
+      r.pod_cont_off[size_t(p) + 1] = uint32_t(t.pod_cont_off[p + 1] - c0);
+    }
+    r.lab_key.resize(size_t(nl - l0));
+    r.lab_val.resize(size_t(nl - l0));
+    for (int64_t j = l0; j < nl; j++) {
+      r.lab_key[size_t(j - l0)] = id(t.label_key[j], "label_key", j);
+      r.lab_val[size_t(j - l0)] = id(t.label_val[j], "label_val", j);
+    }
+    r.conts.resize(size_t(nc - c0));
+    for (int64_t j = c0; j < nc; j++) {
+      Container& c = r.conts[size_t(j - c0)];
+      c.name = id(t.cont_name[j], "cont_name", j);
+      c.port = t.cont_port[j];
+      c.proto = id(t.cont_proto[j], "cont_proto", j);
+      c.port_name = id(t.cont_port_name[j], "cont_port_name", j);
+    }
+  }
+  if (r.str.empty()) r.str.push_back("");  // (ids of absent fields are never read; keep the table non-empty)
   return r;
 }
 
@@ -690,6 +1159,21 @@ std::vector<ProbeConfig> load_probes(const Node& n) {
   };
   if (n.is_arr()) for (auto& p : n.a) one(p);
   else if (n.is_obj()) one(n);
+  return out;
+}
+
+std::vector<ProbeConfig> load_probe_configs(const cyc_probe_config* cfgs, int64_t n) {
+  if (n < 0 || (n && !cfgs)) throw Panic{CYC_ERR_ARG, "cyc_probe_config: null or negative count"};
+  std::vector<ProbeConfig> out(static_cast<size_t>(n));
+  for (int64_t i = 0; i < n; i++) {
+    ProbeConfig& c = out[size_t(i)];
+    c.all_available = cfgs[i].all_available != 0;
+    if (c.all_available) continue;
+    c.port.is_str = cfgs[i].port_is_name != 0;
+    if (c.port.is_str) c.port.s = cfgs[i].port_name ? cfgs[i].port_name : "";
+    else c.port.i = cfgs[i].port;
+    c.proto = cfgs[i].protocol ? cfgs[i].protocol : "";
+  }
   return out;
 }
 
@@ -868,46 +1352,65 @@ uint32_t Problem::intern(const std::string& s) {
 namespace {
 struct Flattener {
   Problem& pb;
-  std::unordered_map<std::string, uint32_t> ls_ids, sel_ids, cidr_ids, desc_ids;
+  BytesMap ls_ids;   // label set id = its id here (0 = the empty map)
+  BytesMap sel_ids;  // selector id = its id here
+  std::unordered_map<std::string, uint32_t> cidr_ids;
+  std::unordered_map<uint64_t, std::vector<uint32_t>> desc_ids;  // (name, protocol) -> descriptors by port
   std::unordered_map<int, uint32_t> pm_ids;
   const PolicyIR& ir;
 
   Flattener(Problem& p, const PolicyIR& i) : pb(p), ir(i) {
     pb.ls_off = {0};
-    ls_ids[""] = 0;  // label set 0 == empty map (nil behaves the same for reads)
+    ls_ids.get("", 0);  // label set 0 == empty map (nil behaves the same for reads)
     pb.ls_off.push_back(0);
     pb.sel_off = {0};
   }
 
-  uint32_t label_set(const std::map<std::string, std::string>& l) {
-    if (l.empty()) return 0;
-    std::string key;
-    for (auto& kv : l) {
-      key += kv.first;
-      key += '\0';
-      key += kv.second;
-      key += '\0';
-    }
-    auto it = ls_ids.find(key);
-    if (it != ls_ids.end()) return it->second;
-    std::vector<std::pair<uint32_t, uint32_t>> kvs;
-    for (auto& kv : l) kvs.emplace_back(pb.intern(kv.first), pb.intern(kv.second));
+  // A label map as (key id, value id) pairs of the problem's dictionary, keys unique: sorted here,
+  // then looked up by their raw bytes (every map with the same contents gets the same set)
+  uint32_t label_set(std::vector<std::pair<uint32_t, uint32_t>>& kvs) {
+    if (kvs.empty()) return 0;
     std::sort(kvs.begin(), kvs.end());
+    bool added = false;
+    const uint32_t id = ls_ids.get(reinterpret_cast<const char*>(kvs.data()), kvs.size() * sizeof(kvs[0]), &added);
+    if (!added) return id;
     for (auto& kv : kvs) {
       pb.ls_key.push_back(kv.first);
       pb.ls_val.push_back(kv.second);
     }
-    uint32_t id = uint32_t(pb.ls_off.size() - 1);
     pb.ls_off.push_back(uint32_t(pb.ls_key.size()));
-    ls_ids.emplace(key, id);
     return id;
   }
+  uint32_t label_set(const std::map<std::string, std::string>& l) {
+    std::vector<std::pair<uint32_t, uint32_t>> kvs;
+    for (auto& kv : l) kvs.emplace_back(pb.intern(kv.first), pb.intern(kv.second));
+    return label_set(kvs);
+  }
 
+  // a selector's identity: its matchLabels (sorted) and expressions, length-prefixed into one key
+  std::string sel_key;
+  void key_str(const std::string& x) {
+    const uint32_t n = uint32_t(x.size());
+    sel_key.append(reinterpret_cast<const char*>(&n), 4);
+    sel_key.append(x);
+  }
   uint32_t selector(const Selector& s) {
-    std::string key = s.serialize();
-    for (auto& e : s.exprs) key += "\x01" + e.op;  // operators are part of serialize; keep explicit
-    auto it = sel_ids.find(key);
-    if (it != sel_ids.end()) return it->second;
+    sel_key.clear();
+    for (auto& kv : s.labels) {
+      key_str(kv.first);
+      key_str(kv.second);
+    }
+    sel_key.push_back('\x01');
+    for (auto& e : s.exprs) {
+      key_str(e.key);
+      key_str(e.op);
+      const uint32_t nv = uint32_t(e.values.size());
+      sel_key.append(reinterpret_cast<const char*>(&nv), 4);
+      for (auto& v : e.values) key_str(v);
+    }
+    bool added = false;
+    const uint32_t id = sel_ids.get(sel_key.data(), sel_key.size(), &added);
+    if (!added) return id;
     for (auto& kv : s.labels) {  // matchLabels first (labelselector.go:69-74), then expressions
       DReq r{};
       r.key = pb.intern(kv.first);
@@ -930,9 +1433,7 @@ struct Flattener {
       }
       pb.reqs.push_back(r);
     }
-    uint32_t id = uint32_t(pb.sel_off.size() - 1);
     pb.sel_off.push_back(uint32_t(pb.reqs.size()));
-    sel_ids.emplace(key, id);
     return id;
   }
 
@@ -985,16 +1486,19 @@ struct Flattener {
     return id;
   }
 
-  uint32_t desc(int32_t port, const std::string& name, const std::string& proto) {
-    uint32_t n = pb.intern(name), p = pb.intern(proto);
-    std::string key = std::to_string(port) + "/" + std::to_string(n) + "/" + std::to_string(p);
-    auto it = desc_ids.find(key);
-    if (it != desc_ids.end()) return it->second;
+  // job descriptor (ResolvedPort, ResolvedPortName id, Protocol id)
+  uint32_t desc(int32_t port, uint32_t n, uint32_t p) {
+    const uint64_t k1 = (uint64_t(n) << 32) | p;
+    auto it = desc_ids.find(k1);
+    if (it != desc_ids.end())
+      for (uint32_t id : it->second)
+        if (pb.descs[id].port == port) return id;
     uint32_t id = uint32_t(pb.descs.size());
     pb.descs.push_back(DDesc{port, n, p, 0});
-    desc_ids.emplace(key, id);
+    desc_ids[k1].push_back(id);
     return id;
   }
+  uint32_t desc(int32_t port, const std::string& name, const std::string& proto) { return desc(port, pb.intern(name), pb.intern(proto)); }
 };
 }  // namespace
 
@@ -1071,28 +1575,50 @@ static void finish_tables(Problem& pb) {
 // reference's message continues with the Job as %+v and the stack pkg/errors prints; the job is
 // named here by FromKey, ToKey and ToContainer (the oracle's text, oracle/oracle.cpp).
 // Pods [q0, q1) are the problem's pods (a batched block's, or all).
-static std::string table_build_error(const Resources& res, const Problem& pb, const ProbeConfig& pc, size_t c, uint32_t koff,
+// Name groups of pods [q0, q1) — pods sharing their PodString "ns/name" share Items: grp[p] = the
+// group's first pod.  Grouped by the (ns, name) pair of string ids (equal ids <=> equal strings in a
+// Resources), which is the same relation as the joined string unless a namespace or name holds a '/'
+// (then by the string itself).
+static void name_groups(const Resources& res, uint32_t q0, uint32_t q1, std::vector<uint32_t>& grp) {
+  grp.assign(q1, 0);
+  bool slash = false;
+  for (uint32_t p = q0; p < q1 && !slash; p++)
+    slash = res.s(res.pod_ns[p]).find('/') != std::string::npos || res.s(res.pod_name[p]).find('/') != std::string::npos;
+  if (slash) {
+    std::unordered_map<std::string, uint32_t> first_of;
+    for (uint32_t p = q0; p < q1; p++) grp[p] = first_of.emplace(res.pod_string(p), p).first->second;
+    return;
+  }
+  U64Map first_of(q1 - q0);
+  for (uint32_t p = q0; p < q1; p++) grp[p] = first_of.emplace((uint64_t(res.pod_ns[p]) << 32) | res.pod_name[p], p);
+}
+
+static std::string table_build_error(const Resources& res, const Problem& pb, const ProbeConfig& pc, uint32_t koff,
                                      uint32_t q0, uint32_t q1) {
   const uint32_t P = q1;
   if (q1 <= q0) return "";
-  std::unordered_map<std::string, uint32_t> first_of;  // name group: first pod with the ns/name
-  std::vector<uint32_t> grp(P);
+  std::vector<uint32_t> grp;
+  name_groups(res, q0, q1, grp);
   uint32_t s_b = P;  // the first pod that is not the first of its name group
-  for (uint32_t p = q0; p < P; p++) {
-    grp[p] = first_of.emplace(pb.pod_key[p], p).first->second;
-    if (grp[p] != p && s_b == P) s_b = p;
-  }
+  std::vector<uint8_t> multi(P, 0);  // the pod's name group has other pods
+  for (uint32_t p = q0; p < P; p++)
+    if (grp[p] != p) {
+      if (s_b == P) s_b = p;
+      multi[p] = multi[grp[p]] = 1;
+    }
+  // a job's key Protocol/ResolvedPort (job.go:23-25) as (protocol id, port)
   struct DJob {
     uint32_t d, i;  // destination pod, container index (AllAvailable) or 0
-    std::string key;
+    uint32_t proto;
+    int32_t port;
   };
+  // PortProtocol jobs all carry the config's protocol: their keys differ by port only
+  const uint32_t pc_proto = 0;
   std::vector<DJob> jobs[3];
   for (uint32_t d = q0; d < P; d++) {
-    const Pod& pod = res.pods[d];
     const size_t base = size_t(d) * pb.K + koff;
     if (pc.all_available) {
-      for (uint32_t i = 0; i < pod.conts.size(); i++)
-        jobs[0].push_back({d, i, pod.conts[i].proto + "/" + std::to_string(pod.conts[i].port)});
+      for (uint32_t i = 0; i < res.n_conts(d); i++) jobs[0].push_back({d, i, res.cont(d, i).proto, res.cont(d, i).port});
       continue;
     }
     const uint8_t st = pb.slot_status[base];
@@ -1100,42 +1626,70 @@ static std::string table_build_error(const Resources& res, const Problem& pb, co
     if (st == CYC_JOB_VALID) port = pb.descs[size_t(pb.slot_desc[base])].port;
     else if (st == CYC_JOB_BAD_PORT_PROTOCOL) port = pc.port.i;
     const int cat = st == CYC_JOB_VALID ? 0 : st == CYC_JOB_BAD_PORT_PROTOCOL ? 1 : 2;
-    jobs[cat].push_back({d, 0, pc.proto + "/" + std::to_string(port)});
+    jobs[cat].push_back({d, 0, pc_proto, port});
   }
-  std::set<std::pair<uint32_t, std::string>> seen;  // (name group of the destination, key)
+  // (name group, key) pairs seen so far: a pod alone in its group can only repeat a key among its
+  // own jobs (its containers, AllAvailable), checked in place; groups of several pods share a set
+  struct GK {
+    uint32_t g, proto;
+    int32_t port;
+    bool operator<(const GK& o) const { return std::tie(g, proto, port) < std::tie(o.g, o.proto, o.port); }
+  };
+  std::set<GK> seen;
+  auto repeats = [&](const DJob& j, const std::vector<DJob>& js, size_t at) {
+    if (multi[j.d]) return !seen.insert(GK{grp[j.d], j.proto, j.port}).second;
+    // the pod's earlier jobs of this category are the entries just before it (same d)
+    for (size_t x = at; x-- > 0 && js[x].d == j.d;)
+      if (js[x].proto == j.proto && js[x].port == j.port) return true;
+    return false;
+  };
+  auto key_text = [&](const DJob& j) {
+    const std::string& proto = pc.all_available ? res.s(res.cont(j.d, j.i).proto) : pc.proto;
+    return proto + "/" + std::to_string(j.port);
+  };
+  auto message = [&](const DJob& j, uint32_t from) {
+    const std::string to_cont = pc.all_available ? res.s(res.cont(j.d, j.i).name) : "";
+    return "unable to add job result: duplicate key " + key_text(j) + " (job {FromKey:" + res.pod_string(from) +
+           " ToKey:" + res.pod_string(j.d) + " ToContainer:" + to_cont + "})";
+  };
   for (int cat = 0; cat < 3; cat++) {
     const DJob* hit = nullptr;
-    for (const DJob& j : jobs[cat])
-      if (!seen.insert({grp[j.d], j.key}).second) {
-        hit = &j;
-        break;
-      }
-    if (!hit && s_b < P && !jobs[cat].empty()) {
-      hit = &jobs[cat][0];
-      const std::string to_cont = pc.all_available ? res.pods[hit->d].conts[hit->i].name : "";
-      return "unable to add job result: duplicate key " + hit->key + " (job {FromKey:" + pb.pod_key[s_b] +
-             " ToKey:" + pb.pod_key[hit->d] + " ToContainer:" + to_cont + "})";
-    }
-    if (hit) {
-      const std::string to_cont = pc.all_available ? res.pods[hit->d].conts[hit->i].name : "";
-      return "unable to add job result: duplicate key " + hit->key + " (job {FromKey:" + pb.pod_key[q0] + " ToKey:" +
-             pb.pod_key[hit->d] + " ToContainer:" + to_cont + "})";
-    }
+    for (size_t x = 0; x < jobs[cat].size() && !hit; x++)
+      if (repeats(jobs[cat][x], jobs[cat], x)) hit = &jobs[cat][x];
+    if (!hit && s_b < P && !jobs[cat].empty()) return message(jobs[cat][0], s_b);
+    if (hit) return message(*hit, q0);
   }
   return "";
 }
 
+// Problem dictionary ids of the resources' strings, interned on first use.
+namespace {
+struct ResIds {
+  Problem& pb;
+  const Resources& res;
+  std::vector<uint32_t> sid;
+  ResIds(Problem& p, const Resources& r) : pb(p), res(r), sid(r.str.size(), UINT32_MAX) {}
+  uint32_t operator()(uint32_t r) {
+    uint32_t& x = sid[r];
+    if (x == UINT32_MAX) x = pb.intern(res.str[r]);
+    return x;
+  }
+};
+}  // namespace
+
 Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vector<ProbeConfig>& probes,
                       const std::vector<ProbeBlock>* blocks) {
   Problem pb;
+  PhaseClock clk("build_problem");
   Flattener F(pb, ir);
-  pb.P = uint32_t(res.pods.size());
+  ResIds R(pb, res);
+  pb.P = uint32_t(res.pods());
   pb.W = (pb.P + 63) / 64;
   if (blocks) {  // batched blocks: consecutive pod ranges covering the pods, namespaces private to a block
     pb.blocks = *blocks;
     pb.pod_blk.assign(pb.P, 0);
     uint32_t at = 0;
-    std::unordered_map<std::string, uint32_t> ns_blk;
+    std::unordered_map<uint32_t, uint32_t> ns_blk;
     for (uint32_t b = 0; b < blocks->size(); b++) {
       const ProbeBlock& bl = (*blocks)[b];
       if (bl.p0 != at || bl.p1 < bl.p0 || bl.p1 > pb.P || bl.cfg >= probes.size())
@@ -1144,42 +1698,70 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
         pb.pod_blk[q] = b;
         // a namespace's targets apply to all its pods (TargetsApplyingToPod policy.go:68-82): a block's
         // problem is its own only if no other block has pods in its namespaces
-        auto it = ns_blk.emplace(res.pods[q].ns, b).first;
-        if (it->second != b) throw Panic{CYC_ERR_ARG, "namespace " + res.pods[q].ns + " has pods in two blocks"};
+        auto it = ns_blk.emplace(R(res.pod_ns[q]), b).first;
+        if (it->second != b) throw Panic{CYC_ERR_ARG, "namespace " + res.s(res.pod_ns[q]) + " has pods in two blocks"};
       }
       at = bl.p1;
     }
     if (at != pb.P) throw Panic{CYC_ERR_ARG, "blocks must cover every pod"};
   }
 
+  // ---- namespaces: r.Namespaces[ns] (nil when absent) as a label set, by namespace id
+  std::unordered_map<uint32_t, uint32_t> ns_ls;
+  std::vector<std::pair<uint32_t, uint32_t>> kvs;
+  auto labels = [&](const std::vector<uint32_t>& key, const std::vector<uint32_t>& val, uint32_t lo, uint32_t hi) {
+    // a Go map: each key once (a repeated key in the input: the last one wins)
+    kvs.clear();
+    for (uint32_t j = lo; j < hi; j++) kvs.emplace_back(R(key[j]), R(val[j]));
+    if (kvs.size() > 1) {
+      std::stable_sort(kvs.begin(), kvs.end(), [](auto& a, auto& b) { return a.first < b.first; });
+      size_t w = 0;
+      for (size_t j = 0; j < kvs.size(); j++) {
+        if (w && kvs[w - 1].first == kvs[j].first) kvs[w - 1] = kvs[j];
+        else kvs[w++] = kvs[j];
+      }
+      kvs.resize(w);
+    }
+    return F.label_set(kvs);
+  };
+  for (size_t i = 0; i < res.ns_name.size(); i++)
+    ns_ls[R(res.ns_name[i])] = res.ns_nil[i] ? 0u : labels(res.ns_lab_key, res.ns_lab_val, res.ns_lab_off[i], res.ns_lab_off[i + 1]);
+
   // ---- pods
   bool any_bad_ip = false;
-  std::vector<uint32_t> ns_ls_cache;
-  std::unordered_map<std::string, uint32_t> nsls;
-  for (auto& p : res.pods) {
-    pb.pod_ns.push_back(pb.intern(p.ns));
-    pb.pod_ls.push_back(F.label_set(p.labels));
-    auto it = nsls.find(p.ns);
-    if (it == nsls.end()) {
-      uint32_t id = 0;
-      auto nit = res.namespaces.find(p.ns);  // r.Namespaces[ns]: nil when absent
-      if (nit != res.namespaces.end() && nit->second) id = F.label_set(*nit->second);
-      it = nsls.emplace(p.ns, id).first;
+  pb.pod_ns.resize(pb.P);
+  pb.pod_ls.resize(pb.P);
+  pb.pod_nsls.resize(pb.P);
+  pb.pod_ip.resize(pb.P);
+  pb.pod_ip_str.assign(pb.P, std::string());
+  std::vector<DIP> ip_of(res.str.size());  // an IP string parsed once
+  std::vector<uint8_t> ip_done(res.str.size(), 0);
+  for (uint32_t p = 0; p < pb.P; p++) {
+    const uint32_t ns = R(res.pod_ns[p]);
+    pb.pod_ns[p] = ns;
+    pb.pod_ls[p] = labels(res.lab_key, res.lab_val, res.pod_lab_off[p], res.pod_lab_off[p + 1]);
+    auto it = ns_ls.find(ns);
+    pb.pod_nsls[p] = it == ns_ls.end() ? 0u : it->second;
+    const uint32_t ips = res.pod_ip[p];
+    if (!ip_done[ips]) {
+      ip_of[ips] = parse_ip(res.s(ips));
+      ip_done[ips] = 1;
     }
-    pb.pod_nsls.push_back(it->second);
-    DIP ip = parse_ip(p.ip);
-    if (!ip.valid) any_bad_ip = true;
-    pb.pod_ip.push_back(ip);
-    pb.pod_ip_str.push_back(p.ip);
-    pb.pod_key.push_back(p.ns + "/" + p.name);
+    pb.pod_ip[p] = ip_of[ips];
+    if (!pb.pod_ip[p].valid) {
+      any_bad_ip = true;
+      pb.pod_ip_str[p] = res.s(ips);
+    }
   }
 
+  clk.lap("pods");
   bool any_ip_peer = flatten_targets(pb, F, ir);
   if (any_ip_peer && any_bad_ip) pb.may_err = true;
+  clk.lap("targets");
 
   // ---- probe job slots (resources.go:274-364, resolved per destination pod)
   size_t maxc = 0;
-  for (auto& p : res.pods) maxc = std::max(maxc, p.conts.size());
+  for (uint32_t p = 0; p < pb.P; p++) maxc = std::max<size_t>(maxc, res.n_conts(p));
   std::vector<uint32_t> cfg_off;
   for (size_t c = 0; c < probes.size(); c++) {
     cfg_off.push_back(pb.K);
@@ -1197,65 +1779,61 @@ Problem build_problem(const PolicyIR& ir, const Resources& res, const std::vecto
   pb.expand_panic.assign(probes.size(), 0);
   {
     bool bare = false, any_cont = false;
-    for (auto& p : res.pods) (p.conts.empty() ? bare : any_cont) = true;
+    for (uint32_t p = 0; p < pb.P; p++) (res.n_conts(p) == 0 ? bare : any_cont) = true;
     for (size_t c = 0; c < probes.size(); c++)  // PortProtocol: every (from, to) pair builds a job;
       pb.expand_panic[c] = bare && (probes[c].all_available ? any_cont : true);  // AllAvailable: one per dst container
     pb.blk_expand_panic.assign(pb.blocks.size(), 0);
     for (size_t b = 0; b < pb.blocks.size(); b++) {  // the same, per block over its own pods
       bool bb = false, bc = false;
-      for (uint32_t q = pb.blocks[b].p0; q < pb.blocks[b].p1; q++) (res.pods[q].conts.empty() ? bb : bc) = true;
+      for (uint32_t q = pb.blocks[b].p0; q < pb.blocks[b].p1; q++) (res.n_conts(q) == 0 ? bb : bc) = true;
       pb.blk_expand_panic[b] = bb && (probes[pb.blocks[b].cfg].all_available ? bc : true);
     }
   }
   for (size_t c = 0; c < probes.size(); c++) {
     const ProbeConfig& pc = probes[c];
+    const uint32_t proto = pb.intern(pc.proto), pname = pc.port.is_str ? pb.intern(pc.port.s) : 0u;
     for (uint32_t d = 0; d < pb.P; d++) {
       if (!pb.blocks.empty() && pb.blocks[pb.pod_blk[d]].cfg != c) continue;  // a block answers its config only
-      const Pod& pod = res.pods[d];
-      size_t base = size_t(d) * pb.K + cfg_off[c];
+      const size_t base = size_t(d) * pb.K + cfg_off[c];
+      const uint32_t nc = res.n_conts(d);
       if (pc.all_available) {  // GetJobsAllAvailableServers :336-364
-        for (size_t i = 0; i < pod.conts.size(); i++) {
-          auto& ct = pod.conts[i];
-          pb.slot_desc[base + i] = int32_t(F.desc(ct.port, ct.port_name, ct.proto));
+        for (uint32_t i = 0; i < nc; i++) {
+          const Container& ct = res.cont(d, i);
+          pb.slot_desc[base + i] = int32_t(F.desc(ct.port, R(ct.port_name), R(ct.proto)));
           pb.slot_status[base + i] = CYC_JOB_VALID;
         }
         continue;
       }
       // GetJobsForNamedPortProtocol :284-334 (every pair gets a job)
+      const Container* hit = nullptr;
+      for (uint32_t i = 0; i < nc && !hit; i++) {
+        const Container& ct = res.cont(d, i);
+        if (pc.port.is_str ? R(ct.port_name) == pname : ct.port == pc.port.i) hit = &ct;
+      }
       if (pc.port.is_str) {  // ResolveNamedPort pod.go:132-139
-        const Container* hit = nullptr;
-        for (auto& ct : pod.conts)
-          if (ct.port_name == pc.port.s) {
-            hit = &ct;
-            break;
-          }
         if (hit) {
-          pb.slot_desc[base] = int32_t(F.desc(hit->port, pc.port.s, pc.proto));
+          pb.slot_desc[base] = int32_t(F.desc(hit->port, pname, proto));
           pb.slot_status[base] = CYC_JOB_VALID;
         } else {
           pb.slot_status[base] = CYC_JOB_BAD_NAMED_PORT;
         }
       } else {  // ResolveNumberedPort pod.go:141-148 (protocol ignored)
-        const Container* hit = nullptr;
-        for (auto& ct : pod.conts)
-          if (ct.port == pc.port.i) {
-            hit = &ct;
-            break;
-          }
         if (hit) {
-          pb.slot_desc[base] = int32_t(F.desc(pc.port.i, hit->port_name, pc.proto));
+          pb.slot_desc[base] = int32_t(F.desc(pc.port.i, R(hit->port_name), proto));
           pb.slot_status[base] = CYC_JOB_VALID;
         } else {
           pb.slot_status[base] = CYC_JOB_BAD_PORT_PROTOCOL;
         }
       }
     }
-    if (pb.blocks.empty()) pb.dup_key_msg[c] = table_build_error(res, pb, pc, c, cfg_off[c], 0, pb.P);
+    clk.lap("job slots");
+    if (pb.blocks.empty()) pb.dup_key_msg[c] = table_build_error(res, pb, pc, cfg_off[c], 0, pb.P);
+    clk.lap("table build");
   }
   pb.blk_dup_msg.assign(pb.blocks.size(), "");
   for (size_t b = 0; b < pb.blocks.size(); b++) {
     const ProbeBlock& bl = pb.blocks[b];
-    pb.blk_dup_msg[b] = table_build_error(res, pb, probes[bl.cfg], bl.cfg, cfg_off[bl.cfg], bl.p0, bl.p1);
+    pb.blk_dup_msg[b] = table_build_error(res, pb, probes[bl.cfg], cfg_off[bl.cfg], bl.p0, bl.p1);
   }
 
   finish_tables(pb);

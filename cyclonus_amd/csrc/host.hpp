@@ -7,7 +7,10 @@
 // jobs (resources.go:284-364; O(pods x containers)).  Every O(pods x policies) and O(pods^2 x
 // ports) step of the verdict path runs on the GPU (engine.hip).
 #pragma once
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <optional>
 #include <string>
@@ -15,9 +18,25 @@
 #include <vector>
 
 #include "cjson.hpp"
+#include "cyclonus_hip.h"
 #include "tables.h"
 
 namespace cyc {
+
+// CYC_TRACE_PREPARE=1: host phase times of cyc_probe_prepare on stderr (development aid)
+struct PhaseClock {
+  const char* what;
+  bool on = getenv("CYC_TRACE_PREPARE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit PhaseClock(const char* w) : what(w) {}
+  void lap(const char* phase) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[cyc %s] %-14s %8.2f ms\n", what, phase, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+
 
 // A Go panic the reference would raise (message text follows the reference).
 struct Panic {
@@ -113,22 +132,35 @@ PolicyIR build_network_policies(const json::Node& netpols, bool simplify);
 // Load json.Marshal(*matcher.Policy) — what a cgo binding hands over.
 PolicyIR load_policy_ir(const json::Node& ir);
 std::string dump_policy_ir(const PolicyIR& p);
+// The same IR from the flat tables of include/cyclonus_hip.h (cyc_policy_tables); throws Panic{CYC_ERR_ARG}.
+PolicyIR load_policy_tables(const cyc_policy_tables& t);
 
 // ----------------------------------------------------------------------------- probe model
-struct Container {  // probe.Container (pod.go:173-179)
-  std::string name;
+// probe.Resources (resources.go:15-19, pod.go:44-51,173-179) in interned form: every string is an
+// index into `str` (duplicates allowed: the flat tables of a binding may repeat a string), maps and
+// lists are offset ranges.  Both loaders fill it — the JSON one (cyc_resources_load_json) and the
+// flat tables a cgo binding passes without JSON (cyc_resources_load) — and build_problem reads only
+// this, mapping each distinct string to the problem's dictionary once instead of once per use.
+struct Container {  // probe.Container: Name, Port, Protocol, PortName
+  uint32_t name = 0, proto = 0, port_name = 0;
   int32_t port = 0;
-  std::string proto, port_name;
 };
-struct Pod {  // probe.Pod (pod.go:44-51)
-  std::string ns, name, ip;
-  bool labels_nil = true;
-  std::map<std::string, std::string> labels;
+struct Resources {
+  std::vector<std::string> str;
+  // Namespaces map[string]map[string]string: key, nil-ness of the label map, its labels
+  std::vector<uint32_t> ns_name;
+  std::vector<uint8_t> ns_nil;
+  std::vector<uint32_t> ns_lab_off{0}, ns_lab_key, ns_lab_val;
+  // Pods, in Resources.Pods order
+  std::vector<uint32_t> pod_ns, pod_name, pod_ip;
+  std::vector<uint32_t> pod_lab_off{0}, lab_key, lab_val;  // a Go map: duplicate keys, if given, last wins
+  std::vector<uint32_t> pod_cont_off{0};
   std::vector<Container> conts;
-};
-struct Resources {  // probe.Resources (resources.go:15-19)
-  std::map<std::string, std::optional<std::map<std::string, std::string>>> namespaces;
-  std::vector<Pod> pods;
+  size_t pods() const { return pod_ns.size(); }
+  uint32_t n_conts(size_t p) const { return pod_cont_off[p + 1] - pod_cont_off[p]; }
+  const Container& cont(size_t p, uint32_t i) const { return conts[pod_cont_off[p] + i]; }
+  const std::string& s(uint32_t id) const { return str[id]; }
+  std::string pod_string(size_t p) const { return str[pod_ns[p]] + "/" + str[pod_name[p]]; }  // PodString
 };
 struct ProbeConfig {  // generator.ProbeConfig (AllAvailable | PortProtocol)
   bool all_available = false;
@@ -137,7 +169,11 @@ struct ProbeConfig {  // generator.ProbeConfig (AllAvailable | PortProtocol)
 };
 
 Resources load_resources(const json::Node& n);
+// The flat tables of include/cyclonus_hip.h, validated (a bad index or offset throws Panic{CYC_ERR_ARG}).
+Resources load_resources_tables(const cyc_resource_tables& t);
+std::string dump_resources(const Resources& r);  // json.Marshal(*probe.Resources) of the kept fields
 std::vector<ProbeConfig> load_probes(const json::Node& n);
+std::vector<ProbeConfig> load_probe_configs(const cyc_probe_config* cfgs, int64_t n);
 
 // A batched problem's block (cyc_probe_prepare_blocks): pods [p0, p1) of the Resources form an
 // independent probe problem answering probe config `cfg` only, over its own pods only.
@@ -164,7 +200,7 @@ struct Problem {
   // pods
   std::vector<uint32_t> pod_ns, pod_ls, pod_nsls;
   std::vector<DIP> pod_ip;
-  std::vector<std::string> pod_ip_str, pod_key;  // pod IP strings (messages), "ns/name"
+  std::vector<std::string> pod_ip_str;  // pod IP strings (panic messages; only the unparsable ones are kept)
   // CIDRs / IP blocks
   std::vector<DCidr> cidrs;
   std::vector<std::string> cidr_str;

@@ -65,6 +65,42 @@ class Engine:
         check(self._ctx, lib().cyc_resources_load_json(self._ctx, b, len(b)))
         return self
 
+    # ---------------------------------------------------------------- flat tables (no JSON)
+    def load_resources_tables(self, tables) -> "Engine":
+        """cyc_resources_load: a flat.ResourceTables (or a probe.Resources dict, flattened here)."""
+        from . import flat
+
+        t = tables if isinstance(tables, flat.ResourceTables) else flat.ResourceTables(tables)
+        check(self._ctx, lib().cyc_resources_load(self._ctx, ctypes.byref(t.c)))
+        return self
+
+    def load_policy_tables(self, tables) -> "Engine":
+        """cyc_policy_load: a flat.PolicyTables (or a json.Marshal(*matcher.Policy) dict, flattened here)."""
+        from . import flat
+
+        t = tables if isinstance(tables, flat.PolicyTables) else flat.PolicyTables(tables)
+        check(self._ctx, lib().cyc_policy_load(self._ctx, ctypes.byref(t.c)))
+        return self
+
+    def prepare_configs(self, probes) -> dict:
+        """cyc_probe_prepare_configs: the probe configs as cyc_probe_config structs."""
+        from . import flat
+
+        cfg = probes if isinstance(probes, flat.ProbeConfigs) else flat.ProbeConfigs(probes)
+        sh = _lib.ProbeShape()
+        check(self._ctx, lib().cyc_probe_prepare_configs(self._ctx, cfg.c, cfg.n, ctypes.byref(sh)))
+        self.shape = sh.as_dict()
+        return self.shape
+
+    def resources_json(self) -> dict:
+        """The loaded probe model (cyc_resources_json: json.Marshal(*probe.Resources) of the kept fields)."""
+        n = lib().cyc_resources_json(self._ctx, None, 0)
+        if n < 0:
+            raise _lib.CyclonusError(_lib.ERR_ARG, "no resources loaded")
+        buf = ctypes.create_string_buffer(int(n))
+        lib().cyc_resources_json(self._ctx, buf, int(n))
+        return json.loads(buf.value.decode())
+
     def prepare(self, probes) -> dict:
         b = _bytes(probes)
         sh = _lib.ProbeShape()

@@ -101,6 +101,101 @@ int cyc_resources_load_json(cyc_ctx* ctx, const char* resources_json, size_t len
  * flattens + uploads all tables and allocates device scratch.  Fills *shape. */
 int cyc_probe_prepare(cyc_ctx* ctx, const char* probes_json, size_t len, cyc_probe_shape* shape);
 
+/* ---- Flat-table ingestion (no JSON): what a cgo binding passes straight from its Go values.
+ * Every string is an index into one string table (duplicates allowed); maps and lists are
+ * [n + 1] offset arrays into shared element arrays; optional arrays may be NULL.  The caller keeps
+ * ownership: everything is copied during the call (cgo rule: no Go pointer is retained).  Indices
+ * and offsets are validated (CYC_ERR_ARG names the first bad one). */
+typedef struct {
+  int64_t n;           /* strings */
+  const char* bytes;   /* their bytes, concatenated (Go strings: any bytes, NUL included) */
+  const int64_t* off;  /* [n + 1]: string i = bytes[off[i], off[i + 1]) */
+} cyc_strings;
+
+/* probe.Resources (pkg/connectivity/probe/resources.go:15-19, pod.go:44-51,173-179) */
+typedef struct {
+  cyc_strings str;
+  /* Namespaces map[string]map[string]string */
+  int64_t n_namespaces;
+  const int32_t* ns_name;        /* [n_namespaces] the map key */
+  const uint8_t* ns_nil;         /* [n_namespaces] 1: a nil label map (optional) */
+  const int64_t* ns_label_off;   /* [n_namespaces + 1] into ns_label_key / ns_label_val */
+  const int32_t *ns_label_key, *ns_label_val;
+  /* Pods []*Pod, in order */
+  int64_t n_pods;
+  const int32_t *pod_ns, *pod_name, *pod_ip;  /* [n_pods] Namespace, Name, IP */
+  const int64_t* pod_label_off;  /* [n_pods + 1] into label_key / label_val (Labels map) */
+  const int32_t *label_key, *label_val;
+  const int64_t* pod_cont_off;   /* [n_pods + 1] into the container arrays (Containers) */
+  const int32_t *cont_name, *cont_port, *cont_proto, *cont_port_name;  /* Name, Port, Protocol, PortName */
+} cyc_resource_tables;
+
+/* generator.ProbeConfig (pkg/generator/probeconfig.go): AllAvailable, or PortProtocol{Port intstr, Protocol} */
+typedef struct {
+  int32_t all_available;  /* 1: one job per destination container (resources.go:336-364) */
+  int32_t port_is_name;   /* intstr.Type: 0 Int (port), 1 String (port_name) */
+  int32_t port;
+  const char* port_name;  /* NUL-terminated; NULL = "" */
+  const char* protocol;   /* NUL-terminated raw protocol string (compared as is: "tcp" != "TCP"); NULL = "" */
+} cyc_probe_config;
+
+/* *matcher.Policy after BuildNetworkPolicies (+ Simplify) (pkg/matcher/policy.go:11-14,
+ * target.go:11-23, peermatcher.go, podpeermatcher.go, ippeermatcher.go, portmatcher.go): the already
+ * built Go policy, flattened.  Targets are given per direction (ingress then egress); each holds its
+ * ordered peer list; a peer's port matcher is an index (peers of one rule may share one). */
+typedef enum { CYC_PEER_ALL = 0, CYC_PEER_PORTS = 1, CYC_PEER_POD = 2, CYC_PEER_IP = 3 } cyc_peer_kind;
+typedef enum { CYC_NS_EXACT = 0, CYC_NS_ALL = 1, CYC_NS_LABEL = 2 } cyc_ns_kind;
+typedef enum { CYC_PORT_ANY = 0, CYC_PORT_NUMBER = 1, CYC_PORT_NAME = 2 } cyc_port_kind;
+typedef struct {
+  cyc_strings str;
+  /* metav1.LabelSelector: MatchLabels, then MatchExpressions {Key, Operator, Values} */
+  int64_t n_selectors;
+  const int64_t* sel_label_off;  /* [n_selectors + 1] into sel_label_key / sel_label_val */
+  const int32_t *sel_label_key, *sel_label_val;
+  const int64_t* sel_expr_off;   /* [n_selectors + 1] into expr_key / expr_op / expr_value_off */
+  const int32_t *expr_key, *expr_op;  /* expr_op: the operator text ("In", "NotIn", "Exists", "DoesNotExist";
+                                         anything else panics when reached, labelselector.go:57) */
+  const int64_t* expr_value_off; /* [n_exprs + 1] into expr_value */
+  const int32_t* expr_value;
+  /* PortMatcher: AllPortMatcher, or SpecificPortMatcher{Ports, PortRanges} */
+  int64_t n_port_matchers;
+  const uint8_t* pm_all;         /* [n_port_matchers] 1: AllPortMatcher */
+  const uint8_t *pm_ports_nil, *pm_ranges_nil;  /* optional: nil slices (json.Marshal fidelity only) */
+  const int64_t* pm_port_off;    /* [n_port_matchers + 1] into port_* (PortProtocolMatcher) */
+  const uint8_t* port_kind;      /* cyc_port_kind: Port == nil / number / name */
+  const int32_t* port_value;     /* the number, or the name's string index */
+  const int32_t* port_proto;     /* Protocol string index */
+  const int64_t* pm_range_off;   /* [n_port_matchers + 1] into range_* (PortRangeMatcher) */
+  const int32_t *range_from, *range_to, *range_proto;
+  /* targets: n_targets[0] ingress, then n_targets[1] egress, each direction sorted or not (the
+   * library orders them by primary key, target.go:57-62, as Go's map keys) */
+  int64_t n_targets[2];
+  const int32_t* target_ns;      /* Namespace string index */
+  const int32_t* target_sel;     /* PodSelector: selector index */
+  const uint8_t* target_peers_nil; /* optional: Peers == nil (json.Marshal fidelity only) */
+  const int64_t* target_peer_off;  /* [n_in + n_eg + 1] into peer_* (ordered: Target.Allows short-circuits) */
+  const int64_t* target_rule_off;  /* optional [n_in + n_eg + 1] into rule_name (SourceRules' names) */
+  const int32_t* rule_name;
+  /* peers */
+  const uint8_t* peer_kind;      /* cyc_peer_kind */
+  const int32_t* peer_port;      /* port matcher index (ignored for CYC_PEER_ALL) */
+  const uint8_t* peer_ns_kind;   /* cyc_ns_kind (pod peers) */
+  const int32_t* peer_ns;        /* CYC_NS_EXACT: namespace string index; CYC_NS_LABEL: selector index */
+  const int32_t* peer_pod_sel;   /* pod peers: selector index, -1 = all pods */
+  const int32_t* peer_cidr;      /* IP peers: CIDR string index */
+  const int64_t* peer_except_off;  /* [n_peers + 1] into except_cidr (IP peers' Except) */
+  const uint8_t* peer_except_nil;  /* optional: Except == nil (json.Marshal fidelity only) */
+  const int32_t* except_cidr;
+} cyc_policy_tables;
+
+/* the flat counterparts of cyc_resources_load_json, cyc_policy_load_ir_json and cyc_probe_prepare */
+int cyc_resources_load(cyc_ctx* ctx, const cyc_resource_tables* tables);
+int cyc_policy_load(cyc_ctx* ctx, const cyc_policy_tables* tables);
+int cyc_probe_prepare_configs(cyc_ctx* ctx, const cyc_probe_config* configs, int64_t n, cyc_probe_shape* shape);
+/* the loaded probe model as json.Marshal(*probe.Resources) would write it (Pod.ServiceIP and
+ * Container.BatchJobs are not kept); returns bytes needed (+1), as cyc_policy_ir_json */
+int64_t cyc_resources_json(cyc_ctx* ctx, char* buf, size_t cap);
+
 /* Compute the verdict planes on the GPU for target-pod rows [row_lo, row_hi) (rows are pods in
  * Resources.Pods order; pass 0, P for the whole table).  Device pointers; `hip_stream` is the
  * hipStream_t to enqueue on (NULL = the HIP default stream, as with every HIP API).  Asynchronous

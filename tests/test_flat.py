@@ -1,0 +1,95 @@
+"""Flat-table ingestion on the CPU (include/cyclonus_hip.h cyc_resources_load / cyc_policy_load /
+cyc_probe_prepare_configs): the tables a cgo binding passes without JSON load the same probe model and
+the same compiled policy as the JSON entry points, and malformed tables are refused with CYC_ERR_ARG."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+from cyclonus_amd import _lib, flat
+from cyclonus_amd.engine import Engine
+from randgen import random_problem
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _both(res):
+    a = Engine(0).load_resources(res).resources_json()
+    b = Engine(0).load_resources_tables(res).resources_json()
+    return a, b
+
+
+def test_resources_tables_equal_json_random():
+    for seed in range(60):
+        _, res, _ = random_problem(7000 + seed, dups=seed % 2 == 0)
+        a, b = _both(res)
+        assert a == b, seed
+
+
+def test_resources_tables_equal_json_config1_and_edges():
+    res = json.load(open(os.path.join(ROOT, "tests", "golden", "config1.json")))["resources"]
+    a, b = _both(res)
+    assert a == b
+    edge = {"Namespaces": {"x": None, "y": {}, "z": {"k": ""}},
+            "Pods": [{"Namespace": "x", "Name": "a", "Labels": None, "IP": "", "Containers": None},
+                     {"Namespace": "x/y", "Name": "é\u0000b", "Labels": {"": ""}, "IP": "::1",
+                      "Containers": [{"Name": "c", "Port": -5, "Protocol": "tcp", "PortName": ""}]}]}
+    a, b = _both(edge)
+    assert a == b
+    assert a["Namespaces"]["x"] is None and a["Pods"][1]["Name"] == "é\u0000b"
+
+
+def test_policy_tables_roundtrip():
+    """json.Marshal(*Policy) -> flat tables -> cyc_policy_load -> the same IR (targets, ordered peers,
+    shared and range port matchers, selectors with expressions, IPBlocks with nil / empty excepts)."""
+    for seed in range(80):
+        pols, _, _ = random_problem(8000 + seed)
+        e = Engine(0).build_policies(pols)
+        ir = e.policy_ir()
+        got = Engine(0).load_policy_tables(ir).policy_ir()
+        assert got == ir, seed
+
+
+def test_probe_configs():
+    pc = flat.ProbeConfigs([{"Port": 80, "Protocol": "TCP"}, {"Port": "serve-81-udp", "Protocol": "UDP"},
+                            {"AllAvailable": True}, {"PortProtocol": {"Port": 53, "Protocol": "sctp"}}])
+    assert pc.n == 4
+    assert (pc.c[0].port, pc.c[0].port_is_name, pc.c[0].protocol) == (80, 0, b"TCP")
+    assert (pc.c[1].port_is_name, pc.c[1].port_name) == (1, b"serve-81-udp")
+    assert pc.c[2].all_available == 1
+    assert (pc.c[3].port, pc.c[3].protocol) == (53, b"sctp")
+
+
+def test_malformed_tables_refused():
+    res = {"Namespaces": {"x": {"a": "b"}}, "Pods": [{"Namespace": "x", "Name": "p", "IP": "10.0.0.1",
+                                                      "Labels": {"a": "b"}, "Containers": []}]}
+    e = Engine(0)
+
+    def load(mutate):
+        t = flat.ResourceTables(res)
+        mutate(t.c)
+        return _lib.lib().cyc_resources_load(e._ctx, ctypes.byref(t.c)), _lib.lib().cyc_last_error(e._ctx).decode()
+
+    bad = np.array([99], np.int32)
+    rc, msg = load(lambda c: setattr(c, "pod_ns", bad.ctypes.data_as(flat.i32p)))
+    assert rc == _lib.ERR_ARG and "pod_ns[0]" in msg and "out of range" in msg
+    dec = np.array([0, 2, 1], np.int64)
+    rc, msg = load(lambda c: (setattr(c, "n_pods", 2), setattr(c, "pod_label_off", dec.ctypes.data_as(flat.i64p))))
+    assert rc == _lib.ERR_ARG and "decreases" in msg
+    rc, msg = load(lambda c: setattr(c, "pod_ns", None))
+    assert rc == _lib.ERR_ARG and "null pod_ns" in msg
+    # a refused load leaves the earlier model in place
+    e.load_resources(res)
+    rc, _ = load(lambda c: setattr(c, "pod_ip", bad.ctypes.data_as(flat.i32p)))
+    assert rc == _lib.ERR_ARG and e.resources_json()["Pods"][0]["IP"] == "10.0.0.1"
+    # policy tables: a peer's port matcher out of range, duplicate primary keys
+    ir = Engine(0).build_policies(random_problem(8100)[0]).policy_ir()
+    t = flat.PolicyTables(ir)
+    t.c.n_port_matchers = 0
+    assert _lib.lib().cyc_policy_load(e._ctx, ctypes.byref(t.c)) == _lib.ERR_ARG
+    one = {"Ingress": {"a": {"Namespace": "x", "PodSelector": {}, "Peers": None, "SourceRules": []},
+                       "b": {"Namespace": "x", "PodSelector": {}, "Peers": None, "SourceRules": []}}, "Egress": {}}
+    with pytest.raises(_lib.CyclonusError, match="primary key"):
+        Engine(0).load_policy_tables(one)
