@@ -664,7 +664,11 @@ struct DWordIP {
   uint32_t min4, max4;         // over the word's IPv4 pods
   uint64_t m4, m6;             // bits of the IPv4 / IPv6 pods
   uint32_t min6[4], max6[4];   // over the word's IPv6 pods (big-endian 128-bit)
-  uint64_t pad;
+  // per family (v4: bits 0-7, v6: bits 8-15): bit 7 set when the family's pods of the word have
+  // AFFINE addresses — the pod in lane i holds min + (i - first), first = bits 0-5 = the lowest lane of
+  // the family (addresses handed out in pod order); a network then covers a lane range computed from
+  // its bounds, no per-pod address load (word records of chunks: 0)
+  uint32_t aff, pad;
 };
 static_assert(sizeof(DWordIP) == 64, "DWordIP is one 64-byte record");
 
@@ -701,6 +705,44 @@ __device__ __forceinline__ uint32_t span_vs_cidr6(const uint32_t* mn, const uint
 // none stores no PM word at all, any other chunk stores all 64.  Readers issue the PM and cnz loads
 // together and drop the PM word of an all-zero chunk, so the zero chunks — most of a row — cost
 // no HBM writes.
+// Lanes of a word whose pods of family `v4` hold addresses in network c, when those addresses are
+// affine in the lane (DWordIP::aff): lane i holds min + (i - first), so the network's bounds
+// [lo, hi] give the lane range [first + (lo - min), first + (hi - min)] clamped to the word.  Both
+// differences are taken only where the bound lies in [min, max] (a span under 64), so 64-bit
+// arithmetic on the low words is exact for IPv6 too.
+__device__ __forceinline__ uint64_t lanes_in_range(uint32_t first, uint32_t span, uint64_t lo_off, bool lo_below, bool lo_above,
+                                                   uint64_t hi_off, bool hi_below, bool hi_above) {
+  // lo_below: lo <= min (range starts at the first lane); lo_above: lo > max (no lane)
+  // hi_above: hi >= max (range ends at the last lane); hi_below: hi < min (no lane)
+  if (lo_above || hi_below) return 0ull;
+  const uint32_t a = lo_below ? first : first + uint32_t(lo_off);
+  const uint32_t b = hi_above ? first + span : first + uint32_t(hi_off);
+  if (b < a) return 0ull;
+  const uint64_t upto = b >= 63 ? ~0ull : ((1ull << (b + 1)) - 1);
+  return upto & ~((1ull << a) - 1);
+}
+__device__ __forceinline__ uint64_t affine_lanes4(const DWordIP& wd, const DCidr& c) {
+  const uint32_t lo = c.net[3] & c.mask[3], hi = lo | ~c.mask[3];
+  const uint32_t first = wd.aff & 63u;
+  return lanes_in_range(first, wd.max4 - wd.min4, uint64_t(lo - wd.min4), lo <= wd.min4, lo > wd.max4, uint64_t(hi - wd.min4),
+                        hi < wd.min4, hi >= wd.max4);
+}
+__device__ __forceinline__ uint64_t low64(const uint32_t* x) { return (uint64_t(x[2]) << 32) | x[3]; }
+__device__ __forceinline__ uint64_t affine_lanes6(const DWordIP& wd, const DCidr& c) {
+  uint32_t lo[4], hi[4];
+  for (int i = 0; i < 4; i++) {
+    lo[i] = c.net[i] & c.mask[i];
+    hi[i] = lo[i] | ~c.mask[i];
+  }
+  const uint32_t first = (wd.aff >> 8) & 63u;
+  const uint64_t mn = low64(wd.min6), mx = low64(wd.max6);
+  return lanes_in_range(first, uint32_t(mx - mn), low64(lo) - mn, !lt128(wd.min6, lo), lt128(wd.max6, lo), low64(hi) - mn,
+                        lt128(hi, wd.min6), !lt128(hi, wd.max6));
+}
+
+#ifndef CYC_IP_AFFINE
+#define CYC_IP_AFFINE 1  // 0: every straddling word tested a pod per lane (the affine-address lane ranges off)
+#endif
 #ifndef CYC_IP_MIXB
 #define CYC_IP_MIXB 1  // straddling words of an IP row whose pod addresses are loaded at once (2: config #4 launch B +4 us)
 #endif
@@ -714,7 +756,15 @@ __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, c
   if (valid) {
     const bool v4 = t.cidr.fam == 4;
     const uint64_t fm = v4 ? wd.m4 : wd.m6;  // pods of the network's family; the others never match
-    if (fm) {
+    if (fm && ((wd.aff >> (v4 ? 7 : 15)) & 1u)) {
+      // affine addresses: the network and each except of its family are lane ranges (ipaddress.go:22-40:
+      // in the CIDR and in none of the excepts)
+      res = fm & (v4 ? affine_lanes4(wd, t.cidr) : affine_lanes6(wd, t.cidr));
+      for (uint32_t e = 0; e < t.excnt && res; e++) {
+        const DCidr x = ex[e];
+        if (x.fam == t.cidr.fam) res &= ~(v4 ? affine_lanes4(wd, x) : affine_lanes6(wd, x));
+      }
+    } else if (fm) {
       uint32_t pos = v4 ? span_vs_cidr4(wd.min4, wd.max4, t.cidr) : span_vs_cidr6(wd.min6, wd.max6, t.cidr);
       if (pos == 2) uniform = false;
       else if (pos == 1) {
@@ -3597,19 +3647,44 @@ static void prepare_device(cyc_ctx* c) {
         DWordIP d{};
         d.min4 = 0xFFFFFFFFu;
         for (int i = 0; i < 4; i++) d.min6[i] = 0xFFFFFFFFu;
+        // affine check per family: every pod of the family at lane i holds base + i (128-bit, big-endian
+        // words; v4 in w[3]) for one base (DWordIP::aff)
+        bool aff[2] = {true, true};
+        int first[2] = {-1, -1};
+        uint32_t base[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
         for (uint32_t q = w * 64; q < std::min<uint32_t>(pb.P, w * 64 + 64); q++) {
           const DIP& ip = pb.pod_ip[q];
           if (!ip.valid) continue;  // only with may_err, where the fast kernel is not used
+          const uint32_t lane = q - w * 64;
+          const int f = ip.fam == 4 ? 0 : 1;
+          uint32_t a[4] = {f ? ip.w[0] : 0u, f ? ip.w[1] : 0u, f ? ip.w[2] : 0u, ip.w[3]};
+          // b = a - lane (128-bit): the pod's base
+          uint32_t b[4];
+          uint64_t borrow = lane;
+          for (int i = 3; i >= 0; i--) {
+            const uint64_t v = uint64_t(a[i]) - borrow;
+            b[i] = uint32_t(v);
+            borrow = (v >> 63) & 1u;  // went below zero
+          }
+          if (borrow) aff[f] = false;  // address < lane: no base (never affine)
+          if (first[f] < 0) {
+            first[f] = int(lane);
+            std::copy(b, b + 4, base[f]);
+          } else if (!std::equal(b, b + 4, base[f])) {
+            aff[f] = false;
+          }
           if (ip.fam == 4) {
-            d.m4 |= 1ull << (q - w * 64);
+            d.m4 |= 1ull << lane;
             d.min4 = std::min(d.min4, ip.w[3]);
             d.max4 = std::max(d.max4, ip.w[3]);
           } else {
-            d.m6 |= 1ull << (q - w * 64);
+            d.m6 |= 1ull << lane;
             if (std::lexicographical_compare(ip.w, ip.w + 4, d.min6, d.min6 + 4)) std::copy(ip.w, ip.w + 4, d.min6);
             if (std::lexicographical_compare(d.max6, d.max6 + 4, ip.w, ip.w + 4)) std::copy(ip.w, ip.w + 4, d.max6);
           }
         }
+        for (int f = 0; f < 2; f++)
+          if (first[f] >= 0 && aff[f] && CYC_IP_AFFINE) d.aff |= (uint32_t(first[f]) | 0x80u) << (8 * f);
         wi[w] = d;
       }
       for (uint32_t ch = 0; ch < NC; ch++) {
