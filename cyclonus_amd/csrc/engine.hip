@@ -368,10 +368,7 @@ struct DWordNS {
 // labelled apart, e.g. a `pod: <name>` label): then the identity-space outcomes cost as much as
 // this and the run expansion above loops over up to 64 runs per word.
 // Words [w0, w0 + nw) of each row (a source shard's ingress peers: its word window).
-#ifndef CYC_PR_DIRECT_G
-#define CYC_PR_DIRECT_G 4  // pod peers per wave of the direct pod-peer rows
-#endif
-constexpr uint32_t PR_DIRECT_G = CYC_PR_DIRECT_G;
+constexpr uint32_t PR_DIRECT_G = 4;  // pod peers per wave of the direct pod-peer rows
 // Wave = (PR_DIRECT_G pod peers, one 64-pod word), lane = pod: the word's pod identities (pod ->
 // identity -> namespace, namespace labels, labels) are loaded once for the group, then every
 // peer's two matcher bytes at once, one ballot per peer.
@@ -436,10 +433,7 @@ __global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P
 // (their loads in flight together).  Rows are stored chunk-dense with their nonzero word span and chunk masks,
 // exactly like the IP rows (ip_row_word), so the class rows skip their zero chunks: with every pod
 // labelled apart (identities ~ pods) most pod-peer rows are a namespace's worth of words.
-#ifndef CYC_PR_WB
-#define CYC_PR_WB 8
-#endif
-constexpr uint32_t PR_WB = CYC_PR_WB;  // words evaluated at once per wave
+constexpr uint32_t PR_WB = 8;  // words evaluated at once per wave
 
 // Word masks of pod peer pr over chunk `chunk` (this lane's word w): the namespace outcome per word
 // first, then a pod per lane for the words it leaves open — only those of rank part, part + parts,
@@ -743,10 +737,7 @@ __device__ __forceinline__ uint64_t affine_lanes6(const DWordIP& wd, const DCidr
 #ifndef CYC_IP_AFFINE
 #define CYC_IP_AFFINE 1  // 0: every straddling word tested a pod per lane (the affine-address lane ranges off)
 #endif
-#ifndef CYC_IP_MIXB
-#define CYC_IP_MIXB 1  // straddling words of an IP row whose pod addresses are loaded at once (2: config #4 launch B +4 us)
-#endif
-constexpr uint32_t IP_MIXB = CYC_IP_MIXB;
+constexpr uint32_t IP_MIXB = 1;  // straddling words of an IP row whose pod addresses are loaded at once (2: config #4 launch B +4 us)
 __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
                                             const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
                                             uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng,
@@ -861,7 +852,7 @@ __device__ __forceinline__ uint64_t cnz_mask(const uint32_t* __restrict__ cnz, u
 // word): the group's tests and their except records are staged into LDS once (one coalesced load
 // per block, instead of a chain of dependent scalar loads per peer and except), and each wave loads
 // its words' [min, max] records once for the whole group.
-constexpr uint32_t IP_GROUP = 16, IP_GROUP_MAX = 64, IP_EX_LDS = 256;  // 16: profiles/r02_ip_group_ab.txt
+constexpr uint32_t IP_GROUP = 16, IP_GROUP_MAX = 64, IP_EX_LDS = 256;  // IP peers per block (profiles/r02_ip_group_ab.txt)
 // Chunks [c0, c0 + nch) of the rows (a source shard's ingress peers: the chunks of its word window).
 __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
@@ -1285,13 +1276,9 @@ constexpr uint32_t IDO_LDS_BYTES = 48 * 1024;  // staged identity sets per class
 // peers): the identities' (namespace, namespace labels, labels) are loaded once and the group's
 // outcomes (podpeermatcher.go:21-28: namespace then pod matcher) are independent selres gathers;
 // one ballot per peer -> IDOB (no-panic runs only).
-#ifndef CYC_PB_GROUP
-#define CYC_PB_GROUP 16  // pod peers per identity-set wave (8: +4 % launch B, profiles/r02_pb_group_ab.txt)
-#endif
-constexpr uint32_t PB_GROUP = CYC_PB_GROUP;
-#ifndef CYC_PB_HALF
-#define CYC_PB_HALF 4  // pod peers whose selector loads are in flight together (8: k_front_b 61 -> 81 VGPRs)
-#endif
+constexpr uint32_t PB_GROUP = 16;  // pod peers per identity-set wave (8: +4 % launch B, profiles/r02_pb_group_ab.txt)
+// pod peers whose selector loads are in flight together (8: k_front_b 61 -> 81 VGPRs)
+constexpr uint32_t PB_HALF_MAX = 4;
 // Identity words [ew0, ew0 + new) of the rows only (a source shard's ingress peers: the words of the
 // egress identities its sources have).
 __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
@@ -1312,7 +1299,7 @@ __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t 
   // so the loads of all of them are in flight together instead of one dependent chain per peer
   // (podpeermatcher.go:21-28 namespace then pod matcher; no panic on this path, so both matchers
   // can be evaluated for every peer and combined)
-  constexpr uint32_t PB_HALF = PB_GROUP < CYC_PB_HALF ? PB_GROUP : CYC_PB_HALF;
+  constexpr uint32_t PB_HALF = PB_GROUP < PB_HALF_MAX ? PB_GROUP : PB_HALF_MAX;
 #pragma unroll
   for (uint32_t h = 0; h < PB_GROUP; h += PB_HALF) {
     uint32_t nk[PB_HALF], nv[PB_HALF], ps[PB_HALF];
@@ -1392,10 +1379,7 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
 // walk dominates this launch on row shards, where few classes leave the chip mostly idle).
 // Classes with more than CI_LDS peers walk the targets directly.
 constexpr uint32_t CI_LDS = 128;
-#ifndef CYC_CI_G
-#define CYC_CI_G 4  // identity sets: job slots (ingress) / descriptors (egress) per wave
-#endif
-constexpr int CI_G = CYC_CI_G;
+constexpr int CI_G = 4;  // identity sets: job slots (ingress) / descriptors (egress) per wave
 template <bool EGRESS, int G>
 __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   __shared__ uint32_t s_j[4][CI_LDS];
@@ -1584,10 +1568,7 @@ __device__ __forceinline__ uint64_t port_mask(const RowArgs& a, const uint8_t* p
     if (pok[d]) okm |= dm[uint64_t(d) * a.W];
   return okm;
 }
-#ifndef CYC_PEER_BATCH
-#define CYC_PEER_BATCH 4
-#endif
-constexpr uint32_t PEER_BATCH = CYC_PEER_BATCH;  // IDO class rows: IP peers whose PM words are loaded at once
+constexpr uint32_t PEER_BATCH = 4;  // IDO class rows: IP peers whose PM words are loaded at once
 
 template <bool EGRESS, bool ERR, int KC>
 __device__ __forceinline__ void class_row_word(const RowArgs& a, uint32_t i, uint32_t kc, uint32_t w, uint32_t w0) {
@@ -1708,17 +1689,9 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
 // (peermatcher.go:18) allows every valid cell; no matching target allows (policy.go:158-160).
 // Lists longer than the LDS part spill into the identity's ip_list slot (sized for every peer of
 // its namespace's targets).
-#ifndef CYC_PL_BATCH
-#define CYC_PL_BATCH 8  // list entries whose PM words are loaded at once (16: occupancy 6 -> 4)
-#endif
-#ifndef CYC_PL_WAVE
-#define CYC_PL_WAVE 1  // class rows a wave per 64-word chunk (pl_wave_chunks) where it applies
-#endif
-constexpr bool PL_WAVE = CYC_PL_WAVE != 0;
-#ifndef CYC_PL_THREADS
-#define CYC_PL_THREADS 128  // threads per class-row block (one representative per block)
-#endif
-constexpr uint32_t PL_LDS = 256, PL_TGT = 64, PL_BATCH = CYC_PL_BATCH, PL_THREADS = CYC_PL_THREADS;
+// PL_BATCH: list entries whose PM words are loaded at once (16: occupancy 6 -> 4); PL_THREADS: threads
+// per class-row block (one representative per block)
+constexpr uint32_t PL_LDS = 256, PL_TGT = 64, PL_BATCH = 8, PL_THREADS = 128;
 constexpr uint32_t PL_SKIP = 0xFFFFFFFEu, PL_ONES = 0xFFFFFFFFu;  // entry rows: zero row / PortsForAllPeers
 constexpr uint32_t PL_IP = 0x80000000u;
 
@@ -1756,13 +1729,7 @@ struct PlShared {  // one per block, shared by both directions' instantiations o
   int32_t rdu[32];  // ingress, K <= 32: the representative's job descriptor per slot (-1: slot not VALID)
 };
 
-#ifndef CYC_PL_ITEMS
-#define CYC_PL_ITEMS 1
-#endif
-constexpr int PL_ITEMS = CYC_PL_ITEMS;
-#ifndef CYC_PL_WAVES
-#define CYC_PL_WAVES  // e.g. __attribute__((amdgpu_waves_per_eu(8, 8))) for A/Bs
-#endif
+constexpr int PL_ITEMS = 1;
 
 // PL_ITEMS (slot chunk, pod word) items of class representative i: items it0, it0 + blockDim.x, ...
 template <bool EGRESS>
@@ -1891,11 +1858,10 @@ __device__ __forceinline__ void pl_items(const RowArgs& a, const PlShared& sh, c
 // in flight together, then ORed into an accumulator per descriptor (egress) or slot (ingress)
 // bit.  The accumulators become the class rows through each word's slot descriptor (DESCW; the DM
 // masks for mixed words).
-#ifndef CYC_PL_WBATCH
-#define CYC_PL_WBATCH 4  // PM words in flight per wave-per-chunk batch (8: 78 VGPRs, config #4 class rows +7 us: profiles/r03_front_b_d_ab.txt)
-#endif
 
-constexpr uint32_t PL_WBATCH = CYC_PL_WBATCH, PL_NB = 4;
+// PL_WBATCH: PM words in flight per wave-per-chunk batch (8: 78 VGPRs, config #4 class rows +7 us:
+// profiles/r03_front_b_d_ab.txt)
+constexpr uint32_t PL_WBATCH = 4, PL_NB = 4;
 // An entry's lane fields for the wave-per-chunk rows: row, port bits, mask of the 64-word chunks
 // holding a nonzero PM word of it (IP rows: from the IP-row pass; other rows: all)
 struct PlLane {
@@ -2643,7 +2609,7 @@ __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
 }
 // PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
 template <bool WAVE>
-__global__ __launch_bounds__(256) CYC_PL_WAVES void k_front_d_pm(FrontRows f) {
+__global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
   __shared__ PlShared sh;
   const uint32_t b = blockIdx.x;
   if (b < f.nb[1]) class_rows_pl_blk<true, WAVE>(f.ra[1], sh, b, f.nb[1]);
@@ -2652,35 +2618,12 @@ __global__ __launch_bounds__(256) CYC_PL_WAVES void k_front_d_pm(FrontRows f) {
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
 // tail is made of the shorter ingress blocks (4 job slots per thread: profiles/r01_front_e_kc_ab.txt)
-#ifndef CYC_E_WAVES
-#define CYC_E_WAVES  // e.g. __attribute__((amdgpu_waves_per_eu(6))) for A/Bs
-#endif
-#ifndef CYC_E_KC
-#define CYC_E_KC 4  // job slots per thread in the fused IDO class rows (k_front_e)
-#endif
-constexpr int E_KC = CYC_E_KC;
-#ifndef CYC_UNI_DESC  // egress class rows with one descriptor per slot when every pod shares it
-#define CYC_UNI_DESC 1
-#endif
-#ifndef CYC_E_SPLIT
-#define CYC_E_SPLIT 1  // 1: launch E as one kernel per direction (k_class_rows_ido, each at its own register
-                       // budget: egress 101 VGPRs, ingress 61) instead of k_front_e (both at 101): config #3
-                       // 189 -> 170 us (profiles/r03_e_split_ab.txt)
-#endif
-#ifndef CYC_E_UNI_FUSED
-#define CYC_E_UNI_FUSED 1  // egress with one descriptor per slot: both directions' class rows in one launch (k_front_e_uni;
-                           // config #3 132 -> 124 us, profiles/r03_ido_rows_ab.txt)
-#endif
+constexpr int E_KC = 4;  // job slots per thread in the IDO class rows of the fused front
 // Launch E as one kernel when the egress rows take the one-descriptor-per-slot form (UNI): both
 // bodies then stay near 60 VGPRs, so the fused launch keeps their occupancy and saves a launch.
 __global__ __launch_bounds__(256) void k_front_e_uni(FrontRows f) {
   const uint32_t b = blockIdx.x;
   if (b < f.nb[1]) class_rows_ido_blk<true, E_KC, true>(f.ra[1], b, f.nb[1]);
-  else class_rows_ido_blk<false, E_KC>(f.ra[0], b - f.nb[1], f.nb[0]);
-}
-__global__ __launch_bounds__(256) CYC_E_WAVES void k_front_e(FrontRows f) {
-  const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_ido_blk<true, E_KC>(f.ra[1], b, f.nb[1]);
   else class_rows_ido_blk<false, E_KC>(f.ra[0], b - f.nb[1], f.nb[0]);
 }
 
@@ -3281,7 +3224,6 @@ struct cyc_ctx {
                         // from materialised PM rows (0), or IDO when every word has <= IDO_MAX_RUNS runs
   int64_t class_rpb_opt = 4;  // "class_rpb": IDO class-row representatives per block
                               // (config3 N=1 -1%: profiles/r01_class_rpb_ab.txt)
-  uint32_t ip_group = IP_GROUP;  // "ip_group": IP-peer tests per block in the IP rows
   int step_events = 0;  // "step_events": graph / eager-DAG runs record the whole-step timing events (1);
                         // off by default: the two timing events cost ~9 us of idle GPU per step
                         // (config #2 0.077 -> 0.069 ms/step, profiles/r02_step_events_ab.txt)
@@ -3731,7 +3673,7 @@ static void prepare_device(cyc_ctx* c) {
       for (uint32_t q = 0; q < pb.P && uni; q++)
         uni = pb.slot_status[size_t(q) * pb.K + k] == CYC_JOB_VALID && pb.slot_desc[size_t(q) * pb.K + k] == ud[k];
     }
-    c->uni_desc = CYC_UNI_DESC && uni;
+    c->uni_desc = uni;
     upload(c->udesc, ud);
   }
   c->portok.alloc(std::max<uint64_t>(pb.pms.size() * D, 16));
@@ -4194,7 +4136,7 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
       k_ip_rows<true><<<g, 256, 0, st>>>(Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->PM.as<uint64_t>(),
                                          c->ER.as<uint64_t>(), bat, w0, nw);
     } else {
-      const uint32_t grp = c->ip_group;
+      const uint32_t grp = IP_GROUP;
       k_ip_rows_fast<<<unsigned(ip_rows_blocks(Ri, nch, grp)), 256, 0, st>>>(
           Ri, P, W, tests, c->ip_ex.as<DCidr>(), c->pod_ip.as<DIP>(), c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>(),
           c->ip_rng.as<uint32_t>(), ip_cnz(c), grp, c0, nch);
@@ -4301,7 +4243,7 @@ static RowArgs row_args(cyc_ctx* c, int d) {
 // (descriptors and slots <= PL_NB) and every peer's port bits are available.
 static bool pl_wave_ok(const cyc_ctx* c) {
   const Problem& pb = c->pb;
-  return PL_WAVE && c->pl_wave && pb.K <= PL_NB && pb.descs.size() <= PL_NB && pb.descs.size() && pb.pms.size() &&
+  return c->pl_wave && pb.K <= PL_NB && pb.descs.size() <= PL_NB && pb.descs.size() && pb.pms.size() &&
          port_bits_on(c) && pb.W <= 64 * 64;
 }
 
@@ -4342,9 +4284,7 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // shard's word window, egress rows of its sources over all words).  d_status (may be null): the
 // status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
 // in the plan; the caller then copies the status plane itself).
-#ifndef CYC_EMIT_WIDE_MIN
-#define CYC_EMIT_WIDE_MIN 16384  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
-#endif
+constexpr uint64_t EMIT_WIDE_MIN = 16384;  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
 static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out_in, uint64_t* out_eg) {
   EmitArgs ea = ea_in;
   ea.per_xcd = (ea.n_rows[0] + ea.n_rows[1] + 7) / 8;
@@ -4362,7 +4302,7 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     k_emit_wide<1024, 7><<<g, 1024, 0, st>>>(ea);
   } else if (row_bytes > 256 * 8 * 16) {  // 32-56 KB: 512 x 7 (source shards at N = 2)
     k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
-  } else if (row_bytes >= CYC_EMIT_WIDE_MIN) {  // 256-thread single pass (16-32 KB rows)
+  } else if (row_bytes >= EMIT_WIDE_MIN) {  // 256-thread single pass (16-32 KB rows)
     const uint64_t need = (ea.row_words / 2 + 255) / 256;
     if (need <= 2) k_emit_wide<256, 2><<<g, 256, 0, st>>>(ea);
     else if (need <= 4) k_emit_wide<256, 4><<<g, 256, 0, st>>>(ea);
@@ -4524,7 +4464,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.PM = c->PM.as<uint64_t>();
   fb.rng = c->ip_rng.as<uint32_t>();
   fb.cnz = ip_cnz(c);
-  fb.ip_grp = c->ip_group;
+  fb.ip_grp = IP_GROUP;
   for (int x = 0; x < 2; x++) {
     const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
     const uint32_t i0 = c->ri_off[dlo];
@@ -4623,7 +4563,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fe.ra[d].ht_clear_words = 0;
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + CI_G - 1) / CI_G) + 3) / 4);
     // egress with one descriptor per slot (udesc): only the block's slots' sets are staged
-    if (d == 1 && CYC_E_SPLIT && c->uni_desc) fe.ra[d].udesc = c->udesc.as<int32_t>();
+    if (d == 1 && c->uni_desc) fe.ra[d].udesc = c->udesc.as<int32_t>();
     const size_t per = size_t(d == 0 || fe.ra[d].udesc ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8 +
                        IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
     fe.ra[d].rpb = class_rpb(c, per);
@@ -4654,14 +4594,13 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     return true;
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
-  if (CYC_E_UNI_FUSED && fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
+  if (fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
     k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);
-  } else if (CYC_E_SPLIT) {  // the directions' class rows as two launches, each at its own register budget
+  } else {  // the directions' class rows as two launches, each at its own register budget (egress 101
+            // VGPRs, ingress 61: one launch at 101 ran config #3 189 -> 170 us, profiles/r03_e_split_ab.txt)
     if (fe.nb[1] && fe.ra[1].udesc) k_class_rows_ido<true, E_KC, true><<<fe.nb[1], 256, lds_uni, st>>>(fe.ra[1]);
     else if (fe.nb[1]) k_class_rows_ido<true, E_KC><<<fe.nb[1], 256, lds, st>>>(fe.ra[1]);
     if (fe.nb[0]) k_class_rows_ido<false, E_KC><<<fe.nb[0], 256, lds, st>>>(fe.ra[0]);
-  } else if (fe.nb[0] + fe.nb[1]) {
-    k_front_e<<<fe.nb[0] + fe.nb[1], 256, lds, st>>>(fe);
   }
   if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
   return true;
@@ -5534,7 +5473,6 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "pod_rows") range(-1, 1), c->pod_rows = int(value);
     else if (n == "member_wave") range(-1, 1), c->member_wave = int(value);
     else if (n == "class_rpb") range(1, 64), c->class_rpb_opt = value;
-    else if (n == "ip_group") range(1, 64), c->ip_group = uint32_t(value);
     else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
     else if (n == "sel_lazy") range(-1, 1), c->sel_lazy = int(value);
     else if (n == "pr_group") range(-1, 64), c->pr_group = int(value == 0 ? -1 : value);
@@ -5560,7 +5498,6 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "pod_rows") *value = c->pod_rows;
   else if (n == "member_wave") *value = c->member_wave;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
-  else if (n == "ip_group") *value = c->ip_group;
   else if (n == "pl_wave") *value = c->pl_wave;
   else if (n == "sel_lazy") *value = c->sel_lazy;
   else if (n == "pr_group") *value = c->pr_group;

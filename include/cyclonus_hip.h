@@ -329,7 +329,6 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  *   "member_wave" -1 (default: auto = 1 for <= 4096 identities) / 0 / 1: target membership with a
  *                 thread (0) or a wave (1) per pod identity
  *   "class_rpb"   4 (default, 1..64): class representatives per identity-set class-row block
- *   "ip_group"    16 (default, 1..64): IP peers per IP-row block
  *   "step_events" 0 (default) / 1: graph and fused-eager runs also record the whole-step timing
  *                 events cyc_last_timings reads (they idle the GPU ~9 us between steps)
  *   "pl_wave"     1 (default) / 0: materialised-row class rows a wave per 64-word chunk where they

@@ -1,7 +1,7 @@
 """Back-to-back step throughput (what bench.py times) under cyc_set_option settings, interleaved
 repetitions so box drift hits every setting alike.
 
-    python scripts/throughput.py config3 ip_group=4,8 [steps=20] [reps=3] [shards=N] [rank=R] [part=target|source] [init.<option>=v]
+    python scripts/throughput.py config3 pr_group=4,8 [steps=20] [reps=3] [shards=N] [rank=R] [part=target|source] [init.<option>=v]
 """
 import itertools
 import json

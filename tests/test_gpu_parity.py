@@ -261,14 +261,12 @@ def test_graph_and_eager_paths_agree(gpu):
         sh = eng.prepare(probes)
         P, K, W = sh["pods"], sh["slots"], sh["words"]
         outs = []
-        for graphs, fused, mw, pod_rows, grp in ((0, 1, -1, -1, 8), (1, 1, -1, -1, 8), (1, 1, -1, -1, 8), (2, 1, 1, 1, 3),
-                                                 (1, 0, 0, 0, 1), (2, 0, -1, 1, 64), (0, 0, 1, 0, 8), (-1, 1, 0, -1, 5),
-                                                 (-1, 0, 1, 1, 2)):
+        for graphs, fused, mw, pod_rows in ((0, 1, -1, -1), (1, 1, -1, -1), (1, 1, -1, -1), (2, 1, 1, 1), (1, 0, 0, 0),
+                                            (2, 0, -1, 1), (0, 0, 1, 0), (-1, 1, 0, -1), (-1, 0, 1, 1)):
             eng.set_option("graphs", graphs)
             eng.set_option("front_fused", fused)
             eng.set_option("member_wave", mw)
             eng.set_option("pod_rows", pod_rows)
-            eng.set_option("ip_group", grp)
             eng.set_option("class_inplace", int(graphs != 2))  # class rows in the planes or in their own buffer
             d_in = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
             d_eg = torch.full((P, K, W), 7, dtype=torch.int64, device="cuda")
@@ -664,7 +662,7 @@ def test_launch_modes_and_knobs(gpu):
     fused = not eng.shape["may_panic"]  # no-panic build: the fused front applies
     assert eng.get_option("front_fused_active") == int(fused)
     assert eng.get_option("launch") == (2 if fused else 1)
-    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("ip_group", 3), ("graphs", 1), ("graphs", -1),
+    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("graphs", 1), ("graphs", -1),
                     ("step_events", 1), ("step_events", 0), ("pr_group", 5), ("pr_group", -1), ("sel_lazy", 1),
                     ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1)):
         eng.set_option(name, v)
@@ -686,7 +684,7 @@ def test_launch_modes_and_knobs(gpu):
     assert_same(want, eng.run_host(), "DAG graph")
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
-    for name, v in (("class_rpb", 0), ("class_rpb", 65), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
+    for name, v in (("class_rpb", 0), ("class_rpb", 65), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
