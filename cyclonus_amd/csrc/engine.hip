@@ -945,6 +945,27 @@ __device__ __forceinline__ void portbits_blk(uint32_t M, uint32_t D, const uint8
   for (uint32_t e = 0; e < D; e++) bits |= portok[uint64_t(m) * D + e] ? (1u << e) : 0u;
   portbits[m] = bits;
 }
+// The same bit rows straight from the port matchers (no byte table first): launch B builds them next
+// to the byte table when there is no launch A, so the identity sets of launch D can read them.
+__device__ __forceinline__ void portbits_direct_blk(uint32_t M, uint32_t D, const DPortM* pms, const DPortEntry* pents,
+                                                    const DDesc* descs, uint32_t* __restrict__ portbits, uint32_t bid_) {
+  const uint32_t m = bid_ * 256 + threadIdx.x;
+  if (m >= M) return;
+  const DPortM pm = pms[m];
+  uint32_t bits = 0;
+  for (uint32_t e = 0; e < D; e++) {
+    const DDesc d = descs[e];
+    bool ok = pm.all != 0;
+    for (uint32_t j = 0; j < pm.ecnt && !ok; j++) {
+      const DPortEntry pe = pents[pm.eoff + j];
+      if (pe.proto != d.proto) continue;  // raw protocol string compare ("tcp" != "TCP")
+      ok = pe.kind == PE_PROTO ? true : pe.kind == PE_INT ? pe.a == d.port : pe.kind == PE_NAME ? uint32_t(pe.a) == d.name
+                                                                          : pe.a <= d.port && d.port <= pe.b;
+    }
+    bits |= ok ? 1u << e : 0u;
+  }
+  portbits[m] = bits;
+}
 __global__ __launch_bounds__(256) void k_portbits(uint32_t M, uint32_t D, const uint8_t* __restrict__ portok,
                                                   uint32_t* __restrict__ portbits) {
   portbits_blk(M, D, portok, portbits, blockIdx.x);
@@ -1152,12 +1173,35 @@ __device__ __forceinline__ void classify_blk(MemberArgs a, uint32_t* __restrict_
     uint32_t s = ht_find(a.ht_key, a.ht_cap, a.hash[i]);
     uint32_t r = s == 0xFFFFFFFFu ? i : a.ht_rep[s];
     if (r != i) {  // verify (a 64-bit hash collision must never merge distinct classes)
-      bool eq = a.cnt[r] == a.cnt[i] && (!a.id_blk || a.id_blk[r] == a.id_blk[i]);
-      for (uint32_t j = 0; eq && j < a.cnt[i]; j++) eq = a.list[a.list_off[r] + j] == a.list[a.list_off[i] + j];
+      // 8 list entries / job slots of both identities per batch, every load of a batch issued
+      // before any compare (one memory round trip per batch instead of one per entry)
+      const uint32_t n = a.cnt[i], oi = a.list_off[i], orr = a.list_off[r];
+      bool eq = a.cnt[r] == n && (!a.id_blk || a.id_blk[r] == a.id_blk[i]);
+      for (uint32_t j0 = 0; eq && j0 < n; j0 += 8) {
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+          const uint32_t j = min(j0 + u, n - 1);
+          x[u] = a.list[oi + j];
+          y[u] = a.list[orr + j];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) eq = eq && x[u] == y[u];
+      }
       if (eq && a.id_desc) {
-        for (uint32_t k = 0; eq && k < a.K; k++) {
-          uint8_t si = a.id_status[uint64_t(i) * a.K + k], sr = a.id_status[uint64_t(r) * a.K + k];
-          eq = si == sr && (si != CYC_JOB_VALID || a.id_desc[uint64_t(i) * a.K + k] == a.id_desc[uint64_t(r) * a.K + k]);
+        for (uint32_t k0 = 0; eq && k0 < a.K; k0 += 8) {
+          uint8_t si[8], sr[8];
+          int32_t di[8], dr[8];
+#pragma unroll
+          for (uint32_t u = 0; u < 8; u++) {
+            const uint64_t k = min(k0 + u, a.K - 1);
+            si[u] = a.id_status[uint64_t(i) * a.K + k];
+            sr[u] = a.id_status[uint64_t(r) * a.K + k];
+            di[u] = a.id_desc[uint64_t(i) * a.K + k];
+            dr[u] = a.id_desc[uint64_t(r) * a.K + k];
+          }
+#pragma unroll
+          for (uint32_t u = 0; u < 8; u++) eq = eq && si[u] == sr[u] && (si[u] != CYC_JOB_VALID || di[u] == dr[u]);
         }
       }
       c = eq ? r : i;
@@ -1237,6 +1281,17 @@ struct RowArgs {
   // kernel in block slices once k_classify is done with it: no memset node precedes k_member
   uint32_t* ht_clear;
   uint64_t ht_clear_words;
+  // the class election inside the identity sets (fused IDO fronts, class_ident_blk ELECT): the
+  // membership's hash table and each identity's hash; class_of / reps / rep_cnt are written there
+  const uint32_t* act;
+  uint32_t n_act, ht_cap;
+  const unsigned long long* ht_key;
+  const uint32_t* ht_rep;
+  const uint64_t* hash;
+  const uint32_t* id_blk;
+  uint32_t* class_of_w;
+  uint32_t* reps_w;
+  uint32_t* rep_cnt_w;
 };
 
 // Row of A holding representative i's class rows: its identity slot, or (in-place class rows) the
@@ -1380,17 +1435,69 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
 // Classes with more than CI_LDS peers walk the targets directly.
 constexpr uint32_t CI_LDS = 128;
 constexpr int CI_G = 4;  // identity sets: job slots (ingress) / descriptors (egress) per wave
-template <bool EGRESS, int G>
+// The class election of one identity by a wave (classify_blk's per-identity part, lanes over the
+// membership lists and job slots): its class is the representative the membership elected for its
+// hash, verified equal (a 64-bit hash collision never merges classes), else itself.  The owner wave
+// writes class_of and appends a representative to reps.  Returns whether i represents its class.
+template <bool EGRESS>
+__device__ __forceinline__ bool elect_rep(const RowArgs& a, uint32_t i, uint32_t lane, bool owner) {
+  uint32_t c = i;
+  if (!a.id_err[i]) {
+    const uint32_t s = ht_find(a.ht_key, a.ht_cap, a.hash[i]);
+    const uint32_t r = s == 0xFFFFFFFFu ? i : a.ht_rep[s];
+    if (r != i) {
+      const uint32_t n = a.cnt[i];
+      bool eq = a.cnt[r] == n && (!a.id_blk || a.id_blk[r] == a.id_blk[i]);
+      if (eq) {
+        const uint32_t oi = a.list_off[i], orr = a.list_off[r];
+        bool diff = false;
+        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+          const uint32_t j = j0 + lane;
+          diff |= __ballot(j < n && a.list[oi + j] != a.list[orr + j]) != 0;
+        }
+        if (!EGRESS)  // ingress identities include every slot's job status and descriptor
+          for (uint32_t k0 = 0; k0 < a.K; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            bool d = false;
+            if (k < a.K) {
+              const uint8_t si = a.id_status[uint64_t(i) * a.K + k], sr = a.id_status[uint64_t(r) * a.K + k];
+              const int32_t di = a.id_desc[uint64_t(i) * a.K + k], dr = a.id_desc[uint64_t(r) * a.K + k];
+              d = si != sr || (si == CYC_JOB_VALID && di != dr);
+            }
+            diff |= __ballot(d) != 0;
+          }
+        eq = !diff;
+      }
+      c = eq ? r : i;
+    }
+  }
+  if (owner && lane == 0) {
+    a.class_of_w[i] = c;
+    if (c == i) a.reps_w[atomicAdd(a.rep_cnt_w, 1u) + 1u] = i;  // the counter starts at ~0 (membership)
+  }
+  return c == i;
+}
+
+template <bool EGRESS, int G, bool ELECT = false>
 __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   __shared__ uint32_t s_j[4][CI_LDS];
   __shared__ uint32_t s_pid[4][CI_LDS], s_pk[4][CI_LDS];  // per entry: identity-set row; kind << 16 | port-test bits
-  ht_clear_slice(a, bid_, nblk_);
-  // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
+  ht_clear_slice(a, bid_, nblk_);  // (ELECT: the class rows of launch E clear it instead)
+  // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G.
+  // ELECT: a wave per (active identity, G NB indices), the class election first; the waves of
+  // identities that do not represent their class end there (their class rows are their class's).
   const uint32_t wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wv = bid_ * 4 + wi, lane = threadIdx.x & 63;
   const uint32_t nbc = (a.NB + G - 1) / G;
   const uint32_t r = wv / nbc, nb0 = (wv % nbc) * G;
-  if (r >= *a.rep_cnt + 1u) return;
-  const uint32_t i = a.reps[r];
+  uint32_t i;
+  if (ELECT) {
+    if (r >= a.n_act) return;
+    i = a.act[r];
+    if (!elect_rep<EGRESS>(a, i, lane, nb0 == 0)) return;
+  } else {
+    if (r >= *a.rep_cnt + 1u) return;
+    i = a.reps[r];
+  }
   int32_t du[G];
   {  // ingress: the slots' status and descriptor, all G pairs loaded at once
     uint8_t st[G];
@@ -2191,6 +2298,7 @@ struct RepHead {  // a class-row block's representative: identity, class-row ind
 template <bool EGRESS, int KC, bool UNI = false>
 __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   extern __shared__ uint64_t sB[];
+  ht_clear_slice(a, bid_, nblk_);  // fused fronts: the election of launch D is done with the hash table
   // block = (a.rpb consecutive class representatives, KC job slots, 256 pod words): each word's runs
   // and slot words are loaded once for all its representatives
   const uint32_t cg = ido_chunk_groups(a.WA), nkc = (a.K + KC - 1) / KC;
@@ -2451,7 +2559,10 @@ __global__ __launch_bounds__(256) void k_front_a(FrontA f) {
 // rows and of the per-pod pod-peer rows is one direction's sub-list (target-row runs put both
 // directions into segment 0: one window).
 struct FrontB {
-  uint32_t nb[7];       // IP rows x2 | pod-peer rows x2 (or identity sets, segment 2) | membership in | eg | port bits
+  uint32_t nb[9];       // IP rows x2 | pod-peer rows x2 (or identity sets, segment 2) | membership in | eg | port bits |
+                        // port table | slot words (the last two: runs without launch A, enq_front_fused)
+  FrontA pre;           // launch A's port table and slot-word arguments
+  uint32_t bits_direct; // port bits from the matchers (pre.pms ...), not from the byte table
   uint32_t ip_grp;      // IP rows: peers per wave
   uint32_t pod_direct;  // PM builds with few pod-peer words: segments 2-3 = full pod-peer rows per pod
                         // (pod_rows_direct_blk), else segment 2 = identity sets (IDO)
@@ -2512,7 +2623,16 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
     }
     b -= f.nb[4 + d];
   }
-  if (b < f.nb[6]) portbits_blk(f.M, f.D, f.portok, f.portbits, b);  // for the egress class rows
+  if (b < f.nb[6]) {  // for the identity sets and the class rows
+    if (f.bits_direct) return portbits_direct_blk(f.M, f.D, f.pre.pms, f.pre.pents, f.pre.descs, f.portbits, b);
+    return portbits_blk(f.M, f.D, f.portok, f.portbits, b);
+  }
+  b -= f.nb[6];
+  if (b < f.nb[7]) return portok_blk(f.pre.M, f.pre.D, f.pre.pms, f.pre.pents, f.pre.descs, f.pre.portok, b, f.nb[7]);
+  b -= f.nb[7];
+  if (b < f.nb[8])
+    slot_words_blk(f.pre.P, f.pre.K, f.pre.W, f.pre.D, f.pre.slot_desc, f.pre.slot_status, f.pre.VALID, f.pre.DESCW, f.pre.DM, b,
+                   f.nb[8]);
 }
 
 // Pod-peer rows from posting lists: a pod selector that is ONE requirement `k = v` or `k in (v0,
@@ -2602,10 +2722,11 @@ struct FrontRows {
   uint32_t nb[2];
   RowArgs ra[2];
 };
+// IDO builds: the class election and the identity sets in one launch (class_ident_blk ELECT)
 __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[0]) class_ident_blk<false, CI_G>(f.ra[0], b, f.nb[0]);
-  else class_ident_blk<true, CI_G>(f.ra[1], b - f.nb[0], f.nb[1]);
+  if (b < f.nb[0]) class_ident_blk<false, CI_G, true>(f.ra[0], b, f.nb[0]);
+  else class_ident_blk<true, CI_G, true>(f.ra[1], b - f.nb[0], f.nb[1]);
 }
 // PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
 template <bool WAVE>
@@ -2652,6 +2773,8 @@ struct EmitArgs {
   uint8_t* st_dst;            // emit's blocks in slices: no separate copy node ends the step
   uint64_t st_bytes;
   uint32_t interleave;        // the row list alternates ingress / egress rows (n_rows equal)
+  uint32_t* reset;            // the IP rows' word-span records (RowArgs::ip_rng), reset to ~0 for the NEXT
+  uint64_t reset_n;           // run in block slices (their readers are all done): no fill launch before it
 };
 
 // Row r of the row list -> (plane, pod).
@@ -2674,8 +2797,13 @@ __device__ __forceinline__ const uint64_t* emit_src(const EmitArgs& a, uint32_t 
   return r == p - a.row_lo[pl] ? nullptr : a.out[pl] + uint64_t(r) * a.row_words;
 }
 
-// Block b's slice of the status plane copy (every emit kernel calls this first).
+// Block b's slice of the status plane copy and of the word-span reset (every emit kernel calls this first).
 __device__ __forceinline__ void emit_status(const EmitArgs& a) {
+  if (a.reset_n) {
+    const uint64_t per = (a.reset_n + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
+    const uint64_t hi = lo + per < a.reset_n ? lo + per : a.reset_n;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.reset[i] = 0xFFFFFFFFu;
+  }
   if (!a.st_bytes) return;
   const uint64_t per = (a.st_bytes + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
   const uint64_t hi = lo + per < a.st_bytes ? lo + per : a.st_bytes;
@@ -3268,6 +3396,10 @@ struct cyc_ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   double last_ms[3] = {0, 0, 0};
   bool timed = false;  // the last run recorded the step timing events
+  // the IP rows' word-span records are all ~0: the last enqueued run's emit reset them (EmitArgs::reset),
+  // so the next fused front needs no fill before its IP rows (and, without a selector table, no launch A)
+  bool ip_rng_clean = false;
+  bool capturing = false;  // a hipGraph capture is in progress (captured steps always fill the spans themselves)
   bool ran = false;    // a run has been enqueued
   hipEvent_t run_done = nullptr;  // recorded on the run's stream after every run (cyc_last_classes)
   // batched blocks (cyc_probe_prepare_blocks; pb.blocks non-empty)
@@ -3538,12 +3670,36 @@ static void prepare_device(cyc_ctx* c) {
       c->plvt_ready = false;
       // label postings: the pods under each (dense key, value) of their own labels, and per EQ / IN
       // (<= 2 values) requirement the postings of its values (pod_rows_post_blk)
+      // (key, value, pod) triples sorted by (key, value), pods ascending within: two counting-sort
+      // passes (value, then key; both are dictionary ids), O(pairs + dictionary)
       std::vector<std::pair<uint64_t, uint32_t>> kv;
-      for (uint32_t q = 0; q < pb.P; q++) {
-        const uint32_t l = pb.pod_ls[q];
-        for (uint32_t x = pb.ls_off[l]; x < pb.ls_off[l + 1]; x++) kv.push_back({(uint64_t(kx[pb.ls_key[x]]) << 32) | pb.ls_val[x], q});
+      {
+        const size_t NV = pb.strings.size() + 1, NK = nk + 1;
+        size_t n = 0;
+        for (uint32_t q = 0; q < pb.P; q++) n += pb.ls_off[pb.pod_ls[q] + 1] - pb.ls_off[pb.pod_ls[q]];
+        std::vector<uint32_t> kk(n), vv(n), qq(n), cnt(std::max(NV, NK) + 1);
+        size_t x0 = 0;
+        for (uint32_t q = 0; q < pb.P; q++) {
+          const uint32_t l = pb.pod_ls[q];
+          for (uint32_t x = pb.ls_off[l]; x < pb.ls_off[l + 1]; x++, x0++) {
+            kk[x0] = uint32_t(kx[pb.ls_key[x]]);
+            vv[x0] = pb.ls_val[x];
+            qq[x0] = q;
+          }
+        }
+        std::vector<uint32_t> ord(n), ord2(n);
+        auto pass = [&](const std::vector<uint32_t>& key, size_t range, const std::vector<uint32_t>& in, std::vector<uint32_t>& out) {
+          std::fill(cnt.begin(), cnt.begin() + range + 1, 0u);
+          for (uint32_t i : in) cnt[key[i] + 1]++;
+          for (size_t r = 0; r < range; r++) cnt[r + 1] += cnt[r];
+          for (uint32_t i : in) out[cnt[key[i]]++] = i;
+        };
+        std::iota(ord.begin(), ord.end(), 0u);  // pod order (q ascending)
+        pass(vv, NV, ord, ord2);
+        pass(kk, NK, ord2, ord);
+        kv.resize(n);
+        for (size_t i = 0; i < n; i++) kv[i] = {(uint64_t(kk[ord[i]]) << 32) | vv[ord[i]], qq[ord[i]]};
       }
-      std::sort(kv.begin(), kv.end());
       std::vector<uint32_t> pods(kv.size());
       for (size_t i = 0; i < kv.size(); i++) pods[i] = kv[i].second;
       auto range = [&](uint32_t key, uint32_t v) {
@@ -4340,6 +4496,7 @@ static bool enq_emit_blocks(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64
 
 static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, uint8_t* d_status, bool inplace = false) {
   Problem& pb = c->pb;
+  c->ip_rng_clean = false;  // (set again below when this emit resets the spans for the next run)
   if (!pb.blocks.empty()) return enq_emit_blocks(c, st, out_in, out_eg, d_status);
   const uint32_t K = pb.K;
   const uint64_t rw[2] = {uint64_t(K) * c->win_wa, uint64_t(K) * pb.W};  // words per plane row
@@ -4350,6 +4507,9 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.st_src = c->slot_status.as<uint8_t>();
   ea.st_dst = d_status;
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
+  ea.reset = c->ip_rng.as<uint32_t>();
+  ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
+  c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
     ea.row_lo[pl] = uint32_t(c->rl[pl]);
     ea.order[pl] = c->order[pl].as<uint32_t>();
@@ -4377,7 +4537,7 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
     e1.n_rows[0] = pl == 0 ? nr[0] : 0u;  // the row list is [plane 0 rows][plane 1 rows]
     e1.n_rows[1] = pl == 1 ? nr[1] : 0u;
     e1.row_words = rw[pl];
-    if (!first) e1.st_bytes = 0;
+    if (!first) e1.st_bytes = e1.reset_n = 0;
     first = false;
     enq_emit_launch(e1, st, pl == 0 ? out_in : reinterpret_cast<uint64_t*>(16), pl == 1 ? out_eg : reinterpret_cast<uint64_t*>(16));
   }
@@ -4559,8 +4719,25 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
       fd.ra[d].pod_sparse = pod_sparse(c);  // pod rows from pod_rows_sparse_blk (launch C)
       continue;
     }
+    // launch D elects the classes (no launch C) while it builds the identity sets; launch E's blocks
+    // then empty the hash table for the next run
+    fc.nb[d] = 0;
+    {
+      const MemberArgs& ma = fb.ma[d];
+      RowArgs& ra = fd.ra[d];
+      ra.act = ma.act;
+      ra.n_act = na;
+      ra.ht_cap = ma.ht_cap;
+      ra.ht_key = ma.ht_key;
+      ra.ht_rep = ma.ht_rep;
+      ra.hash = ma.hash;
+      ra.id_blk = ma.id_blk;
+      ra.class_of_w = c->dir[d].class_of.as<uint32_t>();
+      ra.reps_w = ma.reps;
+      ra.rep_cnt_w = ma.rep_cnt;
+    }
     fe.ra[d] = fd.ra[d];
-    fe.ra[d].ht_clear_words = 0;
+    fd.ra[d].ht_clear_words = 0;
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + CI_G - 1) / CI_G) + 3) / 4);
     // egress with one descriptor per slot (udesc): only the block's slots' sets are staged
     if (d == 1 && c->uni_desc) fe.ra[d].udesc = c->udesc.as<int32_t>();
@@ -4571,14 +4748,28 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     if (d == 1 && fe.ra[d].udesc) lds_uni = per * fe.ra[d].rpb;
     else lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
   }
-  const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
   const bool bits = fa.nb[1] && port_bits_on(c);
+  const uint32_t nb_bits = bits ? blocks((uint64_t(M) + 255) / 256) : 0u;
   fb.M = M;
   fb.D = D;
   fb.portok = c->portok.as<uint8_t>();
   fb.portbits = c->portbits.as<uint32_t>();
-  fb.nb[6] = bits ? blocks((uint64_t(M) + 255) / 256) : 0u;
+  fb.nb[6] = nb_bits;
   fe.ra[1].portbits = bits && fe.nb[1] ? c->portbits.as<uint32_t>() : nullptr;
+  // Without a selector table to build (lazy selectors) launch A is dropped: its port table, slot
+  // words and port bits (from the matchers directly) join launch B — their readers are the class
+  // rows, launches D / E — and the IP rows' word spans were reset by the previous run's emit
+  // (EmitArgs::reset; a memset when they were not).  Captured graphs keep launch A: a replay must not
+  // depend on the step before it.
+  if (fa.nb[3] == 0 && !c->capturing) {
+    fb.pre = fa;
+    fb.bits_direct = 1;
+    fb.nb[7] = fa.nb[1];
+    fb.nb[8] = fa.nb[2];
+    if (fa.fill_n && !c->ip_rng_clean) HIPCHK(hipMemsetAsync(fa.fill_p, 0xFF, fa.fill_n * 4, st));
+    fa.nb[0] = fa.nb[1] = fa.nb[2] = 0;
+  }
+  const uint64_t ga = uint64_t(fa.nb[0]) + fa.nb[1] + fa.nb[2] + fa.nb[3];
   uint64_t gb = 0, gc = 0;
   for (uint32_t x : fb.nb) gb += x;
   for (uint32_t x : fc.nb) gc += x;
@@ -4594,6 +4785,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     return true;
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
+  for (int d = 0; d < 2; d++)  // an election without class rows (an empty word window): the table is emptied here
+    if (fd.nb[d] && !fe.nb[d]) enq_member_clear(c, d, st);
   if (fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
     k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);
   } else {  // the directions' class rows as two launches, each at its own register budget (egress 101
@@ -4797,7 +4990,14 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
       ensure_cap_streams(c);
       hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
-      capture_pipeline(c, c->cap_stream, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status);
+      c->capturing = true;
+      try {
+        capture_pipeline(c, c->cap_stream, c->cap_stream2, c->cap_stream3, d_in, d_eg, d_status);
+      } catch (...) {
+        c->capturing = false;
+        throw;
+      }
+      c->capturing = false;
       HIPCHK(hipStreamEndCapture(c->cap_stream, &g));
       c->graph = g;  // destroyed with the exec (drop_graph / reap_graphs)
       HIPCHK(hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
