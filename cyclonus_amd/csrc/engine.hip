@@ -1162,51 +1162,61 @@ __global__ __launch_bounds__(256) void k_member_wave(MemberArgs a) { member_wave
 // order (ascending identity), at a base taken with one atomicAdd — consecutive identities (one
 // namespace) stay adjacent, so consecutive class-row blocks share their targets' peer rows in
 // L2.  The counter starts at ~0 (hash-table memset), so it ends at count - 1.
+// The class of identity i (a thread's work): the representative the membership elected for its
+// hash, verified equal — a 64-bit hash collision must never merge distinct classes — else i itself.
+// 8 list entries / job slots of both identities per batch, every load of a batch issued before any
+// compare (one memory round trip per batch instead of one per entry).  id_desc null: egress.
+__device__ __forceinline__ uint32_t class_of_identity(uint32_t i, const uint8_t* __restrict__ err, const uint64_t* __restrict__ hash,
+                                                      const unsigned long long* ht_key, const uint32_t* ht_rep, uint32_t ht_cap,
+                                                      const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ list_off,
+                                                      const uint32_t* __restrict__ list, const uint32_t* __restrict__ id_blk,
+                                                      const uint8_t* __restrict__ id_status, const int32_t* __restrict__ id_desc,
+                                                      uint32_t K) {
+  if (err[i]) return i;
+  const uint32_t s = ht_find(ht_key, ht_cap, hash[i]);
+  const uint32_t r = s == 0xFFFFFFFFu ? i : ht_rep[s];
+  if (r == i) return i;
+  const uint32_t n = cnt[i], oi = list_off[i], orr = list_off[r];
+  bool eq = cnt[r] == n && (!id_blk || id_blk[r] == id_blk[i]);
+  for (uint32_t j0 = 0; eq && j0 < n; j0 += 8) {
+    uint32_t x[8], y[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) {
+      const uint32_t j = min(j0 + u, n - 1);
+      x[u] = list[oi + j];
+      y[u] = list[orr + j];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) eq = eq && x[u] == y[u];
+  }
+  if (eq && id_desc) {
+    for (uint32_t k0 = 0; eq && k0 < K; k0 += 8) {
+      uint8_t si[8], sr[8];
+      int32_t di[8], dr[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) {
+        const uint64_t k = min(k0 + u, K - 1);
+        si[u] = id_status[uint64_t(i) * K + k];
+        sr[u] = id_status[uint64_t(r) * K + k];
+        di[u] = id_desc[uint64_t(i) * K + k];
+        dr[u] = id_desc[uint64_t(r) * K + k];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) eq = eq && si[u] == sr[u] && (si[u] != CYC_JOB_VALID || di[u] == dr[u]);
+    }
+  }
+  return eq ? r : i;
+}
+
 __device__ __forceinline__ void classify_blk(MemberArgs a, uint32_t* __restrict__ class_of, uint32_t bid_, uint32_t nblk_) {
   __shared__ uint32_t wsum[4], base;
   const uint32_t ii = bid_ * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool live = ii < a.n_act;
   const uint32_t i = live ? a.act[ii] : 0;
-  uint32_t c = i;
-  if (live && !a.err[i]) {
-    uint32_t s = ht_find(a.ht_key, a.ht_cap, a.hash[i]);
-    uint32_t r = s == 0xFFFFFFFFu ? i : a.ht_rep[s];
-    if (r != i) {  // verify (a 64-bit hash collision must never merge distinct classes)
-      // 8 list entries / job slots of both identities per batch, every load of a batch issued
-      // before any compare (one memory round trip per batch instead of one per entry)
-      const uint32_t n = a.cnt[i], oi = a.list_off[i], orr = a.list_off[r];
-      bool eq = a.cnt[r] == n && (!a.id_blk || a.id_blk[r] == a.id_blk[i]);
-      for (uint32_t j0 = 0; eq && j0 < n; j0 += 8) {
-        uint32_t x[8], y[8];
-#pragma unroll
-        for (uint32_t u = 0; u < 8; u++) {
-          const uint32_t j = min(j0 + u, n - 1);
-          x[u] = a.list[oi + j];
-          y[u] = a.list[orr + j];
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < 8; u++) eq = eq && x[u] == y[u];
-      }
-      if (eq && a.id_desc) {
-        for (uint32_t k0 = 0; eq && k0 < a.K; k0 += 8) {
-          uint8_t si[8], sr[8];
-          int32_t di[8], dr[8];
-#pragma unroll
-          for (uint32_t u = 0; u < 8; u++) {
-            const uint64_t k = min(k0 + u, a.K - 1);
-            si[u] = a.id_status[uint64_t(i) * a.K + k];
-            sr[u] = a.id_status[uint64_t(r) * a.K + k];
-            di[u] = a.id_desc[uint64_t(i) * a.K + k];
-            dr[u] = a.id_desc[uint64_t(r) * a.K + k];
-          }
-#pragma unroll
-          for (uint32_t u = 0; u < 8; u++) eq = eq && si[u] == sr[u] && (si[u] != CYC_JOB_VALID || di[u] == dr[u]);
-        }
-      }
-      c = eq ? r : i;
-    }
-  }
+  const uint32_t c = live ? class_of_identity(i, a.err, a.hash, a.ht_key, a.ht_rep, a.ht_cap, a.cnt, a.list_off, a.list, a.id_blk,
+                                              a.id_status, a.id_desc, a.K)
+                          : i;
   if (live) class_of[i] = c;
   const bool f = live && c == i;
   const uint64_t m = __ballot(f);
@@ -1281,8 +1291,8 @@ struct RowArgs {
   // kernel in block slices once k_classify is done with it: no memset node precedes k_member
   uint32_t* ht_clear;
   uint64_t ht_clear_words;
-  // the class election inside the identity sets (fused IDO fronts, class_ident_blk ELECT): the
-  // membership's hash table and each identity's hash; class_of / reps / rep_cnt are written there
+  // the class election inside the PM class rows (fused PM fronts, class_rows_pl_blk ELECT): the
+  // membership's hash table and each identity's hash; class_of is written there
   const uint32_t* act;
   uint32_t n_act, ht_cap;
   const unsigned long long* ht_key;
@@ -1435,69 +1445,17 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
 // Classes with more than CI_LDS peers walk the targets directly.
 constexpr uint32_t CI_LDS = 128;
 constexpr int CI_G = 4;  // identity sets: job slots (ingress) / descriptors (egress) per wave
-// The class election of one identity by a wave (classify_blk's per-identity part, lanes over the
-// membership lists and job slots): its class is the representative the membership elected for its
-// hash, verified equal (a 64-bit hash collision never merges classes), else itself.  The owner wave
-// writes class_of and appends a representative to reps.  Returns whether i represents its class.
-template <bool EGRESS>
-__device__ __forceinline__ bool elect_rep(const RowArgs& a, uint32_t i, uint32_t lane, bool owner) {
-  uint32_t c = i;
-  if (!a.id_err[i]) {
-    const uint32_t s = ht_find(a.ht_key, a.ht_cap, a.hash[i]);
-    const uint32_t r = s == 0xFFFFFFFFu ? i : a.ht_rep[s];
-    if (r != i) {
-      const uint32_t n = a.cnt[i];
-      bool eq = a.cnt[r] == n && (!a.id_blk || a.id_blk[r] == a.id_blk[i]);
-      if (eq) {
-        const uint32_t oi = a.list_off[i], orr = a.list_off[r];
-        bool diff = false;
-        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
-          const uint32_t j = j0 + lane;
-          diff |= __ballot(j < n && a.list[oi + j] != a.list[orr + j]) != 0;
-        }
-        if (!EGRESS)  // ingress identities include every slot's job status and descriptor
-          for (uint32_t k0 = 0; k0 < a.K; k0 += 64) {
-            const uint32_t k = k0 + lane;
-            bool d = false;
-            if (k < a.K) {
-              const uint8_t si = a.id_status[uint64_t(i) * a.K + k], sr = a.id_status[uint64_t(r) * a.K + k];
-              const int32_t di = a.id_desc[uint64_t(i) * a.K + k], dr = a.id_desc[uint64_t(r) * a.K + k];
-              d = si != sr || (si == CYC_JOB_VALID && di != dr);
-            }
-            diff |= __ballot(d) != 0;
-          }
-        eq = !diff;
-      }
-      c = eq ? r : i;
-    }
-  }
-  if (owner && lane == 0) {
-    a.class_of_w[i] = c;
-    if (c == i) a.reps_w[atomicAdd(a.rep_cnt_w, 1u) + 1u] = i;  // the counter starts at ~0 (membership)
-  }
-  return c == i;
-}
-
-template <bool EGRESS, int G, bool ELECT = false>
+template <bool EGRESS, int G>
 __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   __shared__ uint32_t s_j[4][CI_LDS];
   __shared__ uint32_t s_pid[4][CI_LDS], s_pk[4][CI_LDS];  // per entry: identity-set row; kind << 16 | port-test bits
-  ht_clear_slice(a, bid_, nblk_);  // (ELECT: the class rows of launch E clear it instead)
-  // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G.
-  // ELECT: a wave per (active identity, G NB indices), the class election first; the waves of
-  // identities that do not represent their class end there (their class rows are their class's).
+  ht_clear_slice(a, bid_, nblk_);
+  // one wave per (representative, G NB indices): each peer's IDOB word is loaded once for all G
   const uint32_t wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wv = bid_ * 4 + wi, lane = threadIdx.x & 63;
   const uint32_t nbc = (a.NB + G - 1) / G;
   const uint32_t r = wv / nbc, nb0 = (wv % nbc) * G;
-  uint32_t i;
-  if (ELECT) {
-    if (r >= a.n_act) return;
-    i = a.act[r];
-    if (!elect_rep<EGRESS>(a, i, lane, nb0 == 0)) return;
-  } else {
-    if (r >= *a.rep_cnt + 1u) return;
-    i = a.reps[r];
-  }
+  if (r >= *a.rep_cnt + 1u) return;
+  const uint32_t i = a.reps[r];
   int32_t du[G];
   {  // ingress: the slots' status and descriptor, all G pairs loaded at once
     uint8_t st[G];
@@ -1834,6 +1792,7 @@ struct PlShared {  // one per block, shared by both directions' instantiations o
   uint32_t pre[PL_TGT + 1], poff[PL_TGT];
   uint32_t all;
   int32_t rdu[32];  // ingress, K <= 32: the representative's job descriptor per slot (-1: slot not VALID)
+  uint32_t rl[256], nrl;  // ELECT: the representatives among the block's identities just elected
 };
 
 constexpr int PL_ITEMS = 1;
@@ -2101,14 +2060,44 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
   }
 }
 
-template <bool EGRESS, bool WAVE>
+template <bool EGRESS, bool WAVE, bool ELECT = false>
 __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
-  ht_clear_slice(a, bid_, nblk_);
-  const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC;
+  ht_clear_slice(a, bid_, nblk_);  // (ELECT: the emit empties the table instead)
+  const uint32_t nkc = (a.K + KC - 1) / KC;
   const bool kbits = EGRESS ? a.portbits != nullptr : a.K <= 32;
-  for (uint32_t r = bid_; r < n_reps; r += nblk_) {
-    const uint32_t i = a.reps[r];
+  // ELECT (fused PM fronts: no class-election launch): block b elects the classes of its own slice of
+  // the active identities, a thread each (class_of_identity), collects the slice's representatives
+  // in LDS, and computes their class rows; otherwise the blocks stride over the elected representatives.
+  const uint32_t per = ELECT ? (a.n_act + nblk_ - 1) / nblk_ : 0u;
+  const uint32_t lo = ELECT ? min(a.n_act, bid_ * per) : 0u, hi = ELECT ? min(a.n_act, lo + per) : 0u;
+  const uint32_t n_reps = ELECT ? 0u : *a.rep_cnt + 1u;
+  uint32_t chunk = lo;  // ELECT: the slice's identities [chunk, chunk + blockDim.x) elected last
+  uint32_t nloc = 0;    // and the representatives among them (sh.rl)
+  for (uint32_t r = ELECT ? 0u : bid_;; r += ELECT ? 1u : nblk_) {
+    if (ELECT) {
+      while (r >= nloc && chunk < hi) {  // elect the next chunk of the slice
+        __syncthreads();                 // (sh.rl / sh.nrl of the previous chunk are no longer read)
+        if (threadIdx.x == 0) sh.nrl = 0;
+        __syncthreads();
+        const uint32_t ii = chunk + threadIdx.x;
+        if (ii < hi) {
+          const uint32_t id = a.act[ii];
+          const uint32_t cl = class_of_identity(id, a.id_err, a.hash, a.ht_key, a.ht_rep, a.ht_cap, a.cnt, a.list_off, a.list,
+                                                a.id_blk, a.id_status, EGRESS ? nullptr : a.id_desc, a.K);
+          a.class_of_w[id] = cl;
+          if (cl == id) sh.rl[atomicAdd(&sh.nrl, 1u)] = id;
+        }
+        __syncthreads();
+        chunk += blockDim.x;
+        nloc = sh.nrl;
+        r = 0;
+      }
+      if (r >= nloc) break;
+    } else if (r >= n_reps) {
+      break;
+    }
+    const uint32_t i = ELECT ? sh.rl[r] : a.reps[r];
     const uint32_t nt = a.cnt[i];
     const uint32_t* lst = a.list + a.list_off[i];
     uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
@@ -2298,7 +2287,6 @@ struct RepHead {  // a class-row block's representative: identity, class-row ind
 template <bool EGRESS, int KC, bool UNI = false>
 __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
   extern __shared__ uint64_t sB[];
-  ht_clear_slice(a, bid_, nblk_);  // fused fronts: the election of launch D is done with the hash table
   // block = (a.rpb consecutive class representatives, KC job slots, 256 pod words): each word's runs
   // and slot words are loaded once for all its representatives
   const uint32_t cg = ido_chunk_groups(a.WA), nkc = (a.K + KC - 1) / KC;
@@ -2722,19 +2710,19 @@ struct FrontRows {
   uint32_t nb[2];
   RowArgs ra[2];
 };
-// IDO builds: the class election and the identity sets in one launch (class_ident_blk ELECT)
 __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[0]) class_ident_blk<false, CI_G, true>(f.ra[0], b, f.nb[0]);
-  else class_ident_blk<true, CI_G, true>(f.ra[1], b - f.nb[0], f.nb[1]);
+  if (b < f.nb[0]) class_ident_blk<false, CI_G>(f.ra[0], b, f.nb[0]);
+  else class_ident_blk<true, CI_G>(f.ra[1], b - f.nb[0], f.nb[1]);
 }
-// PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
-template <bool WAVE>
+// PM builds (pod-peer words from materialised rows): the class rows, egress blocks first; ELECT: each
+// block elects the classes of its slice of the identities first (no class-election launch)
+template <bool WAVE, bool ELECT>
 __global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
   __shared__ PlShared sh;
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_pl_blk<true, WAVE>(f.ra[1], sh, b, f.nb[1]);
-  else class_rows_pl_blk<false, WAVE>(f.ra[0], sh, b - f.nb[1], f.nb[0]);
+  if (b < f.nb[1]) class_rows_pl_blk<true, WAVE, ELECT>(f.ra[1], sh, b, f.nb[1]);
+  else class_rows_pl_blk<false, WAVE, ELECT>(f.ra[0], sh, b - f.nb[1], f.nb[0]);
 }
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
@@ -2773,8 +2761,15 @@ struct EmitArgs {
   uint8_t* st_dst;            // emit's blocks in slices: no separate copy node ends the step
   uint64_t st_bytes;
   uint32_t interleave;        // the row list alternates ingress / egress rows (n_rows equal)
-  uint32_t* reset;            // the IP rows' word-span records (RowArgs::ip_rng), reset to ~0 for the NEXT
-  uint64_t reset_n;           // run in block slices (their readers are all done): no fill launch before it
+  // k_emit_units (planes whose rows differ in length, a source shard): per plane its row length in
+  // words, rows per unit (a unit = one block's pass) and units; the unit list is [plane 0][plane 1]
+  uint64_t pl_words[2];
+  uint32_t unit_rows[2], n_units[2];
+  // buffers reset to ~0 for the NEXT run in block slices (their readers are all done): the IP rows'
+  // word-span records (RowArgs::ip_rng) and, for PM builds whose class rows elect the classes, the
+  // membership hash tables — no fill launch or memset node before the next front
+  uint32_t* reset[3];
+  uint64_t reset_n[3];
 };
 
 // Row r of the row list -> (plane, pod).
@@ -2792,17 +2787,19 @@ __device__ __forceinline__ void emit_row_of(const EmitArgs& a, uint32_t r, uint3
 // (in-place class rows: nothing to copy).
 __device__ __forceinline__ const uint64_t* emit_src(const EmitArgs& a, uint32_t pl, uint32_t p) {
   const uint32_t c = a.class_of[pl][a.pod_id[pl][p]];
-  if (!a.arow[pl]) return a.A[pl] + uint64_t(c) * a.row_words;
+  if (!a.arow[pl]) return a.A[pl] + uint64_t(c) * a.pl_words[pl];
   const uint32_t r = a.arow[pl][c];
-  return r == p - a.row_lo[pl] ? nullptr : a.out[pl] + uint64_t(r) * a.row_words;
+  return r == p - a.row_lo[pl] ? nullptr : a.out[pl] + uint64_t(r) * a.pl_words[pl];
 }
 
 // Block b's slice of the status plane copy and of the word-span reset (every emit kernel calls this first).
 __device__ __forceinline__ void emit_status(const EmitArgs& a) {
-  if (a.reset_n) {
-    const uint64_t per = (a.reset_n + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
-    const uint64_t hi = lo + per < a.reset_n ? lo + per : a.reset_n;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.reset[i] = 0xFFFFFFFFu;
+#pragma unroll
+  for (int x = 0; x < 3; x++) {
+    if (!a.reset_n[x]) continue;
+    const uint64_t per = (a.reset_n[x] + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
+    const uint64_t hi = lo + per < a.reset_n[x] ? lo + per : a.reset_n[x];
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.reset[x][i] = 0xFFFFFFFFu;
   }
   if (!a.st_bytes) return;
   const uint64_t per = (a.st_bytes + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
@@ -2906,6 +2903,55 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
 #pragma unroll
     for (int u = 0; u < UNROLL; u++)
       if (x0 + u * BS < n2) emit_store(v[u], &di[x0 + u * BS]);
+  }
+}
+
+// Planes whose rows differ in length (a source shard: ingress rows of every destination over the
+// shard's words, egress rows of its sources over all words) in ONE launch: the unit list is plane 0's
+// rows in groups of unit_rows[0], then plane 1's in groups of unit_rows[1], each group about one
+// block pass (BS x UNROLL x 16 B: config #3 at N = 8 one 100 KB egress row or eight 12.5 KB ingress
+// rows), cut into 8 XCD segments.  A block stages its rows' source / destination addresses in LDS
+// (in-place class rows skipped), then sweeps their 16-byte chunks as one flat range.  Two launches
+// (k_emit_wide + k_emit_flat) ran config #3's N = 8 source shard at 6.0 TB/s against the target
+// shard's single launch at 7.0 (r04a).
+constexpr uint32_t EMIT_UNIT_MAX_ROWS = 64;
+template <int BS, int UNROLL>
+__global__ __launch_bounds__(BS) void k_emit_units(EmitArgs a) {
+  emit_status(a);
+  __shared__ const u64x2* s_src[EMIT_UNIT_MAX_ROWS];
+  __shared__ u64x2* s_dst[EMIT_UNIT_MAX_ROWS];
+  __shared__ uint32_t s_cnt;
+  const uint32_t b = blockIdx.x, n = a.n_units[0] + a.n_units[1], x = b & 7;
+  const uint32_t u = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the unit list
+  if (u >= min(n, (x + 1) * a.per_xcd)) return;
+  const uint32_t pl = u >= a.n_units[0] ? 1u : 0u, r0 = (u - pl * a.n_units[0]) * a.unit_rows[pl];
+  const uint32_t nr = min(a.unit_rows[pl], a.n_rows[pl] - r0);
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  if (threadIdx.x < nr) {
+    const uint32_t p = a.order[pl][r0 + threadIdx.x];
+    const u64x2* src = reinterpret_cast<const u64x2*>(emit_src(a, pl, p));
+    if (src) {  // (row order within the unit does not matter: each row is copied whole)
+      const uint32_t k = atomicAdd(&s_cnt, 1u);
+      s_src[k] = src;
+      s_dst[k] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.pl_words[pl]);
+    }
+  }
+  __syncthreads();
+  const uint32_t n2 = uint32_t(a.pl_words[pl] / 2), tot = s_cnt * n2;
+  for (uint32_t i0 = threadIdx.x; i0 < tot; i0 += BS * UNROLL) {
+    u64x2 v[UNROLL];
+    uint32_t row[UNROLL], col[UNROLL];
+#pragma unroll
+    for (int q = 0; q < UNROLL; q++) {
+      const uint32_t i = i0 + q * BS;
+      row[q] = i / n2;
+      col[q] = i - row[q] * n2;
+      if (i < tot) v[q] = s_src[row[q]][col[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < UNROLL; q++)
+      if (i0 + q * BS < tot) emit_store(v[q], &s_dst[row[q]][col[q]]);
   }
 }
 
@@ -3400,6 +3446,7 @@ struct cyc_ctx {
   // so the next fused front needs no fill before its IP rows (and, without a selector table, no launch A)
   bool ip_rng_clean = false;
   bool capturing = false;  // a hipGraph capture is in progress (captured steps always fill the spans themselves)
+  bool emit_clears_ht[2] = {false, false};  // this run's emit empties the direction's hash table (PM ELECT)
   bool ran = false;    // a run has been enqueued
   hipEvent_t run_done = nullptr;  // recorded on the run's stream after every run (cyc_last_classes)
   // batched blocks (cyc_probe_prepare_blocks; pb.blocks non-empty)
@@ -3920,7 +3967,12 @@ static void ensure_plvt(cyc_ctx* c, hipStream_t st) {
 }
 static bool lazy_sel(const cyc_ctx* c) {
   if (!c->dense_sel || c->pb.may_err || c->sel_lazy == 0 || !front_fused_ok(c)) return false;
-  if (!ido_mode(c) && !pod_sparse(c)) return false;  // the full pod-peer rows read the dense selector table
+  const bool pod_peers = c->rp_off[2] > c->rp_off[0];
+  // the full pod-peer rows read the dense selector table
+  if (!ido_mode(c) && !pod_sparse(c) && pod_peers) return false;
+  // no pod-peer rows at all (IPBlock-only policies, config #4): the membership is the only selector
+  // user, one record and one label-table load per target — no table, and no launch A
+  if (!pod_peers && c->sel_lazy < 0) return true;
   // auto: lazy once the dense table would take ~0.1 ms (>= 64M pairs; config #3u: 0.75G pairs,
   // 1.1 ms; config #2 stays dense — its multi-requirement selectors cost more evaluated per use)
   // IDO builds always: their identity sets and membership evaluate fewer pairs than the table
@@ -4497,19 +4549,29 @@ static bool enq_emit_blocks(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64
 static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, uint8_t* d_status, bool inplace = false) {
   Problem& pb = c->pb;
   c->ip_rng_clean = false;  // (set again below when this emit resets the spans for the next run)
-  if (!pb.blocks.empty()) return enq_emit_blocks(c, st, out_in, out_eg, d_status);
+  const bool clears_ht[2] = {c->emit_clears_ht[0], c->emit_clears_ht[1]};
+  c->emit_clears_ht[0] = c->emit_clears_ht[1] = false;
   const uint32_t K = pb.K;
   const uint64_t rw[2] = {uint64_t(K) * c->win_wa, uint64_t(K) * pb.W};  // words per plane row
   uint32_t nr[2];
   for (int d = 0; d < 2; d++) nr[d] = rw[d] ? uint32_t(c->rh[d] - c->rl[d]) : 0u;
+  if (!pb.blocks.empty() || (!nr[0] && !nr[1]))  // no emit of ours empties the hash tables
+    for (int d = 0; d < 2; d++)
+      if (clears_ht[d]) enq_member_clear(c, d, st);
+  if (!pb.blocks.empty()) return enq_emit_blocks(c, st, out_in, out_eg, d_status);
   if (!nr[0] && !nr[1]) return false;
   EmitArgs ea{};
   ea.st_src = c->slot_status.as<uint8_t>();
   ea.st_dst = d_status;
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
-  ea.reset = c->ip_rng.as<uint32_t>();
-  ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
-  c->ip_rng_clean = ea.reset_n != 0;
+  ea.reset[0] = c->ip_rng.as<uint32_t>();
+  ea.reset_n[0] = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
+  c->ip_rng_clean = ea.reset_n[0] != 0;
+  for (int d = 0; d < 2; d++)  // PM class rows that elected the classes leave the hash tables to the emit
+    if (clears_ht[d]) {
+      ea.reset[1 + d] = static_cast<uint32_t*>(c->dir[d].ht_key.p);
+      ea.reset_n[1 + d] = uint64_t(c->dir[d].ht_cap) * 3;
+    }
   for (uint32_t pl = 0; pl < 2; pl++) {
     ea.row_lo[pl] = uint32_t(c->rl[pl]);
     ea.order[pl] = c->order[pl].as<uint32_t>();
@@ -4520,6 +4582,8 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   }
   ea.out[0] = out_in;
   ea.out[1] = out_eg;
+  ea.pl_words[0] = rw[0];
+  ea.pl_words[1] = rw[1];
   if (rw[0] == rw[1] && nr[0] == nr[1]) {  // target rows: both planes in one launch
     ea.n_rows[0] = ea.n_rows[1] = nr[0];
     ea.row_words = rw[0];
@@ -4530,14 +4594,31 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
     enq_emit_launch(ea, st, out_in, out_eg);
     return true;
   }
+  // rows of different lengths (a source shard): ONE launch over units of about one block pass each
+  const bool aligned = reinterpret_cast<uintptr_t>(out_in) % 16 == 0 && reinterpret_cast<uintptr_t>(out_eg) % 16 == 0;
+  if (aligned && rw[0] % 2 == 0 && rw[1] % 2 == 0) {
+    const uint64_t longest = std::max(nr[0] ? rw[0] : 0, nr[1] ? rw[1] : 0) * 8;
+    const bool big = longest > 512 * 7 * 16;  // 1024 x 7 x 16 B passes for rows over 56 KB, else 256 x 8
+    const uint64_t pass = big ? 1024 * 7 * 16 : 256 * 8 * 16;
+    for (int pl = 0; pl < 2; pl++) {
+      ea.n_rows[pl] = nr[pl];
+      ea.unit_rows[pl] = uint32_t(std::min<uint64_t>(EMIT_UNIT_MAX_ROWS, std::max<uint64_t>(1, pass / std::max<uint64_t>(rw[pl] * 8, 1))));
+      ea.n_units[pl] = (nr[pl] + ea.unit_rows[pl] - 1) / ea.unit_rows[pl];
+    }
+    ea.per_xcd = (ea.n_units[0] + ea.n_units[1] + 7) / 8;
+    const unsigned g = ea.per_xcd * 8;
+    if (big) k_emit_units<1024, 7><<<g, 1024, 0, st>>>(ea);
+    else k_emit_units<256, 8><<<g, 256, 0, st>>>(ea);
+    return true;
+  }
   bool first = true;
-  for (int pl = 0; pl < 2; pl++) {  // rows of different lengths: one launch per plane
+  for (int pl = 0; pl < 2; pl++) {  // (8-byte row words or unaligned planes) one launch per plane
     if (!nr[pl]) continue;
     EmitArgs e1 = ea;
     e1.n_rows[0] = pl == 0 ? nr[0] : 0u;  // the row list is [plane 0 rows][plane 1 rows]
     e1.n_rows[1] = pl == 1 ? nr[1] : 0u;
     e1.row_words = rw[pl];
-    if (!first) e1.st_bytes = e1.reset_n = 0;
+    if (!first) e1.st_bytes = e1.reset_n[0] = e1.reset_n[1] = e1.reset_n[2] = 0;
     first = false;
     enq_emit_launch(e1, st, pl == 0 ? out_in : reinterpret_cast<uint64_t*>(16), pl == 1 ? out_eg : reinterpret_cast<uint64_t*>(16));
   }
@@ -4601,7 +4682,10 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fa.VALID = c->VALID.as<uint64_t>();
   fa.DESCW = c->DESCW.as<int32_t>();
   fa.DM = c->DM.as<uint64_t>();
-  fa.nb[2] = blocks((uint64_t(K) * W + 3) / 4);
+  // the slot words (VALID / DESCW / DM per 64 destinations) serve only egress class rows whose
+  // destinations do not all share each slot's descriptor (uni_desc: the UNI class rows read udesc)
+  const bool slot_words = !c->uni_desc || !(ido_mode(c) || pl_wave_ok(c)) || !c->pb.blocks.empty();
+  fa.nb[2] = slot_words ? blocks((uint64_t(K) * W + 3) / 4) : 0u;
   fa.S = c->n_sel;
   fa.L = pb.L;
   fa.sel_off = c->sel_off.as<uint32_t>();
@@ -4713,16 +4797,12 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
       fd.ra[d].A = d == 0 ? out_in : out_eg;
       fd.ra[d].arow = c->arow[d].as<uint32_t>();
     }
-    if (!ido) {  // PM builds: launch D (k_front_d_pm) is the class rows from flattened peer lists
-      fd.nb[d] = pl_blocks(c, d);
-      if (d == 1 && c->uni_desc && c->pb.blocks.empty()) fd.ra[d].udesc = c->udesc.as<int32_t>();
-      fd.ra[d].pod_sparse = pod_sparse(c);  // pod rows from pod_rows_sparse_blk (launch C)
-      continue;
-    }
-    // launch D elects the classes (no launch C) while it builds the identity sets; launch E's blocks
-    // then empty the hash table for the next run
-    fc.nb[d] = 0;
-    {
+    // PM builds elect the classes inside their class-row blocks (launch D; the emit then empties the
+    // hash table; batched blocks keep the election launch).  IDO builds keep launch C: electing inside
+    // the identity-set waves put the election chain on every wave (config #3: C + D 29 -> 45 us, r04a)
+    const bool elect = !ido && c->pb.blocks.empty();
+    if (elect) {
+      fc.nb[d] = 0;
       const MemberArgs& ma = fb.ma[d];
       RowArgs& ra = fd.ra[d];
       ra.act = ma.act;
@@ -4736,8 +4816,18 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
       ra.reps_w = ma.reps;
       ra.rep_cnt_w = ma.rep_cnt;
     }
+    if (!ido) {  // PM builds: launch D (k_front_d_pm) is the class rows from flattened peer lists
+      fd.nb[d] = pl_blocks(c, d);
+      if (d == 1 && c->uni_desc && c->pb.blocks.empty()) fd.ra[d].udesc = c->udesc.as<int32_t>();
+      fd.ra[d].pod_sparse = pod_sparse(c);  // pod rows from pod_rows_sparse_blk (launch C)
+      if (elect) {
+        fd.ra[d].ht_clear_words = 0;
+        c->emit_clears_ht[d] = true;
+      }
+      continue;
+    }
     fe.ra[d] = fd.ra[d];
-    fd.ra[d].ht_clear_words = 0;
+    fe.ra[d].ht_clear_words = 0;  // (launch D's identity sets empty it)
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + CI_G - 1) / CI_G) + 3) / 4);
     // egress with one descriptor per slot (udesc): only the block's slots' sets are staged
     if (d == 1 && c->uni_desc) fe.ra[d].udesc = c->udesc.as<int32_t>();
@@ -4779,14 +4869,16 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (gc) k_front_c<<<unsigned(gc), 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
-    if (fd.nb[0] + fd.nb[1] && pl_wave_ok(c)) k_front_d_pm<true><<<fd.nb[0] + fd.nb[1], pl_threads(c), 0, st>>>(fd);
-    else if (fd.nb[0] + fd.nb[1]) k_front_d_pm<false><<<fd.nb[0] + fd.nb[1], pl_threads(c), 0, st>>>(fd);
+    const bool elect = c->pb.blocks.empty(), wave = pl_wave_ok(c);
+    const unsigned gd = fd.nb[0] + fd.nb[1];
+    if (gd && wave && elect) k_front_d_pm<true, true><<<gd, pl_threads(c), 0, st>>>(fd);
+    else if (gd && elect) k_front_d_pm<false, true><<<gd, pl_threads(c), 0, st>>>(fd);
+    else if (gd && wave) k_front_d_pm<true, false><<<gd, pl_threads(c), 0, st>>>(fd);
+    else if (gd) k_front_d_pm<false, false><<<gd, pl_threads(c), 0, st>>>(fd);
     if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
     return true;
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
-  for (int d = 0; d < 2; d++)  // an election without class rows (an empty word window): the table is emptied here
-    if (fd.nb[d] && !fe.nb[d]) enq_member_clear(c, d, st);
   if (fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
     k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);
   } else {  // the directions' class rows as two launches, each at its own register budget (egress 101

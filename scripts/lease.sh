@@ -11,6 +11,7 @@
 #   scale CFG                  scripts/partition_scaling.py (one-GPU shard timings, both partitions)
 #   tl CFG [N]                 kernel timeline of back-to-back steps (scripts/graph_timeline.py)
 #   py SCRIPT [args]           any python script under scripts/ (180 s limit)
+#   ab CFG SPEC...             kernel stats per library variant (scripts/ab_kernels.sh; REPS env, CYC_SHARD tokens)
 # Invocations are recorded in scripts/LEASES.md.
 set -e
 NAME=$1; shift
@@ -49,6 +50,7 @@ for spec in "$@"; do
       prof_env
       timeout -k 10 120 rocprofv3 --kernel-trace -d $OUT/tl_$tag -o run -- python3 scripts/graph_timeline.py run "$@" > $OUT/tl_$tag.log 2>&1 ;;
     py) timeout -k 10 180 python -u scripts/"$@" > $OUT/py_$tag.log 2>&1 ;;
+    ab) timeout -k 10 900 bash scripts/ab_kernels.sh $NAME "$@" ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
   for e in "${envs[@]}"; do unset "${e%%=*}"; done
