@@ -3776,6 +3776,7 @@ static void prepare_device(cyc_ctx* c) {
   clk.lap("label tables");
   c->PM.alloc(std::max<uint64_t>(R * W * 8, 16));
   c->ip_rng.alloc(std::max<uint64_t>(R * 16 + R * ((W + 63) / 64) * 4, 16));  // [R][4] word spans + chunk masks, then [R][W/64] cnz
+  c->ip_rng_clean = false;  // a new buffer: the next fused front fills it (no emit has reset it yet)
   c->ER.alloc(pb.may_err ? std::max<uint64_t>(R * W * 8, 16) : 16);
   {
     c->plan = plan_peers(pb, c->ids[1]);
@@ -4493,6 +4494,24 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
 // status plane, copied by the (first) emit's blocks.  Returns false if no emit was launched (no rows
 // in the plan; the caller then copies the status plane itself).
 constexpr uint64_t EMIT_WIDE_MIN = 16384;  // shortest plane row (bytes) emitted a block per row; shorter: k_emit_flat
+// k_emit_units over ea.n_rows[] rows of ea.pl_words[] words per plane (16-byte aligned planes, even
+// row words): units of about one 1024 x 7 x 16 B block pass (114 KB) — whole rows of up to that, or
+// several shorter rows — so a block resolves its rows' order -> identity -> class chains together
+static void enq_emit_units(EmitArgs ea, hipStream_t st) {
+  constexpr uint64_t pass = 1024 * 7 * 16;
+  for (int pl = 0; pl < 2; pl++) {
+    const uint64_t rb = std::max<uint64_t>(ea.pl_words[pl] * 8, 1);
+    ea.unit_rows[pl] = uint32_t(std::min<uint64_t>(EMIT_UNIT_MAX_ROWS, std::max<uint64_t>(1, pass / rb)));
+    ea.n_units[pl] = (ea.n_rows[pl] + ea.unit_rows[pl] - 1) / ea.unit_rows[pl];
+  }
+  ea.per_xcd = (ea.n_units[0] + ea.n_units[1] + 7) / 8;
+  k_emit_units<1024, 7><<<ea.per_xcd * 8, 1024, 0, st>>>(ea);
+}
+
+// Plane rows up to this length (bytes) are emitted as units of several rows (k_emit_units) when
+// both planes' rows are alike; longer rows a block each (k_emit_wide)
+constexpr uint64_t EMIT_UNITS_MAX = 512 * 7 * 16;
+
 static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out_in, uint64_t* out_eg) {
   EmitArgs ea = ea_in;
   ea.per_xcd = (ea.n_rows[0] + ea.n_rows[1] + 7) / 8;
@@ -4503,6 +4522,10 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
+  if (row_bytes <= EMIT_UNITS_MAX && !ea.interleave) {
+    enq_emit_units(ea, st);
+    return;
+  }
   // 16-byte chunks per thread and pass <= 8 keeps a block at <= 48 VGPRs (8 waves a SIMD): a 512 x 13
   // one-pass block held 84 VGPRs, 5 waves a SIMD, and ran config #3 3.5 % slower per step on a slow
   // box (profiles/r03_emit_ab.txt; 512 x 7 in two passes was slower still)
@@ -4597,18 +4620,9 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   // rows of different lengths (a source shard): ONE launch over units of about one block pass each
   const bool aligned = reinterpret_cast<uintptr_t>(out_in) % 16 == 0 && reinterpret_cast<uintptr_t>(out_eg) % 16 == 0;
   if (aligned && rw[0] % 2 == 0 && rw[1] % 2 == 0) {
-    const uint64_t longest = std::max(nr[0] ? rw[0] : 0, nr[1] ? rw[1] : 0) * 8;
-    const bool big = longest > 512 * 7 * 16;  // 1024 x 7 x 16 B passes for rows over 56 KB, else 256 x 8
-    const uint64_t pass = big ? 1024 * 7 * 16 : 256 * 8 * 16;
-    for (int pl = 0; pl < 2; pl++) {
-      ea.n_rows[pl] = nr[pl];
-      ea.unit_rows[pl] = uint32_t(std::min<uint64_t>(EMIT_UNIT_MAX_ROWS, std::max<uint64_t>(1, pass / std::max<uint64_t>(rw[pl] * 8, 1))));
-      ea.n_units[pl] = (nr[pl] + ea.unit_rows[pl] - 1) / ea.unit_rows[pl];
-    }
-    ea.per_xcd = (ea.n_units[0] + ea.n_units[1] + 7) / 8;
-    const unsigned g = ea.per_xcd * 8;
-    if (big) k_emit_units<1024, 7><<<g, 1024, 0, st>>>(ea);
-    else k_emit_units<256, 8><<<g, 256, 0, st>>>(ea);
+    ea.n_rows[0] = nr[0];
+    ea.n_rows[1] = nr[1];
+    enq_emit_units(ea, st);
     return true;
   }
   bool first = true;
