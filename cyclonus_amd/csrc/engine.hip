@@ -1291,17 +1291,6 @@ struct RowArgs {
   // kernel in block slices once k_classify is done with it: no memset node precedes k_member
   uint32_t* ht_clear;
   uint64_t ht_clear_words;
-  // the class election inside the PM class rows (fused PM fronts, class_rows_pl_blk ELECT): the
-  // membership's hash table and each identity's hash; class_of is written there
-  const uint32_t* act;
-  uint32_t n_act, ht_cap;
-  const unsigned long long* ht_key;
-  const uint32_t* ht_rep;
-  const uint64_t* hash;
-  const uint32_t* id_blk;
-  uint32_t* class_of_w;
-  uint32_t* reps_w;
-  uint32_t* rep_cnt_w;
 };
 
 // Row of A holding representative i's class rows: its identity slot, or (in-place class rows) the
@@ -1792,7 +1781,6 @@ struct PlShared {  // one per block, shared by both directions' instantiations o
   uint32_t pre[PL_TGT + 1], poff[PL_TGT];
   uint32_t all;
   int32_t rdu[32];  // ingress, K <= 32: the representative's job descriptor per slot (-1: slot not VALID)
-  uint32_t rl[256], nrl;  // ELECT: the representatives among the block's identities just elected
 };
 
 constexpr int PL_ITEMS = 1;
@@ -2060,44 +2048,14 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
   }
 }
 
-template <bool EGRESS, bool WAVE, bool ELECT = false>
+template <bool EGRESS, bool WAVE>
 __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
-  ht_clear_slice(a, bid_, nblk_);  // (ELECT: the emit empties the table instead)
-  const uint32_t nkc = (a.K + KC - 1) / KC;
+  ht_clear_slice(a, bid_, nblk_);
+  const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC;
   const bool kbits = EGRESS ? a.portbits != nullptr : a.K <= 32;
-  // ELECT (fused PM fronts: no class-election launch): block b elects the classes of its own slice of
-  // the active identities, a thread each (class_of_identity), collects the slice's representatives
-  // in LDS, and computes their class rows; otherwise the blocks stride over the elected representatives.
-  const uint32_t per = ELECT ? (a.n_act + nblk_ - 1) / nblk_ : 0u;
-  const uint32_t lo = ELECT ? min(a.n_act, bid_ * per) : 0u, hi = ELECT ? min(a.n_act, lo + per) : 0u;
-  const uint32_t n_reps = ELECT ? 0u : *a.rep_cnt + 1u;
-  uint32_t chunk = lo;  // ELECT: the slice's identities [chunk, chunk + blockDim.x) elected last
-  uint32_t nloc = 0;    // and the representatives among them (sh.rl)
-  for (uint32_t r = ELECT ? 0u : bid_;; r += ELECT ? 1u : nblk_) {
-    if (ELECT) {
-      while (r >= nloc && chunk < hi) {  // elect the next chunk of the slice
-        __syncthreads();                 // (sh.rl / sh.nrl of the previous chunk are no longer read)
-        if (threadIdx.x == 0) sh.nrl = 0;
-        __syncthreads();
-        const uint32_t ii = chunk + threadIdx.x;
-        if (ii < hi) {
-          const uint32_t id = a.act[ii];
-          const uint32_t cl = class_of_identity(id, a.id_err, a.hash, a.ht_key, a.ht_rep, a.ht_cap, a.cnt, a.list_off, a.list,
-                                                a.id_blk, a.id_status, EGRESS ? nullptr : a.id_desc, a.K);
-          a.class_of_w[id] = cl;
-          if (cl == id) sh.rl[atomicAdd(&sh.nrl, 1u)] = id;
-        }
-        __syncthreads();
-        chunk += blockDim.x;
-        nloc = sh.nrl;
-        r = 0;
-      }
-      if (r >= nloc) break;
-    } else if (r >= n_reps) {
-      break;
-    }
-    const uint32_t i = ELECT ? sh.rl[r] : a.reps[r];
+  for (uint32_t r = bid_; r < n_reps; r += nblk_) {
+    const uint32_t i = a.reps[r];
     const uint32_t nt = a.cnt[i];
     const uint32_t* lst = a.list + a.list_off[i];
     uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
@@ -2225,14 +2183,27 @@ __global__ __launch_bounds__(256) void k_class_rows_pl(RowArgs a) {
 // 256 pod words); the representative's identity sets for those slots (ingress) or for every job
 // descriptor (egress) are staged in LDS, each thread expands them over its word's identity runs
 // (one 48-byte record), then ORs in the class's IP peers (PM words; the only per-pod peers).
-__device__ __forceinline__ uint64_t expand_runs(const uint64_t* brow, const WordRuns& wr) {
-  uint64_t m = 0;
+// The staged sets are 32-bit words with the block's rows interleaved (IdoRuns): a run's bit of
+// every slot row is one LDS read, and a run adds its pods to a slot's word with a sign-extended
+// bit field and two and-or operations (v_bfe_i32, v_and_or_b32) instead of a 64-bit shift, compare
+// and two selects: config #3's class rows issued ~1,000 VALU instructions per wave, ~75 % of
+// the launch at 4 cycles each (profiles/r04_pmc_config3.txt).
+struct IdoRuns {  // a thread's word's identity runs, resolved against the staged layout
+  uint32_t off[IDO_MAX_RUNS];  // (identity >> 5) * rows: the run's 32-bit word in a representative's sets
+  uint32_t sh[IDO_MAX_RUNS];   // identity & 31
+  uint32_t lo[IDO_MAX_RUNS], hi[IDO_MAX_RUNS];  // the run's pods in the word (0: unused run)
+};
+__device__ __forceinline__ void ido_or_run(uint32_t bits, uint32_t sh, uint32_t lo, uint32_t hi, uint32_t& alo, uint32_t& ahi) {
+  const uint32_t sel = uint32_t(__builtin_amdgcn_sbfe(int(bits), sh, 1));  // 0 or ~0
+  alo |= lo & sel;
+  ahi |= hi & sel;
+}
+// Row `row` of a representative's staged sets (sq) expanded over the word's runs.
+__device__ __forceinline__ uint64_t expand_runs32(const uint32_t* sq, uint32_t row, const IdoRuns& ir) {
+  uint32_t alo = 0, ahi = 0;
 #pragma unroll
-  for (uint32_t x = 0; x < IDO_MAX_RUNS; x++) {
-    const uint32_t e = wr.e[x];
-    m |= ((brow[e >> 6] >> (e & 63)) & 1) ? wr.m[x] : 0ull;
-  }
-  return m;
+  for (uint32_t x = 0; x < IDO_MAX_RUNS; x++) ido_or_run(sq[ir.off[x] + row], ir.sh[x], ir.lo[x], ir.hi[x], alo, ahi);
+  return (uint64_t(ahi) << 32) | alo;
 }
 
 constexpr uint32_t IDO_RPB_MAX = 64;  // class_rpb's upper bound
@@ -2286,7 +2257,7 @@ struct RepHead {  // a class-row block's representative: identity, class-row ind
 // only the block's KC descriptors' identity sets are staged (config #3 / #4: identical containers).
 template <bool EGRESS, int KC, bool UNI = false>
 __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uint32_t nblk_) {
-  extern __shared__ uint64_t sB[];
+  extern __shared__ __attribute__((aligned(16))) uint64_t sB[];
   // block = (a.rpb consecutive class representatives, KC job slots, 256 pod words): each word's runs
   // and slot words are loaded once for all its representatives
   const uint32_t cg = ido_chunk_groups(a.WA), nkc = (a.K + KC - 1) / KC;
@@ -2294,7 +2265,10 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   const uint32_t r0 = (bid_ / (cg * nkc)) * a.rpb, n_reps = *a.rep_cnt + 1u;
   if (r0 >= n_reps) return;  // whole block
   const uint32_t nr = min(a.rpb, n_reps - r0), k0 = kc * KC;
-  const uint32_t nrow = EGRESS && !UNI ? a.NB : min(uint32_t(KC), a.K - k0), rowsz = nrow * a.EW;
+  const uint32_t nrow = EGRESS && !UNI ? a.NB : min(uint32_t(KC), a.K - k0);
+  // staged layout: 32-bit word j of row r of representative q at sB32[(q * EW32 + j) * NS + r]
+  const uint32_t NS = EGRESS && !UNI ? a.NB : uint32_t(KC), EW32 = 2 * a.EW;
+  uint32_t* const sB32 = reinterpret_cast<uint32_t*>(sB);
   const uint32_t wend = a.w0 + a.WA;
   // the word's own loads (runs) are issued before the staging barrier, so their latency overlaps the
   // staging loads instead of following them
@@ -2330,35 +2304,40 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
 #pragma unroll
   for (int kk = 0; kk < KC; kk++) ud[kk] = EGRESS && UNI ? a.udesc[min(k0 + kk, a.K - 1)] : 0;
   __syncthreads();
-  {  // identity sets: nr x rowsz words, 4 loads per thread in flight at once
-    const uint32_t tot = nr * rowsz;
-    for (uint32_t x0 = threadIdx.x; x0 < tot; x0 += 4 * blockDim.x) {
-      uint64_t v[4];
+  {  // identity sets: a wave per (representative, row) at a time, lanes over the row's words, 4 rows'
+     // loads in flight; (representative, row) is wave-uniform, so the transposing index math is scalar
+    const uint32_t nrows = nr * nrow, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t r0 = wv; r0 < nrows; r0 += 4 * nw)
+      for (uint32_t j0 = 0; j0 < a.EW; j0 += 64) {
+        const uint32_t j = min(j0 + lane, a.EW - 1);
+        uint64_t v[4];
 #pragma unroll
-      for (uint32_t u = 0; u < 4; u++) {
-        const uint32_t x = min(x0 + u * blockDim.x, tot - 1), q = x / rowsz, r = x - q * rowsz;
-        const uint64_t i = s_rep[q].i;
-        const uint64_t* src;
-        if (EGRESS && UNI) {  // the sets of the block's slots' descriptors, one row each
-          const uint32_t kk = r / a.EW;
-          int32_t d = ud[0];
+        for (uint32_t u = 0; u < 4; u++) {
+          const uint32_t qr = min(r0 + u * nw, nrows - 1), q = qr / nrow, row = qr - q * nrow;
+          const uint64_t i = s_rep[q].i;
+          int32_t d = EGRESS ? int32_t(row) : int32_t(k0 + row);  // the set's row in B
+          if (EGRESS && UNI) {  // the sets of the block's slots' descriptors, one row each
+            d = ud[0];
 #pragma unroll
-          for (int y = 1; y < KC; y++) d = uint32_t(y) == kk ? ud[y] : d;
-          src = a.B + (i * a.NB + uint32_t(d)) * a.EW + (r - kk * a.EW);
-        } else {
-          src = a.B + (i * a.NB + (EGRESS ? 0u : k0)) * a.EW + r;
+            for (int y = 1; y < KC; y++) d = uint32_t(y) == row ? ud[y] : d;
+          }
+          v[u] = a.B[(i * a.NB + uint32_t(d)) * a.EW + j];
         }
-        v[u] = *src;
-      }
 #pragma unroll
-      for (uint32_t u = 0; u < 4; u++)
-        if (x0 + u * blockDim.x < tot) sB[x0 + u * blockDim.x] = v[u];
-    }
+        for (uint32_t u = 0; u < 4; u++) {
+          const uint32_t qr = r0 + u * nw, q = qr / nrow, row = qr - q * nrow;
+          if (qr >= nrows || j0 + lane >= a.EW) continue;
+          uint32_t* dst = sB32 + (q * EW32 + 2 * j) * NS + row;
+          dst[0] = uint32_t(v[u]);
+          dst[NS] = uint32_t(v[u] >> 32);
+        }
+      }
   }
   // the first IDO_IPL IP peers of each representative: (PM row, first word, last word, port bits —
   // egress: the descriptor bit row; ingress: a bit per block slot), so the row loop issues only the
   // PM loads (no list -> port table chain per batch)
-  uint4* s_il = reinterpret_cast<uint4*>(sB + ((nr * rowsz + 1) & ~1u));  // 16-byte aligned
+  uint4* s_il = reinterpret_cast<uint4*>(sB32 + ((nr * EW32 * NS + 3) & ~3u));  // 16-byte aligned
   const bool stage_ip = !EGRESS || a.portbits != nullptr;
   if (stage_ip) {
     for (uint32_t t = threadIdx.x; t < nr * IDO_IPL; t += blockDim.x) {
@@ -2385,7 +2364,14 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   // 16-byte stores of word pairs (store_row_pair): even rows of the class rows' window, aligned base
   const bool pair = a.WA % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
   if (w >= wend) return;  // no barrier below
-  const WordRuns& wcur = wr;
+  IdoRuns ir;
+#pragma unroll
+  for (uint32_t x = 0; x < IDO_MAX_RUNS; x++) {
+    ir.off[x] = (wr.e[x] >> 5) * NS;
+    ir.sh[x] = wr.e[x] & 31;
+    ir.lo[x] = uint32_t(wr.m[x]);
+    ir.hi[x] = uint32_t(wr.m[x] >> 32);
+  }
   const uint64_t wmask = (w == a.W - 1) ? lastmask : ~0ull;
   uint64_t valid[KC];
   int32_t du[KC];
@@ -2404,24 +2390,47 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   }
   for (uint32_t q = 0; q < nr; q++) {
     const RepHead<KC>& h = s_rep[q];
-    const uint64_t* sb = sB + q * rowsz;
+    const uint32_t* sq = sB32 + q * EW32 * NS;
     uint64_t allow[KC];
+    if (!EGRESS) {  // the destination's slots: per representative (block-uniform)
 #pragma unroll
-    for (int kk = 0; kk < KC; kk++) {
-      const uint32_t k = k0 + kk;
-      allow[kk] = 0;
-      if (k < a.K) {
-        if (!EGRESS) {  // the destination's slot: per representative (block-uniform)
-          du[kk] = h.du[kk];
-          valid[kk] = du[kk] >= 0 ? wmask : 0ull;
-        }
+      for (int kk = 0; kk < KC; kk++) {
+        du[kk] = k0 + kk < a.K ? h.du[kk] : -2;
+        valid[kk] = du[kk] >= 0 ? wmask : 0ull;
+      }
+    }
+    if (EGRESS && !UNI) {  // per destination word: its slots' descriptors' rows
+#pragma unroll
+      for (int kk = 0; kk < KC; kk++) {
+        const uint32_t k = k0 + kk;
+        allow[kk] = 0;
+        if (k >= a.K) continue;
         if (du[kk] >= 0) {
-          allow[kk] = expand_runs(sb + uint64_t(EGRESS && !UNI ? uint32_t(du[kk]) : uint32_t(kk)) * a.EW, wcur);
-        } else if (EGRESS && !UNI && du[kk] == -1) {  // destinations with mixed job descriptors (rare)
+          allow[kk] = expand_runs32(sq, uint32_t(du[kk]), ir);
+        } else if (du[kk] == -1) {  // destinations with mixed job descriptors (rare)
           const uint64_t* dm = a.DM + uint64_t(k) * a.D * a.W + w;
-          for (uint32_t d = 0; d < a.D; d++) allow[kk] |= expand_runs(sb + uint64_t(d) * a.EW, wcur) & dm[uint64_t(d) * a.W];
+          for (uint32_t d = 0; d < a.D; d++) allow[kk] |= expand_runs32(sq, d, ir) & dm[uint64_t(d) * a.W];
         }
       }
+    } else {  // the block's KC slot rows (a slot not VALID is masked by valid[] at the store)
+      uint32_t alo[KC], ahi[KC];
+#pragma unroll
+      for (int kk = 0; kk < KC; kk++) alo[kk] = ahi[kk] = 0;
+#pragma unroll
+      for (uint32_t x = 0; x < IDO_MAX_RUNS; x++) {
+        if constexpr (KC == 4) {
+          const uint4 b = *reinterpret_cast<const uint4*>(sq + ir.off[x]);
+          ido_or_run(b.x, ir.sh[x], ir.lo[x], ir.hi[x], alo[0], ahi[0]);
+          ido_or_run(b.y, ir.sh[x], ir.lo[x], ir.hi[x], alo[1], ahi[1]);
+          ido_or_run(b.z, ir.sh[x], ir.lo[x], ir.hi[x], alo[2], ahi[2]);
+          ido_or_run(b.w, ir.sh[x], ir.lo[x], ir.hi[x], alo[3], ahi[3]);
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < KC; kk++) ido_or_run(sq[ir.off[x] + kk], ir.sh[x], ir.lo[x], ir.hi[x], alo[kk], ahi[kk]);
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < KC; kk++) allow[kk] = (uint64_t(ahi[kk]) << 32) | alo[kk];
     }
     // IP peers (ippeermatcher.go:43-50): per pod word through the PM rows, PEER_BATCH peers' words
     // loaded at once (no panic in IDO builds: the OR is order-free; the undecided check only ends
@@ -2715,14 +2724,13 @@ __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   if (b < f.nb[0]) class_ident_blk<false, CI_G>(f.ra[0], b, f.nb[0]);
   else class_ident_blk<true, CI_G>(f.ra[1], b - f.nb[0], f.nb[1]);
 }
-// PM builds (pod-peer words from materialised rows): the class rows, egress blocks first; ELECT: each
-// block elects the classes of its slice of the identities first (no class-election launch)
-template <bool WAVE, bool ELECT>
+// PM builds (pod-peer words from materialised rows): the class rows, egress blocks first
+template <bool WAVE>
 __global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
   __shared__ PlShared sh;
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_pl_blk<true, WAVE, ELECT>(f.ra[1], sh, b, f.nb[1]);
-  else class_rows_pl_blk<false, WAVE, ELECT>(f.ra[0], sh, b - f.nb[1], f.nb[0]);
+  if (b < f.nb[1]) class_rows_pl_blk<true, WAVE>(f.ra[1], sh, b, f.nb[1]);
+  else class_rows_pl_blk<false, WAVE>(f.ra[0], sh, b - f.nb[1], f.nb[0]);
 }
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's
@@ -2749,8 +2757,9 @@ struct EmitArgs {
   uint32_t n_rows[2];         // plane rows of this launch (pods [row_lo, row_lo + n_rows)); 0 = plane not in it
   uint32_t row_lo[2];
   uint32_t per_xcd;           // rows of the n_rows[0] + n_rows[1] row list per XCD segment
-  const uint32_t* order[2];   // pods in [row_lo,row_hi) clustered by the plane's class
-  const uint32_t *pod_id[2], *class_of[2];
+  const uint2* order[2];      // (pod, identity) of the pods in [row_lo,row_hi), clustered by the plane's
+                              // identity: a row's class is one dependent load away (class_of[identity])
+  const uint32_t* class_of[2];
   const uint64_t* A[2];
   const uint32_t* arow[2];    // in-place class rows (RowArgs::arow): the class row is a row of out
   uint64_t* out[2];
@@ -2765,28 +2774,26 @@ struct EmitArgs {
   // words, rows per unit (a unit = one block's pass) and units; the unit list is [plane 0][plane 1]
   uint64_t pl_words[2];
   uint32_t unit_rows[2], n_units[2];
-  // buffers reset to ~0 for the NEXT run in block slices (their readers are all done): the IP rows'
-  // word-span records (RowArgs::ip_rng) and, for PM builds whose class rows elect the classes, the
-  // membership hash tables — no fill launch or memset node before the next front
-  uint32_t* reset[3];
-  uint64_t reset_n[3];
+  // the IP rows' word-span records (RowArgs::ip_rng), reset to ~0 for the NEXT run in block slices
+  // (their readers are all done): no fill launch or memset node before the next front
+  uint32_t* reset;
+  uint64_t reset_n;
 };
 
-// Row r of the row list -> (plane, pod).
-__device__ __forceinline__ void emit_row_of(const EmitArgs& a, uint32_t r, uint32_t& pl, uint32_t& p) {
+// Row r of the row list -> (plane, (pod, identity)).
+__device__ __forceinline__ uint2 emit_row_of(const EmitArgs& a, uint32_t r, uint32_t& pl) {
   if (a.interleave) {
     pl = r & 1u;
-    p = a.order[pl][r >> 1];
-  } else {
-    pl = r >= a.n_rows[0] ? 1u : 0u;
-    p = a.order[pl][r - pl * a.n_rows[0]];
+    return a.order[pl][r >> 1];
   }
+  pl = r >= a.n_rows[0] ? 1u : 0u;
+  return a.order[pl][r - pl * a.n_rows[0]];
 }
 
-// Source of plane pl's row for pod p: its class row; null when the row is itself its class's row
-// (in-place class rows: nothing to copy).
-__device__ __forceinline__ const uint64_t* emit_src(const EmitArgs& a, uint32_t pl, uint32_t p) {
-  const uint32_t c = a.class_of[pl][a.pod_id[pl][p]];
+// Source of plane pl's row for (pod, identity) pi: its class row; null when the row is itself its
+// class's row (in-place class rows: nothing to copy).
+__device__ __forceinline__ const uint64_t* emit_src(const EmitArgs& a, uint32_t pl, uint2 pi) {
+  const uint32_t p = pi.x, c = a.class_of[pl][pi.y];
   if (!a.arow[pl]) return a.A[pl] + uint64_t(c) * a.pl_words[pl];
   const uint32_t r = a.arow[pl][c];
   return r == p - a.row_lo[pl] ? nullptr : a.out[pl] + uint64_t(r) * a.pl_words[pl];
@@ -2794,12 +2801,10 @@ __device__ __forceinline__ const uint64_t* emit_src(const EmitArgs& a, uint32_t 
 
 // Block b's slice of the status plane copy and of the word-span reset (every emit kernel calls this first).
 __device__ __forceinline__ void emit_status(const EmitArgs& a) {
-#pragma unroll
-  for (int x = 0; x < 3; x++) {
-    if (!a.reset_n[x]) continue;
-    const uint64_t per = (a.reset_n[x] + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
-    const uint64_t hi = lo + per < a.reset_n[x] ? lo + per : a.reset_n[x];
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.reset[x][i] = 0xFFFFFFFFu;
+  if (a.reset_n) {
+    const uint64_t per = (a.reset_n + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
+    const uint64_t hi = lo + per < a.reset_n ? lo + per : a.reset_n;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) a.reset[i] = 0xFFFFFFFFu;
   }
   if (!a.st_bytes) return;
   const uint64_t per = (a.st_bytes + gridDim.x - 1) / gridDim.x, lo = uint64_t(blockIdx.x) * per;
@@ -2817,11 +2822,11 @@ __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
   emit_status(a);
   const uint32_t b = blockIdx.x, x = b & 7, r = x * a.per_xcd + (b >> 3);
   if (r >= min(a.n_rows[0] + a.n_rows[1], (x + 1) * a.per_xcd)) return;
-  uint32_t pl, p;
-  emit_row_of(a, r, pl, p);
-  const uint64_t* src = emit_src(a, pl, p);
+  uint32_t pl;
+  const uint2 pi = emit_row_of(a, r, pl);
+  const uint64_t* src = emit_src(a, pl, pi);
   if (!src) return;
-  uint64_t* dst = a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.row_words;
+  uint64_t* dst = a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.row_words;
   for (uint64_t i = threadIdx.x; i < a.row_words; i += blockDim.x) dst[i] = src[i];
 }
 
@@ -2845,10 +2850,10 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   const u64x2* src = nullptr;
   u64x2* dst = nullptr;
   if (threadIdx.x < nr) {
-    uint32_t pl, p;
-    emit_row_of(a, r0 + threadIdx.x, pl, p);
-    src = reinterpret_cast<const u64x2*>(emit_src(a, pl, p));
-    dst = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.row_words);
+    uint32_t pl;
+    const uint2 pi = emit_row_of(a, r0 + threadIdx.x, pl);
+    src = reinterpret_cast<const u64x2*>(emit_src(a, pl, pi));
+    dst = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.row_words);
   }
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t keep = __ballot(src != nullptr);
@@ -2889,11 +2894,11 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   const uint32_t b = blockIdx.x, n = a.n_rows[0] + a.n_rows[1], x = b & 7;
   const uint32_t r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
   if (r >= min(n, (x + 1) * a.per_xcd)) return;
-  uint32_t pl, p;
-  emit_row_of(a, r, pl, p);
-  const u64x2* si = reinterpret_cast<const u64x2*>(emit_src(a, pl, p));
+  uint32_t pl;
+  const uint2 pi = emit_row_of(a, r, pl);
+  const u64x2* si = reinterpret_cast<const u64x2*>(emit_src(a, pl, pi));
   if (!si) return;  // in-place class row: already written
-  u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.row_words);
+  u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.row_words);
   const uint32_t n2 = uint32_t(a.row_words / 2);
   for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS * UNROLL) {
     u64x2 v[UNROLL];
@@ -2929,12 +2934,12 @@ __global__ __launch_bounds__(BS) void k_emit_units(EmitArgs a) {
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   if (threadIdx.x < nr) {
-    const uint32_t p = a.order[pl][r0 + threadIdx.x];
-    const u64x2* src = reinterpret_cast<const u64x2*>(emit_src(a, pl, p));
+    const uint2 pi = a.order[pl][r0 + threadIdx.x];
+    const u64x2* src = reinterpret_cast<const u64x2*>(emit_src(a, pl, pi));
     if (src) {  // (row order within the unit does not matter: each row is copied whole)
       const uint32_t k = atomicAdd(&s_cnt, 1u);
       s_src[k] = src;
-      s_dst[k] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(p - a.row_lo[pl]) * a.pl_words[pl]);
+      s_dst[k] = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.pl_words[pl]);
     }
   }
   __syncthreads();
@@ -3446,7 +3451,6 @@ struct cyc_ctx {
   // so the next fused front needs no fill before its IP rows (and, without a selector table, no launch A)
   bool ip_rng_clean = false;
   bool capturing = false;  // a hipGraph capture is in progress (captured steps always fill the spans themselves)
-  bool emit_clears_ht[2] = {false, false};  // this run's emit empties the direction's hash table (PM ELECT)
   bool ran = false;    // a run has been enqueued
   hipEvent_t run_done = nullptr;  // recorded on the run's stream after every run (cyc_last_classes)
   // batched blocks (cyc_probe_prepare_blocks; pb.blocks non-empty)
@@ -4067,14 +4071,19 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
       c->ido_ew1 = e0 == UINT32_MAX ? 0u : (e1 + 63) / 64;
     }
   }
-  for (int d = 0; d < 2; d++) {  // emit row order: clustered by this direction's identity
+  for (int d = 0; d < 2; d++) {  // emit row order: clustered by this direction's identity, (pod, identity) pairs
     std::vector<uint32_t> ord(size_t(c->rh[d] - c->rl[d]));
     std::iota(ord.begin(), ord.end(), uint32_t(c->rl[d]));
     const auto& i1 = c->ids[d].of_pod;
     const auto& i2 = c->ids[1 - d].of_pod;
     std::stable_sort(ord.begin(), ord.end(),
                      [&](uint32_t x, uint32_t y) { return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y]; });
-    upload(c->order[d], ord);
+    std::vector<uint32_t> pairs(ord.size() * 2);
+    for (size_t r = 0; r < ord.size(); r++) {
+      pairs[2 * r] = ord[r];
+      pairs[2 * r + 1] = i1[ord[r]];
+    }
+    upload(c->order[d], pairs);
   }
   std::vector<uint8_t> peer_needed(pb.peers.size(), 0), peer_dir(pb.peers.size(), 0);
   for (const DTarget& t : pb.tgt[1])
@@ -4473,7 +4482,7 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     if (d == 0) k_class_ident<false, CI_G><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
     else k_class_ident<true, CI_G><<<unsigned((waves + 3) / 4), 256, 0, st>>>(ra);
     ra.ht_clear_words = 0;
-    const uint32_t rows = d == 0 ? std::min<uint32_t>(4, K) : D;
+    const uint32_t rows = d == 0 ? 4u : D;  // (class_rows_ido_blk stages KC = 4 slot rows, or D descriptor rows)
     const size_t per = size_t(rows) * ra.EW * 8 + IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
     ra.rpb = class_rpb(c, per);
     const unsigned gi = unsigned(uint64_t(ido_chunk_groups(ra.WA)) * ((K + 3) / 4) * ((c->n_act[d] + ra.rpb - 1) / ra.rpb));
@@ -4508,9 +4517,6 @@ static void enq_emit_units(EmitArgs ea, hipStream_t st) {
   k_emit_units<1024, 7><<<ea.per_xcd * 8, 1024, 0, st>>>(ea);
 }
 
-// Plane rows up to this length (bytes) are emitted as units of several rows (k_emit_units) when
-// both planes' rows are alike; longer rows a block each (k_emit_wide)
-constexpr uint64_t EMIT_UNITS_MAX = 512 * 7 * 16;
 
 static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out_in, uint64_t* out_eg) {
   EmitArgs ea = ea_in;
@@ -4522,10 +4528,6 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
-  if (row_bytes <= EMIT_UNITS_MAX && !ea.interleave) {
-    enq_emit_units(ea, st);
-    return;
-  }
   // 16-byte chunks per thread and pass <= 8 keeps a block at <= 48 VGPRs (8 waves a SIMD): a 512 x 13
   // one-pass block held 84 VGPRs, 5 waves a SIMD, and ran config #3 3.5 % slower per step on a slow
   // box (profiles/r03_emit_ab.txt; 512 x 7 in two passes was slower still)
@@ -4572,33 +4574,22 @@ static bool enq_emit_blocks(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64
 static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, uint8_t* d_status, bool inplace = false) {
   Problem& pb = c->pb;
   c->ip_rng_clean = false;  // (set again below when this emit resets the spans for the next run)
-  const bool clears_ht[2] = {c->emit_clears_ht[0], c->emit_clears_ht[1]};
-  c->emit_clears_ht[0] = c->emit_clears_ht[1] = false;
   const uint32_t K = pb.K;
   const uint64_t rw[2] = {uint64_t(K) * c->win_wa, uint64_t(K) * pb.W};  // words per plane row
   uint32_t nr[2];
   for (int d = 0; d < 2; d++) nr[d] = rw[d] ? uint32_t(c->rh[d] - c->rl[d]) : 0u;
-  if (!pb.blocks.empty() || (!nr[0] && !nr[1]))  // no emit of ours empties the hash tables
-    for (int d = 0; d < 2; d++)
-      if (clears_ht[d]) enq_member_clear(c, d, st);
   if (!pb.blocks.empty()) return enq_emit_blocks(c, st, out_in, out_eg, d_status);
   if (!nr[0] && !nr[1]) return false;
   EmitArgs ea{};
   ea.st_src = c->slot_status.as<uint8_t>();
   ea.st_dst = d_status;
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
-  ea.reset[0] = c->ip_rng.as<uint32_t>();
-  ea.reset_n[0] = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
-  c->ip_rng_clean = ea.reset_n[0] != 0;
-  for (int d = 0; d < 2; d++)  // PM class rows that elected the classes leave the hash tables to the emit
-    if (clears_ht[d]) {
-      ea.reset[1 + d] = static_cast<uint32_t*>(c->dir[d].ht_key.p);
-      ea.reset_n[1 + d] = uint64_t(c->dir[d].ht_cap) * 3;
-    }
+  ea.reset = c->ip_rng.as<uint32_t>();
+  ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
+  c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
     ea.row_lo[pl] = uint32_t(c->rl[pl]);
-    ea.order[pl] = c->order[pl].as<uint32_t>();
-    ea.pod_id[pl] = c->dir[pl].pod_id.as<uint32_t>();
+    ea.order[pl] = c->order[pl].as<uint2>();
     ea.class_of[pl] = c->dir[pl].class_of.as<uint32_t>();
     ea.A[pl] = c->dir[pl].A.as<uint64_t>();
     ea.arow[pl] = inplace ? c->arow[pl].as<uint32_t>() : nullptr;
@@ -4632,7 +4623,7 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
     e1.n_rows[0] = pl == 0 ? nr[0] : 0u;  // the row list is [plane 0 rows][plane 1 rows]
     e1.n_rows[1] = pl == 1 ? nr[1] : 0u;
     e1.row_words = rw[pl];
-    if (!first) e1.st_bytes = e1.reset_n[0] = e1.reset_n[1] = e1.reset_n[2] = 0;
+    if (!first) e1.st_bytes = e1.reset_n = 0;
     first = false;
     enq_emit_launch(e1, st, pl == 0 ? out_in : reinterpret_cast<uint64_t*>(16), pl == 1 ? out_eg : reinterpret_cast<uint64_t*>(16));
   }
@@ -4811,33 +4802,13 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
       fd.ra[d].A = d == 0 ? out_in : out_eg;
       fd.ra[d].arow = c->arow[d].as<uint32_t>();
     }
-    // PM builds elect the classes inside their class-row blocks (launch D; the emit then empties the
-    // hash table; batched blocks keep the election launch).  IDO builds keep launch C: electing inside
-    // the identity-set waves put the election chain on every wave (config #3: C + D 29 -> 45 us, r04a)
-    const bool elect = !ido && c->pb.blocks.empty();
-    if (elect) {
-      fc.nb[d] = 0;
-      const MemberArgs& ma = fb.ma[d];
-      RowArgs& ra = fd.ra[d];
-      ra.act = ma.act;
-      ra.n_act = na;
-      ra.ht_cap = ma.ht_cap;
-      ra.ht_key = ma.ht_key;
-      ra.ht_rep = ma.ht_rep;
-      ra.hash = ma.hash;
-      ra.id_blk = ma.id_blk;
-      ra.class_of_w = c->dir[d].class_of.as<uint32_t>();
-      ra.reps_w = ma.reps;
-      ra.rep_cnt_w = ma.rep_cnt;
-    }
+    // (the class election keeps a launch of its own, C: electing inside the next launch's blocks put
+    // the election chain on every block — IDO identity sets C + D 29 -> 45 us, PM class rows C + D
+    // 79 -> 117 us on config #4: profiles/r04_elect_ab.txt)
     if (!ido) {  // PM builds: launch D (k_front_d_pm) is the class rows from flattened peer lists
       fd.nb[d] = pl_blocks(c, d);
       if (d == 1 && c->uni_desc && c->pb.blocks.empty()) fd.ra[d].udesc = c->udesc.as<int32_t>();
       fd.ra[d].pod_sparse = pod_sparse(c);  // pod rows from pod_rows_sparse_blk (launch C)
-      if (elect) {
-        fd.ra[d].ht_clear_words = 0;
-        c->emit_clears_ht[d] = true;
-      }
       continue;
     }
     fe.ra[d] = fd.ra[d];
@@ -4845,7 +4816,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + CI_G - 1) / CI_G) + 3) / 4);
     // egress with one descriptor per slot (udesc): only the block's slots' sets are staged
     if (d == 1 && c->uni_desc) fe.ra[d].udesc = c->udesc.as<int32_t>();
-    const size_t per = size_t(d == 0 || fe.ra[d].udesc ? std::min<uint32_t>(E_KC, K) : D) * fd.ra[d].EW * 8 +
+    const size_t per = size_t(d == 0 || fe.ra[d].udesc ? uint32_t(E_KC) : D) * fd.ra[d].EW * 8 +
                        IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
     fe.ra[d].rpb = class_rpb(c, per);
     fe.nb[d] = blocks(uint64_t(ido_chunk_groups(fe.ra[d].WA)) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
@@ -4883,12 +4854,9 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (gc) k_front_c<<<unsigned(gc), 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   if (!ido) {
-    const bool elect = c->pb.blocks.empty(), wave = pl_wave_ok(c);
     const unsigned gd = fd.nb[0] + fd.nb[1];
-    if (gd && wave && elect) k_front_d_pm<true, true><<<gd, pl_threads(c), 0, st>>>(fd);
-    else if (gd && elect) k_front_d_pm<false, true><<<gd, pl_threads(c), 0, st>>>(fd);
-    else if (gd && wave) k_front_d_pm<true, false><<<gd, pl_threads(c), 0, st>>>(fd);
-    else if (gd) k_front_d_pm<false, false><<<gd, pl_threads(c), 0, st>>>(fd);
+    if (gd && pl_wave_ok(c)) k_front_d_pm<true><<<gd, pl_threads(c), 0, st>>>(fd);
+    else if (gd) k_front_d_pm<false><<<gd, pl_threads(c), 0, st>>>(fd);
     if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
     return true;
   }

@@ -291,3 +291,52 @@ class PolicyTables:
         t.peer_except_off, t.peer_except_nil, t.except_cidr = (_arr(keep, _offsets(ex_cnt), np.int64, i64p),
                                                                _arr(keep, ex_nil, np.uint8, u8p), _arr(keep, exc, np.int32, i32p))
         self.c, self._keep = t, keep
+
+
+def _dump_struct(t, keep, f, prefix=""):
+    """Write a tables struct field by field: a "name kind count" line, then the raw bytes (kind i64 /
+    i32 / u8; count -1 = NULL).  tests/native/capi_driver.cpp --flat reads this back into the C struct."""
+    kinds = {ctypes.c_int64: "i64", ctypes.c_int32: "i32", ctypes.c_uint8: "u8"}
+    by_addr = {a.ctypes.data: a for a in keep if isinstance(a, np.ndarray)}
+    for name, ty in t._fields_:
+        v = getattr(t, name)
+        if isinstance(v, Strings):
+            blob = next(b for b in keep if isinstance(b, ctypes.Array) and ctypes.addressof(b) == v.bytes)
+            n_bytes = int(by_addr[ctypes.cast(v.off, ctypes.c_void_p).value][-1])
+            f.write(f"{prefix}{name}.n i64 1\n".encode() + np.int64(v.n).tobytes())
+            f.write(f"{prefix}{name}.bytes u8 {n_bytes}\n".encode() + bytes(blob)[:n_bytes])
+            off = by_addr[ctypes.cast(v.off, ctypes.c_void_p).value]
+            f.write(f"{prefix}{name}.off i64 {off.size}\n".encode() + off.tobytes())
+        elif ty is ctypes.c_int64:
+            f.write(f"{prefix}{name} i64 1\n".encode() + np.int64(v).tobytes())
+        elif isinstance(v, ctypes.Array):  # int64[2]
+            f.write(f"{prefix}{name} i64 {len(v)}\n".encode() + np.array(list(v), np.int64).tobytes())
+        else:
+            addr = ctypes.cast(v, ctypes.c_void_p).value
+            kind = kinds[ty._type_]
+            if addr is None:
+                f.write(f"{prefix}{name} {kind} -1\n".encode())
+                continue
+            a = by_addr[addr]
+            f.write(f"{prefix}{name} {kind} {a.size}\n".encode() + a.tobytes())
+
+
+def dump_tables(tables, path):
+    """ResourceTables / PolicyTables -> the field dump capi_driver --flat reads."""
+    with open(path, "wb") as f:
+        _dump_struct(tables.c, tables._keep, f)
+
+
+def dump_probe_configs(probes, path):
+    """generator.ProbeConfig values as capi_driver --flat lines: "all", "int PORT PROTO", "name NAME PROTO"."""
+    pc = ProbeConfigs(probes)
+    with open(path, "w") as f:
+        for i in range(pc.n):
+            c = pc.c[i]
+            proto = (c.protocol or b"").decode()
+            if c.all_available:
+                f.write("all\n")
+            elif c.port_is_name:
+                f.write(f"name {c.port_name.decode()} {proto}\n")
+            else:
+                f.write(f"int {c.port} {proto}\n")

@@ -12,6 +12,7 @@
 #   tl CFG [N]                 kernel timeline of back-to-back steps (scripts/graph_timeline.py)
 #   py SCRIPT [args]           any python script under scripts/ (180 s limit)
 #   ab CFG SPEC...             kernel stats per library variant (scripts/ab_kernels.sh; REPS env, CYC_SHARD tokens)
+#   pmc CFG [NAME=V ...]       per-kernel SQ instruction / wait mix, TCC hits, FETCH / WRITE passes (scripts/pmc_passes.sh)
 # Invocations are recorded in scripts/LEASES.md.
 set -e
 NAME=$1; shift
@@ -22,12 +23,13 @@ prof_env() { cd /tmp && export TMPDIR=/tmp && cd $ROOT; }
 for spec in "$@"; do
   set -- $spec
   step=$1; shift
-  # leading CYC_*=value tokens are environment for this step only (e.g. "ks config3 CYC_SHARD=0/8")
+  # CYC_*=value and REPS=n tokens are environment for this step only (e.g. "ks config3 CYC_SHARD=0/8")
   envs=(); args=()
-  for a in "$@"; do if [[ $a == CYC_*=* ]]; then envs+=("$a"); else args+=("$a"); fi; done
+  for a in "$@"; do if [[ $a == CYC_*=* || $a == REPS=* ]]; then envs+=("$a"); else args+=("$a"); fi; done
   set -- "${args[@]}"
   for e in "${envs[@]}"; do export "$e"; done
   tag=$(echo "$*" | tr ' =/' '___' | cut -c1-60)
+  [ -n "$CYC_HIP_LIB" ] && tag=${tag}_$(basename $(dirname $CYC_HIP_LIB))  # library variant runs apart
   echo "[lease] $(date +%T) $spec" >> $OUT/steps.log
   case $step in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $OUT/gpu_tests.log 2>&1 ;;
@@ -51,6 +53,7 @@ for spec in "$@"; do
       timeout -k 10 120 rocprofv3 --kernel-trace -d $OUT/tl_$tag -o run -- python3 scripts/graph_timeline.py run "$@" > $OUT/tl_$tag.log 2>&1 ;;
     py) timeout -k 10 180 python -u scripts/"$@" > $OUT/py_$tag.log 2>&1 ;;
     ab) timeout -k 10 900 bash scripts/ab_kernels.sh $NAME "$@" ;;
+    pmc) timeout -k 10 700 bash scripts/pmc_passes.sh $NAME "$@" ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
   for e in "${envs[@]}"; do unset "${e%%=*}"; done

@@ -127,3 +127,46 @@ def test_cpp_driver_compile_path(tmp_path):
     args = _driver_inputs(tmp_path, bad, c["resources"], c["probes"])
     r = subprocess.run([drv, *args, "--no-gpu"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 3 and r.stdout.startswith("error cyc_policy_build_json rc=3"), r.stdout
+
+
+def _flat_inputs(tmp_path, tag, pols, res, probes):
+    from cyclonus_amd import flat
+    from cyclonus_amd.engine import Engine
+
+    ir = Engine(0).build_policies(pols).policy_ir()
+    paths = [str(tmp_path / f"{tag}.{x}") for x in ("pol.tab", "res.tab", "probes.txt")]
+    flat.dump_tables(flat.PolicyTables(ir), paths[0])
+    flat.dump_tables(flat.ResourceTables(res), paths[1])
+    flat.dump_probe_configs(probes, paths[2])
+    return ir, paths
+
+
+def test_cpp_driver_flat_tables(tmp_path):
+    """The C++ client through the flat-table entry points (cyc_policy_load, cyc_resources_load — what a
+    cgo binding passes from its Go values): the loaded policy and probe model export the same
+    json.Marshal forms as the JSON path; a table with an out-of-range index is refused with the
+    reference-free CYC_ERR_ARG message, not a crash."""
+    import json
+    import subprocess
+
+    from cyclonus_amd import build, flat
+    from cyclonus_amd.engine import Engine
+    from tests.randgen import random_problem
+
+    drv = build.build_driver()
+    cases = [json.load(open(os.path.join(ROOT, "tests", "golden", "config1.json")))]
+    cases = [(c["policies"], c["resources"], c["probes"]) for c in cases] + [random_problem(s) for s in (11, 12, 13)]
+    for n, (pols, res, probes) in enumerate(cases):
+        ir, paths = _flat_inputs(tmp_path, str(n), pols, res, probes)
+        r = subprocess.run([drv, "--flat", *paths, "--no-gpu"], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        lines = dict(line.split(" ", 1) for line in r.stdout.splitlines())
+        assert json.loads(lines["ir"]) == ir, n
+        assert json.loads(lines["resources"]) == Engine(0).load_resources(res).resources_json(), n
+    # a pod whose namespace index is past the string table
+    rt = flat.ResourceTables(cases[0][1])
+    rt.c.pod_ns[0] = 99
+    flat.dump_tables(rt, paths[1])
+    r = subprocess.run([drv, "--flat", *paths, "--no-gpu"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3 and r.stdout.startswith("error cyc_resources_load rc=%d" % _lib.ERR_ARG), r.stdout
+    assert "pod_ns[0] = 99 out of range" in r.stdout, r.stdout

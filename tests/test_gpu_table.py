@@ -162,10 +162,11 @@ def test_table_panics_and_lifetime():
 
 def test_cpp_driver_tables(tmp_path):
     """The C++ C-ABI driver (tests/native/capi_driver.cpp) prints every cell's Connectivity through
-    cyc_table_run / cyc_table_cells: equal to the oracle's table on config1 and random problems."""
+    cyc_table_run / cyc_table_cells, from the JSON and from the flat-table entry points: equal to the
+    oracle's table on config1 and random problems."""
     import subprocess
 
-    from cyclonus_amd import build
+    from cyclonus_amd import build, flat
 
     drv = build.DRIVER
     assert os.path.exists(drv), "build the driver first (cyclonus_amd.build)"
@@ -183,15 +184,23 @@ def test_cpp_driver_tables(tmp_path):
             p = tmp_path / f"{name}{n}.json"
             p.write_text(json.dumps(doc))
             paths.append(str(p))
-        r = subprocess.run([drv, *paths], capture_output=True, text=True, timeout=100)
-        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        lines = r.stdout.splitlines()
-        P, K = (int(x) for x in lines[0].split()[1:])
-        w = want.cells(0, P, 0, P, 0, K)
-        for line in lines[1:]:
-            s, d, cells = line.split(" ")
-            s, d = int(s), int(d)
-            exp = "".join(short[int(w["ingress"][s, d, k])] + short[int(w["egress"][s, d, k])] + short[int(w["combined"][s, d, k])]
-                          for k in range(K))
-            assert cells == exp, (n, s, d, cells, exp)
-        assert len(lines) == 1 + P * P
+        # the JSON entry points, then the flat-table ones (cyc_policy_load of the built policy,
+        # cyc_resources_load, cyc_probe_prepare_configs: the cgo binding's no-JSON form)
+        ir = Engine(0).build_policies(pols).policy_ir()
+        fpaths = [str(tmp_path / f"{n}.{x}") for x in ("pol.tab", "res.tab", "probes.txt")]
+        flat.dump_tables(flat.PolicyTables(ir), fpaths[0])
+        flat.dump_tables(flat.ResourceTables(res), fpaths[1])
+        flat.dump_probe_configs(probes, fpaths[2])
+        for argv in ([drv, *paths], [drv, "--flat", *fpaths]):
+            r = subprocess.run(argv, capture_output=True, text=True, timeout=100)
+            assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+            lines = r.stdout.splitlines()
+            P, K = (int(x) for x in lines[0].split()[1:])
+            w = want.cells(0, P, 0, P, 0, K)
+            for line in lines[1:]:
+                s, d, cells = line.split(" ")
+                s, d = int(s), int(d)
+                exp = "".join(short[int(w["ingress"][s, d, k])] + short[int(w["egress"][s, d, k])] +
+                              short[int(w["combined"][s, d, k])] for k in range(K))
+                assert cells == exp, (n, argv[1], s, d, cells, exp)
+            assert len(lines) == 1 + P * P
