@@ -2211,29 +2211,28 @@ constexpr uint32_t IDO_IPL = 16;      // IP peers per representative staged in L
 // Grid rows of the IDO class rows per (slot chunk, representative group): 256-word chunks (staging
 // once for 2 / 4 / 7 chunks per block measured slower on config #3: profiles/r03_ido_rows_ab.txt).
 __host__ __device__ inline uint32_t ido_chunk_groups(uint32_t WA) { return (WA + 255) / 256; }
-// The PM words (and chunk marks) of staged IP peers x0 .. x0 + N - 1 of a representative for pod word w.
+// The PM words (and chunk marks) of the staged IP peers listed in the bit mask pend (up to N of them, taken off
+// pend) for pod word w.
 // Branch-free: every lane issues every load (a zero word where the peer is absent or w is outside its
 // span), so the batch's loads are in flight together — a load under a divergent branch is waited
 // for at the branch's end, which serialises a batch into one memory round trip per peer.
 template <uint32_t N>
-__device__ __forceinline__ void ido_ip_loads(const RowArgs& a, const uint4* sl, uint32_t x0, uint32_t ms, uint32_t w,
-                                             uint64_t (&pm)[N], uint32_t (&pbits)[N]) {
+__device__ __forceinline__ void ido_ip_loads_mask(const RowArgs& a, const uint4* sl, uint32_t& pend, uint32_t w,
+                                                  uint64_t (&pm)[N], uint32_t (&pbits)[N]) {
   const uint32_t cw = (a.W + 63) / 64;
   uint4 e[N];
   bool ok[N];
   bool any = false;
 #pragma unroll
   for (uint32_t u = 0; u < N; u++) {
-    e[u] = sl[min(x0 + u, IDO_IPL - 1)];
-    const bool in = x0 + u < ms;
+    const bool in = pend != 0;
+    e[u] = sl[in ? __builtin_ctz(pend) : 0u];
+    pend &= pend - 1;
     ok[u] = in && w >= e[u].y && w <= e[u].z;
     pbits[u] = in ? e[u].w : 0u;
     pm[u] = 0;
     any |= ok[u];
   }
-  // most (representative, 256-word chunk) pairs lie outside every staged peer's nonzero word span
-  // (a CIDR covers a few namespaces' pods): then the wave issues no load and waits for none
-  // (config #3 class rows -6 us: profiles/r03_bench_variance_ipskip.txt)
   if (!__ballot(any)) return;
   uint64_t v[N];
   uint32_t cm[N];
@@ -2339,12 +2338,19 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   // PM loads (no list -> port table chain per batch)
   uint4* s_il = reinterpret_cast<uint4*>(sB32 + ((nr * EW32 * NS + 3) & ~3u));  // 16-byte aligned
   const bool stage_ip = !EGRESS || a.portbits != nullptr;
+  // per representative: which staged peers have nonzero PM words inside the block's words (a CIDR
+  // covers a few namespaces' pods, so most (representative, 256-word chunk) pairs have none)
+  __shared__ uint32_t s_ipm[IDO_RPB_MAX];
   if (stage_ip) {
-    for (uint32_t t = threadIdx.x; t < nr * IDO_IPL; t += blockDim.x) {
-      const RepHead<KC>& h = s_rep[t / IDO_IPL];
+    const uint32_t wlo = a.w0 + (bid_ % cg) * 256, whi = min(wlo + 255, wend - 1);
+    static_assert(64 % IDO_IPL == 0, "a representative's staged peers lie in one wave");
+    for (uint32_t t = threadIdx.x; t < ((nr * IDO_IPL + 63) & ~63u); t += blockDim.x) {
+      const RepHead<KC>& h = s_rep[min(t / IDO_IPL, nr - 1)];
       const uint32_t x = t % IDO_IPL;
-      const bool ok = x < h.m;
+      const bool ok = t < nr * IDO_IPL && x < h.m;
       const uint4 jp = *(ok ? a.ip_list + h.ipoff + x : reinterpret_cast<const uint4*>(a.zero));
+      const uint64_t hit = __ballot(ok && jp.z <= whi && jp.w >= wlo);
+      if (x == 0 && t < nr * IDO_IPL) s_ipm[t / IDO_IPL] = uint32_t(hit >> (t & 63 & ~(IDO_IPL - 1))) & ((1u << IDO_IPL) - 1);
       uint32_t bits = 0;
       if (EGRESS) {
         bits = *(ok ? a.portbits + jp.y : reinterpret_cast<const uint32_t*>(a.zero));
@@ -2437,11 +2443,17 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     // the walk early, once per batch)
     const uint32_t m = h.m, ms = stage_ip ? min(m, IDO_IPL) : 0u;
     const uint4* sl = s_il + q * IDO_IPL;
-    uint64_t undecided = ms ? 0ull : ~0ull;
-    for (uint32_t x0 = 0; x0 < ms; x0 += PEER_BATCH) {
+    uint32_t pend = stage_ip ? s_ipm[q] : 0u;  // staged peers with PM words in the block's words
+    uint64_t undecided = ~0ull;  // (only ends the walk over unstaged peers early)
+    if (!pend && m > ms) {
+      undecided = 0;
+#pragma unroll
+      for (int kk = 0; kk < KC; kk++) undecided |= valid[kk] & ~allow[kk];
+    }
+    while (pend) {
       uint64_t pm[PEER_BATCH];
       uint32_t pbits[PEER_BATCH];
-      ido_ip_loads(a, sl, x0, ms, w, pm, pbits);
+      ido_ip_loads_mask(a, sl, pend, w, pm, pbits);
       undecided = 0;
 #pragma unroll
       for (int kk = 0; kk < KC; kk++) {
@@ -2961,12 +2973,13 @@ __global__ __launch_bounds__(BS) void k_emit_units(EmitArgs a) {
 }
 
 // Batched blocks (cyc_probe_prepare_blocks): block b's own table, bits relative to its first pod.
-// One workgroup per block sweeps its output words — ingress[d][k][j], egress[s][k][j] for its pods
+// `split` workgroups per block sweep its output words — ingress[d][k][j], egress[s][k][j] for its pods
 // and its probe config's slots — each the class row's words [j, j + 1] of the block's window
 // shifted down by the block's first pod's bit, masked to its pods; and its status rows.  The bytes
 // written are exactly the answered cells' bits plus their status.
 struct BlockArgs {
   uint32_t n_blk, K, AS;               // blocks, slots of the class rows, A row stride (words)
+  uint32_t split;                      // workgroups per block (sized on the host from the largest block)
   const uint4* blk;                     // per block: (first pod, pods, first slot, slots)
   const uint64_t* boff;                 // per block: plane slab offset (words), status offset (bytes)
   const uint32_t *pod_id[2], *class_of[2];
@@ -2976,14 +2989,15 @@ struct BlockArgs {
   uint8_t* st_out;
 };
 __global__ __launch_bounds__(256) void k_emit_blocks(BlockArgs a) {
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = blockIdx.x / a.split, g = blockIdx.x % a.split;  // block b's g-th workgroup
   if (b >= a.n_blk) return;
+  const uint32_t t0 = g * blockDim.x + threadIdx.x, stride = a.split * blockDim.x;
   const uint4 bl = a.blk[b];  // (p0, np, k0, nk)
   const uint32_t p0 = bl.x, np = bl.y, k0 = bl.z, nk = bl.w, wb = (np + 63) / 64, sh = p0 % 64;
   const uint32_t wa = (p0 + np + 63) / 64 - p0 / 64;  // the class rows' window words
   const uint64_t n = uint64_t(np) * nk * wb, off = a.boff[2 * b];
   const uint64_t tail = np % 64 ? (1ull << (np % 64)) - 1 : ~0ull;
-  for (uint64_t x = threadIdx.x; x < 2 * n; x += blockDim.x) {
+  for (uint64_t x = t0; x < 2 * n; x += stride) {
     const uint32_t pl = x >= n ? 1u : 0u;
     const uint64_t y = x - pl * n;
     const uint32_t j = uint32_t(y % wb), k = uint32_t((y / wb) % nk), q = uint32_t(y / (uint64_t(wb) * nk));
@@ -2995,7 +3009,7 @@ __global__ __launch_bounds__(256) void k_emit_blocks(BlockArgs a) {
     a.out[pl][off + y] = v;
   }
   const uint64_t soff = a.boff[2 * b + 1];
-  for (uint32_t x = threadIdx.x; x < np * nk; x += blockDim.x)
+  for (uint32_t x = t0; x < np * nk; x += stride)
     a.st_out[soff + x] = a.st_src[uint64_t(p0 + x / nk) * a.K + k0 + x % nk];
 }
 
@@ -3276,6 +3290,13 @@ struct HipErr {
 // Makes `device` current for the scope of an entry point and restores the caller's current device
 // afterwards: a binding calling in from a thread whose current device is another GPU (e.g. PyTorch
 // on cuda:1 with a context on device 0) keeps its own current device.
+// Events of a run (stream order, completion, phase timing) release to device scope: a default
+// (system-scope) event writes back and invalidates the caches when it is recorded, which left a
+// ~15 us idle gap after every step's emit (config #3 timeline, r04c) and inflated the phase timings.
+// Nothing here hands memory to the host through an event: host reads are hipMemcpy calls.
+constexpr unsigned EV_SYNC = hipEventDisableTiming | hipEventReleaseToDevice;
+constexpr unsigned EV_TIMING = hipEventReleaseToDevice;
+
 struct DeviceGuard {
   int prev = -1;
   bool set = false;
@@ -4567,7 +4588,12 @@ static bool enq_emit_blocks(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64
   ba.out[0] = out_in;
   ba.out[1] = out_eg;
   ba.st_out = d_status;
-  k_emit_blocks<<<ba.n_blk, c->blk_np_max * 2 > 128 ? 256 : 128, 0, st>>>(ba);
+  // a block's slab words split over workgroups of ~16 words per thread (one workgroup per block
+  // left a few large blocks on a few CUs); small blocks' extra workgroups exit at once
+  const unsigned bs = c->blk_np_max * 2 > 128 ? 256 : 128;
+  const uint64_t most = 2ull * c->blk_np_max * pb.K * ((c->blk_np_max + 63) / 64);  // largest slab, both planes
+  ba.split = uint32_t(std::min<uint64_t>(64, std::max<uint64_t>(1, most / (uint64_t(bs) * 16))));
+  k_emit_blocks<<<ba.n_blk * ba.split, bs, 0, st>>>(ba);
   return true;
 }
 
@@ -4963,10 +4989,10 @@ static void ensure_cap_streams(cyc_ctx* c) {
   HIPCHK(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&c->cap_stream2, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&c->cap_stream3, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&c->sel_ev, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&c->ports_ev, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&c->sel_ev, EV_SYNC));
+  HIPCHK(hipEventCreateWithFlags(&c->ports_ev, EV_SYNC));
+  HIPCHK(hipEventCreateWithFlags(&c->fork_ev, EV_SYNC));
+  HIPCHK(hipEventCreateWithFlags(&c->join_ev, EV_SYNC));
 }
 
 // Batched blocks: each block's status, as its stand-alone run would end — the job expansion's
@@ -5075,7 +5101,7 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
       HIPCHK(hipStreamEndCapture(c->cap_stream, &g));
       c->graph = g;  // destroyed with the exec (drop_graph / reap_graphs)
       HIPCHK(hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
-      HIPCHK(hipEventCreateWithFlags(&c->graph_done, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&c->graph_done, EV_SYNC));
       memcpy(c->graph_key, key, sizeof(key));
     }
     if (c->step_events) HIPCHK(hipEventRecord(c->ev[0], st));
@@ -5368,8 +5394,8 @@ static int probe_prepare(cyc_ctx* c, const std::function<std::vector<ProbeConfig
     DeviceGuard dg(c->device);
     if (!c->stream) {
       HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-      for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
-      HIPCHK(hipEventCreateWithFlags(&c->run_done, hipEventDisableTiming));
+      for (auto& e : c->ev) HIPCHK(hipEventCreateWithFlags(&e, EV_TIMING));
+      HIPCHK(hipEventCreateWithFlags(&c->run_done, EV_SYNC));
     }
     const std::vector<ProbeConfig> probes = probes_of();
     c->prepared = false;
