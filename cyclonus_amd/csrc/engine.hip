@@ -737,7 +737,10 @@ __device__ __forceinline__ uint64_t affine_lanes6(const DWordIP& wd, const DCidr
 #ifndef CYC_IP_AFFINE
 #define CYC_IP_AFFINE 1  // 0: every straddling word tested a pod per lane (the affine-address lane ranges off)
 #endif
-constexpr uint32_t IP_MIXB = 1;  // straddling words of an IP row whose pod addresses are loaded at once (2: config #4 launch B +4 us)
+#ifndef CYC_IP_MIXB
+#define CYC_IP_MIXB 1
+#endif
+constexpr uint32_t IP_MIXB = CYC_IP_MIXB;  // straddling words of an IP row whose pod addresses are loaded at once (2: config #4 launch B +4 us)
 __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
                                             const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
                                             uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng,
@@ -2845,10 +2848,11 @@ __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
 // Short rows (< 16 KB, auto): one block per a.chunk consecutive rows of an XCD's segment, the
 // threads sweeping the rows' 16-byte chunks as one flat range (row = index / chunks per row), so
 // rows shorter than a block's pass still keep every lane storing.  The rows' source and
-// destination addresses are staged in LDS first.
+// destination addresses are staged in LDS first.  (1024-thread blocks over ~128 KB each: config #2
+// emit 21.8 -> 25.0 us, profiles/r04_emit_flat_ab.txt.)
 constexpr uint32_t EMIT_FLAT_MAX_ROWS = 256;
-template <int UNROLL>
-__global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
+template <int BS, int UNROLL>
+__global__ __launch_bounds__(BS) void k_emit_flat(EmitArgs a) {
   emit_status(a);
   __shared__ const u64x2* s_src[EMIT_FLAT_MAX_ROWS];
   __shared__ u64x2* s_dst[EMIT_FLAT_MAX_ROWS];
@@ -2856,7 +2860,7 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   const uint32_t r0 = x * a.per_xcd + (b >> 3) * a.chunk;
   const uint32_t r_end = min(n, (x + 1) * a.per_xcd);
   if (r0 >= r_end) return;
-  __shared__ uint32_t s_cnt[4];
+  __shared__ uint32_t s_cnt[BS / 64];
   uint32_t nr = min(a.chunk, r_end - r0);
   // the block's rows that need a copy (in-place class rows are skipped), compacted in row order
   const u64x2* src = nullptr;
@@ -2873,26 +2877,28 @@ __global__ __launch_bounds__(256) void k_emit_flat(EmitArgs a) {
   __syncthreads();
   uint32_t off = __popcll(keep & ((1ull << lane) - 1));
   for (uint32_t x = 0; x < wv; x++) off += s_cnt[x];
-  nr = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  nr = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < BS / 64; x++) nr += s_cnt[x];
   if (src) {
     s_src[off] = src;
     s_dst[off] = dst;
   }
   __syncthreads();
   const uint32_t n2 = uint32_t(a.row_words / 2), tot = nr * n2;
-  for (uint32_t i0 = threadIdx.x; i0 < tot; i0 += 256 * UNROLL) {
+  for (uint32_t i0 = threadIdx.x; i0 < tot; i0 += BS * UNROLL) {
     u64x2 v[UNROLL];
     uint32_t row[UNROLL], col[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
-      const uint32_t i = i0 + u * 256;
+      const uint32_t i = i0 + u * BS;
       row[u] = i / n2;
       col[u] = i - row[u] * n2;
       if (i < tot) v[u] = s_src[row[u]][col[u]];
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++)
-      if (i0 + u * 256 < tot) emit_store(v[u], &s_dst[row[u]][col[u]]);
+      if (i0 + u * BS < tot) emit_store(v[u], &s_dst[row[u]][col[u]]);
   }
 }
 
@@ -3422,8 +3428,8 @@ struct cyc_ctx {
                         // -1 = auto by identity count
   int pod_words = -1;   // "pod_words": pod-peer words in the class rows from identity sets (1, IDO),
                         // from materialised PM rows (0), or IDO when every word has <= IDO_MAX_RUNS runs
-  int64_t class_rpb_opt = 4;  // "class_rpb": IDO class-row representatives per block
-                              // (config3 N=1 -1%: profiles/r01_class_rpb_ab.txt)
+  int64_t class_rpb_opt = 0;  // "class_rpb": IDO class-row representatives per block; 0 = auto
+                              // (profiles/r04_class_rpb_ab.txt)
   int step_events = 0;  // "step_events": graph / eager-DAG runs record the whole-step timing events (1);
                         // off by default: the two timing events cost ~9 us of idle GPU per step
                         // (config #2 0.077 -> 0.069 ms/step, profiles/r02_step_events_ab.txt)
@@ -4410,11 +4416,12 @@ static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
 }
 
 // 6. class rows of direction d
-// IDO class rows: representatives per block (cyc_set_option "class_rpb"), as many as fit the
-// staged identity-set budget
-static uint32_t class_rpb(const cyc_ctx* c, size_t per_rep_lds) {
+// IDO class rows: representatives per block (cyc_set_option "class_rpb"; 0 = auto: 4, or more in
+// the fused front, enq_front_fused), as many as fit the staged identity-set budget
+static uint32_t class_rpb(const cyc_ctx* c, size_t per_rep_lds, uint32_t want = 0) {
   const uint64_t fit = std::max<uint64_t>(1, IDO_LDS_BYTES / std::max<size_t>(per_rep_lds, 1));
-  return uint32_t(std::max<int64_t>(1, std::min<int64_t>(c->class_rpb_opt, int64_t(fit))));
+  const int64_t w = want ? int64_t(want) : c->class_rpb_opt ? c->class_rpb_opt : 4;
+  return uint32_t(std::max<int64_t>(1, std::min<int64_t>(w, int64_t(fit))));
 }
 
 static RowArgs row_args(cyc_ctx* c, int d) {
@@ -4565,7 +4572,7 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     else k_emit_wide<256, 8><<<g, 256, 0, st>>>(ea);
   } else {  // flat multi-row sweep over ~32 KB per block
     ea.chunk = uint32_t(std::min<uint64_t>(EMIT_FLAT_MAX_ROWS, std::max<uint64_t>(1, 32768 / row_bytes)));
-    k_emit_flat<8><<<(ea.per_xcd + ea.chunk - 1) / ea.chunk * 8, 256, 0, st>>>(ea);
+    k_emit_flat<256, 8><<<(ea.per_xcd + ea.chunk - 1) / ea.chunk * 8, 256, 0, st>>>(ea);
   }
 }
 
@@ -4813,7 +4820,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     }
   }
   FrontRows fd{}, fe{};
-  size_t lds = 0, lds_uni = 0;
+  size_t lds = 0, lds_uni = 0, e_per[2] = {0, 0};
+  uint32_t e_na[2] = {0, 0};
   for (int d = 0; d < 2; d++) {
     const uint32_t na = c->dir[d].n ? c->n_act[d] : 0u;
     fb.ma[d] = member_args(c, d);
@@ -4842,12 +4850,36 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fd.nb[d] = blocks((uint64_t(na) * ((fd.ra[d].NB + CI_G - 1) / CI_G) + 3) / 4);
     // egress with one descriptor per slot (udesc): only the block's slots' sets are staged
     if (d == 1 && c->uni_desc) fe.ra[d].udesc = c->udesc.as<int32_t>();
-    const size_t per = size_t(d == 0 || fe.ra[d].udesc ? uint32_t(E_KC) : D) * fd.ra[d].EW * 8 +
-                       IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
-    fe.ra[d].rpb = class_rpb(c, per);
-    fe.nb[d] = blocks(uint64_t(ido_chunk_groups(fe.ra[d].WA)) * ((K + E_KC - 1) / E_KC) * ((na + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
-    if (d == 1 && fe.ra[d].udesc) lds_uni = per * fe.ra[d].rpb;
-    else lds = std::max<size_t>(lds, per * fe.ra[d].rpb);
+    e_per[d] = size_t(d == 0 || fe.ra[d].udesc ? uint32_t(E_KC) : D) * fd.ra[d].EW * 8 +
+               IDO_IPL * sizeof(uint4) + 16;  // identity sets + staged IP peers (+ alignment)
+    e_na[d] = na;
+  }
+  // launch E's representatives per block: the most of 16 / 8 that still leaves >= 3000 blocks
+  // (about two rounds of the chip's resident blocks: one block's staging latency is paid once per
+  // 16 representatives), else 4 (config #3: E 106 -> 96 us at N = 1 with 16; at N = 8 a source
+  // shard's ~1,900 blocks of 4 ran 22.8 us, of 8 24.0 — profiles/r04_class_rpb_ab.txt)
+  auto e_blocks = [&](int d, uint32_t rpb) {
+    return uint64_t(ido_chunk_groups(fe.ra[d].WA)) * ((K + E_KC - 1) / E_KC) * ((e_na[d] + rpb - 1) / rpb);
+  };
+  uint32_t e_want = uint32_t(c->class_rpb_opt);
+  if (!e_want) {
+    e_want = 4;
+    for (uint32_t cand : {16u, 8u}) {
+      uint64_t tot = 0;
+      for (int d = 0; d < 2; d++)
+        if (e_per[d]) tot += e_blocks(d, class_rpb(c, e_per[d], cand));
+      if (tot >= 3000) {
+        e_want = cand;
+        break;
+      }
+    }
+  }
+  for (int d = 0; d < 2; d++) {
+    if (!e_per[d]) continue;
+    fe.ra[d].rpb = class_rpb(c, e_per[d], e_want);
+    fe.nb[d] = blocks(e_blocks(d, fe.ra[d].rpb));
+    if (d == 1 && fe.ra[d].udesc) lds_uni = e_per[d] * fe.ra[d].rpb;
+    else lds = std::max<size_t>(lds, e_per[d] * fe.ra[d].rpb);
   }
   const bool bits = fa.nb[1] && port_bits_on(c);
   const uint32_t nb_bits = bits ? blocks((uint64_t(M) + 255) / 256) : 0u;
@@ -5772,7 +5804,7 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "pod_words") range(-1, 1), c->pod_words = int(value);
     else if (n == "pod_rows") range(-1, 1), c->pod_rows = int(value);
     else if (n == "member_wave") range(-1, 1), c->member_wave = int(value);
-    else if (n == "class_rpb") range(1, 64), c->class_rpb_opt = value;
+    else if (n == "class_rpb") range(0, 64), c->class_rpb_opt = value;
     else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
     else if (n == "sel_lazy") range(-1, 1), c->sel_lazy = int(value);
     else if (n == "pr_group") range(-1, 64), c->pr_group = int(value == 0 ? -1 : value);

@@ -456,7 +456,7 @@ def test_pod_words_from_identity_runs(gpu, seed):
     # or thread, several class representatives per class-row block, and the PM path
     for mode, graphs, fused, mw, rpb in ((1, 1, 1, -1, 1), (1, 1, 1, 1, 3), (1, 1, 1, 0, 4), (1, 1, 0, -1, 2),
                                          (1, 2, 1, 0, 1), (1, 2, 0, 1, 5), (1, 0, 1, -1, 2), (1, 0, 0, -1, 3),
-                                         (1, -1, 1, -1, 4), (0, 1, 1, -1, 1), (0, 0, 1, -1, 1), (0, 2, 0, 1, 1)):
+                                         (1, -1, 1, -1, 16), (1, 2, 1, -1, 0), (0, 1, 1, -1, 1), (0, 0, 1, -1, 1), (0, 2, 0, 1, 1)):
         eng.set_option("pod_words", mode)
         eng.set_option("graphs", graphs)
         eng.set_option("front_fused", fused)
@@ -662,7 +662,7 @@ def test_launch_modes_and_knobs(gpu):
     fused = not eng.shape["may_panic"]  # no-panic build: the fused front applies
     assert eng.get_option("front_fused_active") == int(fused)
     assert eng.get_option("launch") == (2 if fused else 1)
-    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("graphs", 1), ("graphs", -1),
+    for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("class_rpb", 16), ("class_rpb", 0), ("graphs", 1), ("graphs", -1),
                     ("step_events", 1), ("step_events", 0), ("pr_group", 5), ("pr_group", -1), ("sel_lazy", 1),
                     ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1)):
         eng.set_option(name, v)
@@ -684,7 +684,7 @@ def test_launch_modes_and_knobs(gpu):
     assert_same(want, eng.run_host(), "DAG graph")
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
-    for name, v in (("class_rpb", 0), ("class_rpb", 65), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
+    for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
