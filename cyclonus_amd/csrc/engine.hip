@@ -31,6 +31,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -734,13 +735,7 @@ __device__ __forceinline__ uint64_t affine_lanes6(const DWordIP& wd, const DCidr
                         lt128(hi, wd.min6), !lt128(hi, wd.max6));
 }
 
-#ifndef CYC_IP_AFFINE
-#define CYC_IP_AFFINE 1  // 0: every straddling word tested a pod per lane (the affine-address lane ranges off)
-#endif
-#ifndef CYC_IP_MIXB
-#define CYC_IP_MIXB 1
-#endif
-constexpr uint32_t IP_MIXB = CYC_IP_MIXB;  // straddling words of an IP row whose pod addresses are loaded at once (2: config #4 launch B +4 us)
+constexpr uint32_t IP_MIXB = 1;  // straddling words of an IP row whose pod addresses are loaded at once (2: config #4 launch B +4 us)
 __device__ __forceinline__ void ip_row_word(const DIPTest& t, const DCidr* ex, const DIP* __restrict__ pod_ip,
                                             const DWordIP& wd, bool valid, uint32_t w, uint32_t chunk, uint32_t P, uint32_t W,
                                             uint32_t lane, uint64_t* __restrict__ PM, uint32_t* __restrict__ rng,
@@ -851,19 +846,102 @@ __device__ __forceinline__ uint64_t cnz_mask(const uint32_t* __restrict__ cnz, u
   return cnz[uint64_t(j) * ((W + 63) / 64) + w / 64] ? ~0ull : 0ull;
 }
 
+// IP rows by address ranges (no-panic runs): an IPBlock that matches few pods
+// is built from the host's address index instead of a test per word — the pods of each family
+// sorted by address, so the CIDR less its same-family excepts (ipaddress.go:22-40: in the network,
+// in none of the excepts) is a few intervals of sorted positions, found by binary search once per
+// problem.  A wave per IPBlock sets its pods' bits in an LDS copy of the row window (64-bit LDS
+// ORs), then stores the chunks holding a bit, chunk-dense like k_ip_rows_fast, with the row's word
+// span and chunk masks.  Cost ~ matching pods + window words, with no per-pod address loads or
+// straddling-word round trips (config #2's pod addresses step by 256 within a namespace, so every
+// word a /16 touches straddled it).
+struct DIPRange {
+  uint32_t peer, ivoff, ivcnt;  // intervals iv[ivoff .. ivoff + ivcnt) of sorted positions
+  uint32_t sw0;                 // first word of the matching pods' span (< IPR_SPAN words long)
+};
+constexpr uint32_t IPR_MAX_MATCH = 4096;  // pods an IPBlock may match to be built from ranges
+constexpr uint32_t IPR_SPAN = 256;        // words of a range row's LDS window (the matching pods' span)
+constexpr uint32_t IP_GROUP_MAX = 64, IP_EX_LDS = 256;
+// LDS of the two IP-row bodies, one allocation in a kernel that holds both (k_front_b): the fast
+// rows' staged tests and excepts, or the range rows' per-wave row windows
+union IpRowsLds {
+  struct {
+    DIPTest t[IP_GROUP_MAX];
+    DCidr ex[IP_EX_LDS];
+  } fast;
+  unsigned long long row[4][IPR_SPAN];
+};
+__shared__ IpRowsLds ip_lds;
+__device__ __forceinline__ void ip_rows_range_blk(uint32_t Rr, uint32_t W, const DIPRange* __restrict__ rt,
+                                                  const uint2* __restrict__ iv, const uint32_t* __restrict__ sorted,
+                                                  uint64_t* __restrict__ PM, uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz,
+                                                  uint32_t bid_, uint32_t c0, uint32_t nch) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t r = __builtin_amdgcn_readfirstlane(bid_ * 4 + wv);  // wave-uniform
+  unsigned long long* row = ip_lds.row[wv];
+  const bool live = r < Rr;
+  for (uint32_t x = lane; x < IPR_SPAN; x += 64) row[x] = 0;
+  DIPRange t{};
+  if (live) t = rt[r];
+  // the LDS window: the span's words inside the run's word window (a source shard's ingress peers)
+  const uint32_t lo_w = max(t.sw0, c0 * 64), hi_w = min(min(t.sw0 + IPR_SPAN, (c0 + nch) * 64), W);
+  __syncthreads();
+  for (uint32_t i = 0; live && i < t.ivcnt; i++) {
+    const uint2 v = iv[t.ivoff + i];
+    for (uint32_t p0 = v.x; p0 < v.y; p0 += 4 * 64) {  // 4 pods a lane in flight
+      uint32_t q[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) q[u] = sorted[min(p0 + u * 64 + lane, v.y - 1)];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t w = q[u] >> 6;
+        if (p0 + u * 64 + lane < v.y && w >= lo_w && w < hi_w) atomicOr(&row[w - t.sw0], 1ull << (q[u] & 63));
+      }
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  const uint32_t j = t.peer, cw = (W + 63) / 64;
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  uint64_t chunks = 0;
+  for (uint32_t c = c0; c < c0 + nch; c++) {
+    const uint32_t w = c * 64 + lane;
+    const bool in = c * 64 + 63 >= lo_w && c * 64 < hi_w;  // wave-uniform: the chunk meets the window
+    const uint64_t v = in && w >= lo_w && w < hi_w ? row[w - t.sw0] : 0ull;
+    const uint64_t nz = __ballot(v != 0);
+    if (nz && w < W) PM[uint64_t(j) * W + w] = v;  // chunk-dense: every word of a chunk with a bit
+    if (lane == 0) cnz[uint64_t(j) * cw + c] = nz ? 1u : 0u;
+    if (nz) {
+      lo = min(lo, c * 64 + uint32_t(__ffsll((unsigned long long)nz) - 1));
+      hi = max(hi, c * 64 + 63 - uint32_t(__clzll((long long)nz)));
+      if (c < 64) chunks |= 1ull << c;
+    }
+  }
+  if (lane == 0) {  // the row's only writer: its span and nonzero-chunk mask (as k_ip_rows_fast's atomics leave them)
+    rng[4 * j] = lo;
+    rng[4 * j + 1] = lo == 0xFFFFFFFFu ? 0xFFFFFFFFu : ~hi;
+    reinterpret_cast<unsigned long long*>(rng)[2 * j + 1] = ~chunks;
+  }
+}
+__global__ __launch_bounds__(256) void k_ip_rows_range(uint32_t Rr, uint32_t W, const DIPRange* __restrict__ rt, const uint2* __restrict__ iv,
+                                                       const uint32_t* __restrict__ sorted, uint64_t* __restrict__ PM,
+                                                       uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t c0, uint32_t nch) {
+  ip_rows_range_blk(Rr, W, rt, iv, sorted, PM, rng, cnz, blockIdx.x, c0, nch);
+}
+
 // A block handles one group of `grp` IP peers over 4 chunks of 64 words (a wave per chunk, lane =
 // word): the group's tests and their except records are staged into LDS once (one coalesced load
 // per block, instead of a chain of dependent scalar loads per peer and except), and each wave loads
 // its words' [min, max] records once for the whole group.
-constexpr uint32_t IP_GROUP = 16, IP_GROUP_MAX = 64, IP_EX_LDS = 256;  // IP peers per block (profiles/r02_ip_group_ab.txt)
+constexpr uint32_t IP_GROUP = 16;  // IP peers per block (profiles/r02_ip_group_ab.txt)
 // Chunks [c0, c0 + nch) of the rows (a source shard's ingress peers: the chunks of its word window).
 __device__ __forceinline__ void ip_rows_fast_blk(uint32_t Ri, uint32_t P, uint32_t W, const DIPTest* __restrict__ tests,
                                                       const DCidr* __restrict__ ip_ex, const DIP* __restrict__ pod_ip,
                                                       const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
                                                       uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t bid_, uint32_t nblk_,
                                                       uint32_t grp, uint32_t c0, uint32_t nch) {
-  __shared__ DIPTest s_t[IP_GROUP_MAX];
-  __shared__ DCidr s_ex[IP_EX_LDS];
+  DIPTest* const s_t = ip_lds.fast.t;
+  DCidr* const s_ex = ip_lds.fast.ex;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t cb = (nch + 3) / 4;
   const uint32_t r0 = (bid_ / cb) * grp;
@@ -2571,8 +2649,13 @@ __global__ __launch_bounds__(256) void k_front_a(FrontA f) {
 // rows and of the per-pod pod-peer rows is one direction's sub-list (target-row runs put both
 // directions into segment 0: one window).
 struct FrontB {
-  uint32_t nb[9];       // IP rows x2 | pod-peer rows x2 (or identity sets, segment 2) | membership in | eg | port bits |
-                        // port table | slot words (the last two: runs without launch A, enq_front_fused)
+  uint32_t nb[11];      // IP rows x2 | pod-peer rows x2 (or identity sets, segment 2) | membership in | eg | port bits |
+                        // port table | slot words (the last two: runs without launch A, enq_front_fused) |
+                        // IP rows from address ranges x2
+  uint32_t Rr[2];       // range-built IP rows per segment (ip_rows_range_blk)
+  const DIPRange* rtests[2];
+  const uint2* ipr_iv;
+  const uint32_t* ipsort;
   FrontA pre;           // launch A's port table and slot-word arguments
   uint32_t bits_direct; // port bits from the matchers (pre.pms ...), not from the byte table
   uint32_t ip_grp;      // IP rows: peers per wave
@@ -2643,8 +2726,15 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   if (b < f.nb[7]) return portok_blk(f.pre.M, f.pre.D, f.pre.pms, f.pre.pents, f.pre.descs, f.pre.portok, b, f.nb[7]);
   b -= f.nb[7];
   if (b < f.nb[8])
-    slot_words_blk(f.pre.P, f.pre.K, f.pre.W, f.pre.D, f.pre.slot_desc, f.pre.slot_status, f.pre.VALID, f.pre.DESCW, f.pre.DM, b,
-                   f.nb[8]);
+    return slot_words_blk(f.pre.P, f.pre.K, f.pre.W, f.pre.D, f.pre.slot_desc, f.pre.slot_status, f.pre.VALID, f.pre.DESCW,
+                          f.pre.DM, b, f.nb[8]);
+  b -= f.nb[8];
+#pragma unroll
+  for (int x = 0; x < 2; x++) {
+    if (b < f.nb[9 + x])
+      return ip_rows_range_blk(f.Rr[x], f.W, f.rtests[x], f.ipr_iv, f.ipsort, f.PM, f.rng, f.cnz, b, f.ic0[x], f.inch[x]);
+    b -= f.nb[9 + x];
+  }
 }
 
 // Pod-peer rows from posting lists: a pod selector that is ONE requirement `k = v` or `k in (v0,
@@ -3410,6 +3500,13 @@ struct cyc_ctx {
   bool dense_sel = false;  // k_selectors_dense (LVT fits)
   uint32_t Rp = 0, Ri = 0;
   uint32_t rp_off[3] = {0, 0, 0}, ri_off[3] = {0, 0, 0};  // per-direction sub-lists (ingress, egress)
+  // IP rows built from address ranges (ip_rows_range_blk): the pods of each family sorted by
+  // address (host keys for the binary searches; the pod order on the device), and per direction the
+  // range-built rows
+  std::vector<uint32_t> ip4_key, ipsort_host;
+  std::vector<std::array<uint32_t, 4>> ip6_key;
+  DevBuf ipsort, ipr_tests, ipr_iv;
+  uint32_t rr_off[3] = {0, 0, 0}, Rr = 0;
   uint32_t rpu_off[3] = {0, 0, 0};  // sub-lists of pod_peers_u: one pod peer per distinct matcher
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
   DevBuf act[2], sel_list;
@@ -3422,6 +3519,7 @@ struct cyc_ctx {
                         // events, -1 = auto: 2 when the fused front applies (its launches on one
                         // stream start ~8 us sooner after the previous step's emit than a graph
                         // replay: profiles/r01_front_fused_ab.txt), else 1
+  int ip_range = -1;    // "ip_range": IP rows of few, close pods from the address index (-1 auto, 0 never)
   int pod_rows = -1;    // "pod_rows": pod-peer PM rows per pod directly (1), through identity outcomes
                         // and word runs (0), or -1 = direct when identities >= pods / 2
   int member_wave = -1; // "member_wave": membership with a wave (1) or a thread (0) per identity,
@@ -3697,6 +3795,21 @@ static void prepare_device(cyc_ctx* c) {
   upload(c->pod_ls, pb.pod_ls);
   upload(c->pod_nsls, pb.pod_nsls);
   upload(c->pod_ip, pb.pod_ip);
+  {  // the address index of the range-built IP rows: IPv4 pods by address, then IPv6 pods
+    std::vector<uint32_t> p4, p6;
+    for (uint32_t q = 0; q < pb.P; q++)
+      if (pb.pod_ip[q].valid) (pb.pod_ip[q].fam == 4 ? p4 : p6).push_back(q);
+    std::stable_sort(p4.begin(), p4.end(), [&](uint32_t x, uint32_t y) { return pb.pod_ip[x].w[3] < pb.pod_ip[y].w[3]; });
+    auto a6 = [&](uint32_t q) { return std::array<uint32_t, 4>{pb.pod_ip[q].w[0], pb.pod_ip[q].w[1], pb.pod_ip[q].w[2], pb.pod_ip[q].w[3]}; };
+    std::stable_sort(p6.begin(), p6.end(), [&](uint32_t x, uint32_t y) { return a6(x) < a6(y); });
+    c->ip4_key.resize(p4.size());
+    c->ip6_key.resize(p6.size());
+    for (size_t x = 0; x < p4.size(); x++) c->ip4_key[x] = pb.pod_ip[p4[x]].w[3];
+    for (size_t x = 0; x < p6.size(); x++) c->ip6_key[x] = a6(p6[x]);
+    c->ipsort_host = p4;
+    c->ipsort_host.insert(c->ipsort_host.end(), p6.begin(), p6.end());
+    upload(c->ipsort, c->ipsort_host);
+  }
   upload(c->cidrs, pb.cidrs);
   upload(c->ipbs, pb.ipbs);
   upload(c->ipb_ex, pb.ipb_ex);
@@ -3861,7 +3974,7 @@ static void prepare_device(cyc_ctx* c) {
           }
         }
         for (int f = 0; f < 2; f++)
-          if (first[f] >= 0 && aff[f] && CYC_IP_AFFINE) d.aff |= (uint32_t(first[f]) | 0x80u) << (8 * f);
+          if (first[f] >= 0 && aff[f]) d.aff |= (uint32_t(first[f]) | 0x80u) << (8 * f);
         wi[w] = d;
       }
       for (uint32_t ch = 0; ch < NC; ch++) {
@@ -4199,9 +4312,64 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   // peer to its row; only the first of each IPBlock gets an IP-row test.
   std::vector<uint32_t> prow(std::max<size_t>(pb.peers.size(), 1));
   for (uint32_t j = 0; j < prow.size(); j++) prow[j] = j;
+  std::vector<DIPRange> rtests;
+  std::vector<uint2> riv;
+  // an IPBlock's matching pods as intervals of the address index (its family's block, less each
+  // same-family except), their count and word span: built from ranges when few and close
+  // (no-panic runs only: the ordered walk with panic bits keeps its dense rows)
+  const uint32_t n4 = uint32_t(c->ip4_key.size());
+  auto range_rows = [&](const DIPTest& t, DIPRange& out) -> bool {
+    if (pb.may_err || !t.cidr.valid || c->ip_range == 0) return false;
+    auto bounds = [&](const DCidr& cd, uint32_t& a, uint32_t& b) {
+      if (cd.fam == 4) {
+        const uint32_t lo = cd.net[3] & cd.mask[3], hi = lo | ~cd.mask[3];
+        a = uint32_t(std::lower_bound(c->ip4_key.begin(), c->ip4_key.end(), lo) - c->ip4_key.begin());
+        b = uint32_t(std::upper_bound(c->ip4_key.begin(), c->ip4_key.end(), hi) - c->ip4_key.begin());
+      } else {
+        std::array<uint32_t, 4> lo, hi;
+        for (int i = 0; i < 4; i++) {
+          lo[i] = cd.net[i] & cd.mask[i];
+          hi[i] = lo[i] | ~cd.mask[i];
+        }
+        a = n4 + uint32_t(std::lower_bound(c->ip6_key.begin(), c->ip6_key.end(), lo) - c->ip6_key.begin());
+        b = n4 + uint32_t(std::upper_bound(c->ip6_key.begin(), c->ip6_key.end(), hi) - c->ip6_key.begin());
+      }
+    };
+    std::vector<uint2> iv(1);
+    bounds(t.cidr, iv[0].x, iv[0].y);
+    for (uint32_t e = 0; e < t.excnt; e++) {
+      const DCidr& x = c->plan.ip_ex[t.exoff + e];
+      if (!x.valid) return false;
+      if (x.fam != t.cidr.fam) continue;  // an except of the other family never contains a pod of this one
+      uint32_t ea, eb;
+      bounds(x, ea, eb);
+      std::vector<uint2> next;
+      for (const uint2& v : iv) {
+        if (ea > v.x) next.push_back(make_uint2(v.x, std::min(v.y, ea)));
+        if (eb < v.y) next.push_back(make_uint2(std::max(v.x, eb), v.y));
+      }
+      iv.clear();
+      for (const uint2& v : next)
+        if (v.y > v.x) iv.push_back(v);
+    }
+    uint64_t n = 0;
+    for (const uint2& v : iv) n += v.y - v.x;
+    if (n > IPR_MAX_MATCH) return false;
+    uint32_t wlo = 0xFFFFFFFFu, whi = 0;
+    for (const uint2& v : iv)
+      for (uint32_t x = v.x; x < v.y; x++) {
+        wlo = std::min(wlo, c->ipsort_host[x] / 64);
+        whi = std::max(whi, c->ipsort_host[x] / 64);
+      }
+    if (n && whi - wlo >= IPR_SPAN) return false;
+    out = DIPRange{t.peer, uint32_t(riv.size()), uint32_t(iv.size()), n ? wlo : 0u};
+    riv.insert(riv.end(), iv.begin(), iv.end());
+    return true;
+  };
   for (int d = 0; d < 2; d++) {  // ingress peers first, then egress: one sub-list per branch
     c->rp_off[d] = uint32_t(pp.size());
     c->ri_off[d] = uint32_t(ip.size());
+    c->rr_off[d] = uint32_t(rtests.size());
     for (uint32_t j : c->plan.pod_peers)
       if (peer_needed[j] && peer_dir[j] == d) pp.push_back(j);
     std::map<std::vector<uint32_t>, uint32_t> ipb_row;
@@ -4217,10 +4385,19 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
         prow[j] = it.first->second;
         continue;
       }
+      DIPRange rt{};
+      if (range_rows(c->plan.ip_tests[r], rt)) {
+        rtests.push_back(rt);
+        continue;
+      }
       ip.push_back(j);
       tests.push_back(c->plan.ip_tests[r]);
     }
   }
+  c->rr_off[2] = uint32_t(rtests.size());
+  c->Rr = uint32_t(rtests.size());
+  upload(c->ipr_tests, rtests);
+  upload(c->ipr_iv, riv);
   upload(c->peer_row, prow);
   c->prow_host = prow;
   c->rp_off[2] = uint32_t(pp.size());
@@ -4282,7 +4459,7 @@ static void enq_common(cyc_ctx* c, hipStream_t st, int parts = COMMON_ALL) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size());
-  if ((parts & COMMON_FILL) && !pb.may_err && c->Ri)  // IP-peer word spans (k_ip_rows_fast)
+  if ((parts & COMMON_FILL) && !pb.may_err && (c->Ri || c->Rr))  // IP-peer word spans (k_ip_rows_fast)
     k_fill_u32<<<grid1(c->pb.peers.size() * 4, 256), 256, 0, st>>>(c->ip_rng.as<uint32_t>(), c->pb.peers.size() * 4, 0xFFFFFFFFu);
   if (!(parts & COMMON_SELECTORS)) goto ports;
   // 1. selectors x label sets
@@ -4369,6 +4546,10 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
       k_pod_rows<false><<<g, 256, 0, st>>>(Rp, E, W, plist, ido, c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(),
                                            c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
   }
+  const uint32_t q0 = c->rr_off[dlo], Rr = (which & PEERS_IP) ? c->rr_off[dhi] - q0 : 0u;
+  if (Rr && nw)
+    k_ip_rows_range<<<(Rr + 3) / 4, 256, 0, st>>>(Rr, W, c->ipr_tests.as<DIPRange>() + q0, c->ipr_iv.as<uint2>(),
+                                                c->ipsort.as<uint32_t>(), c->PM.as<uint64_t>(), c->ip_rng.as<uint32_t>(), ip_cnz(c), c0, nch);
   const uint32_t i0 = c->ri_off[dlo], Ri = (which & PEERS_IP) ? c->ri_off[dhi] - i0 : 0u;
   if (Ri && nw) {
     const DIPTest* tests = c->ip_tests.as<DIPTest>() + i0;
@@ -4703,7 +4884,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   FrontA fa{};
   fa.fill_p = c->ip_rng.as<uint32_t>();
   // the word spans and chunk masks of the IP rows and of PM builds' sparse pod rows (cnz needs no reset)
-  fa.fill_n = (c->Ri || (!ido_mode(c) && c->Rp)) ? pb.peers.size() * 4 : 0;
+  fa.fill_n = (c->Ri || c->Rr || (!ido_mode(c) && c->Rp)) ? pb.peers.size() * 4 : 0;
   fa.nb[0] = blocks((fa.fill_n + 255) / 256);
   fa.M = M;
   fa.D = D;
@@ -4747,6 +4928,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.rng = c->ip_rng.as<uint32_t>();
   fb.cnz = ip_cnz(c);
   fb.ip_grp = IP_GROUP;
+  fb.ipr_iv = c->ipr_iv.as<uint2>();
+  fb.ipsort = c->ipsort.as<uint32_t>();
   for (int x = 0; x < 2; x++) {
     const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
     const uint32_t i0 = c->ri_off[dlo];
@@ -4754,6 +4937,9 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fb.tests[x] = c->ip_tests.as<DIPTest>() + i0;
     peer_chunks(c, one_win ? 1 : x, fb.ic0[x], fb.inch[x]);
     fb.nb[x] = fb.Ri[x] && fb.inch[x] ? blocks(ip_rows_blocks(fb.Ri[x], fb.inch[x], fb.ip_grp)) : 0u;
+    fb.Rr[x] = one_win && x ? 0u : c->rr_off[dhi] - c->rr_off[dlo];
+    fb.rtests[x] = c->ipr_tests.as<DIPRange>() + c->rr_off[dlo];
+    fb.nb[9 + x] = fb.Rr[x] && fb.inch[x] ? blocks((uint64_t(fb.Rr[x]) + 3) / 4) : 0u;
   }
   fb.E = E;
   fb.EW = EW;
@@ -5803,6 +5989,11 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "front_fused") range(0, 1), c->front_fused = int(value);
     else if (n == "pod_words") range(-1, 1), c->pod_words = int(value);
     else if (n == "pod_rows") range(-1, 1), c->pod_rows = int(value);
+    else if (n == "ip_range") {
+      range(-1, 0);
+      c->ip_range = int(value);
+      c->order_lo = c->order_hi = -1;  // the next run re-plans which IP rows are range-built
+    }
     else if (n == "member_wave") range(-1, 1), c->member_wave = int(value);
     else if (n == "class_rpb") range(0, 64), c->class_rpb_opt = value;
     else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
@@ -5828,6 +6019,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   if (n == "graphs") *value = c->use_graphs;
   else if (n == "front_fused") *value = c->front_fused;
   else if (n == "pod_rows") *value = c->pod_rows;
+  else if (n == "ip_range") *value = c->ip_range;
   else if (n == "member_wave") *value = c->member_wave;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "pl_wave") *value = c->pl_wave;

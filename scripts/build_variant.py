@@ -1,5 +1,5 @@
 """Build an A/B variant of libcyclonus_hip.so with extra -D flags (dev helper):
-    python scripts/build_variant.py NAME -DCYC_IP_AFFINE=0   -> cyclonus_amd/_build/var_NAME/libcyclonus_hip.so
+    python scripts/build_variant.py NAME -DMACRO=1          -> cyclonus_amd/_build/var_NAME/libcyclonus_hip.so
     python scripts/build_variant.py NAME --rev HEAD           -> the engine.hip of a git revision
     python scripts/build_variant.py NAME --src FILE           -> a patched copy of engine.hip (diagnostics)
 Run it with CYC_HIP_LIB=<that path> (cyclonus_amd/_lib.py)."""

@@ -332,11 +332,57 @@ def _ip_interval_problem(seed, n_pods=700):
     return pols, res, [{"AllAvailable": True}]
 
 
+def _ip_stride_problem(seed, n_ns=6, per_ns=90):
+    """Pod addresses that step by 256 inside a namespace (10.ns.j.1, config #2's shape: no word holds
+    consecutive addresses) and IPBlocks from /16 with /24 excepts down to single pods, v4-mapped and
+    IPv6 pods mixed in: IP rows built from the address index (ip_rows_range_blk) and by a test per
+    word with straddling words tested a pod per lane."""
+    rng = np.random.default_rng(seed)
+    pods, nss = [], {}
+    for i in range(n_ns):
+        nss[f"n{i}"] = {"ns": f"n{i}"}
+        for j in range(per_ns):
+            u = rng.random()
+            ip = f"10.{i}.{j}.1" if u < 0.8 else (f"::ffff:10.{i}.{j}.2" if u < 0.9 else f"fd00::{i:x}:{j:x}")
+            pods.append({"Namespace": f"n{i}", "Name": f"p{j}", "Labels": {"i": str(j % 5)}, "IP": ip,
+                         "Containers": [{"Name": "c", "Port": 80, "Protocol": "TCP", "PortName": "serve-80-tcp"}]})
+    res = {"Namespaces": nss, "Pods": pods}
+    pols = []
+    for k in range(14):
+        peers = []
+        for _ in range(int(rng.integers(1, 4))):
+            t, a, b = int(rng.integers(0, 4)), int(rng.integers(0, n_ns)), int(rng.integers(0, per_ns))
+            if t == 0:
+                ib = {"cidr": f"10.{a}.0.0/16", "except": [f"10.{a}.{b}.0/24", f"10.{a}.{(b + 7) % per_ns}.0/24"]}
+            elif t == 1:
+                ib = {"cidr": f"10.{a}.{b & ~15}.0/20"}
+            elif t == 2:
+                ib = {"cidr": f"10.{a}.{b}.1/32"}
+            else:
+                ib = {"cidr": "fd00::/64", "except": [f"fd00::{a:x}:0/112"]}
+            peers.append({"ipBlock": ib})
+        spec = {"podSelector": {"matchLabels": {"i": str(k % 5)}}, "policyTypes": ["Ingress", "Egress"],
+                "ingress": [{"from": peers}], "egress": [{"to": peers[::-1]}]}
+        pols.append({"metadata": {"name": f"s{k}", "namespace": f"n{k % n_ns}"}, "spec": spec})
+    return pols, res, [{"AllAvailable": True}]
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_ip_interval_words(gpu, seed):
-    pols, res, probes = _ip_interval_problem(seed)
-    o, g = run_both(pols, res, probes)
-    assert_same(o, g, f"ip intervals seed {seed}")
+    """IP rows by a test per word (ip_range = 0) and, where an IPBlock matches few close pods, from
+    the address index (auto), on affine addresses and on addresses stepping by 256, against the oracle."""
+    for pols, res, probes in (_ip_interval_problem(seed), _ip_stride_problem(seed)):
+        for ipr in (-1, 0):
+            eng = Engine(0)
+            eng.set_option("ip_range", ipr)
+            assert eng.get_option("ip_range") == ipr
+            o, g = run_both(pols, res, probes, engine=eng)
+            assert_same(o, g, f"ip intervals seed {seed} ip_range {ipr}")
+            for opts in ({"front_fused": 0}, {"graphs": 0}):
+                for k, v in opts.items():
+                    eng.set_option(k, v)
+                o2, g2 = run_both(pols, res, probes, engine=eng)
+                assert_same(o2, g2, f"ip intervals seed {seed} ip_range {ipr} {opts}")
 
 
 def _shared_ipblock_problem(seed, bad=False):
@@ -684,7 +730,7 @@ def test_launch_modes_and_knobs(gpu):
     assert_same(want, eng.run_host(), "DAG graph")
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
-    for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
+    for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_range", 1), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
