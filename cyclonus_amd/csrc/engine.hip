@@ -3019,6 +3019,49 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   }
 }
 
+// Rows of 16-32 KB (config #4: 25 KB), persistent: G blocks per XCD walk their XCD's segment of the
+// row list with a stride of G, each loading the NEXT row's (pod, identity) pair and class while it
+// copies the current row, so a row's index chain is off the critical path and a block is
+// dispatched once per ~dozens of rows instead of once per row.  UNROLL x 256 x 16 B covers a row.
+template <int UNROLL>
+__global__ __launch_bounds__(256) void k_emit_persist(EmitArgs a) {
+  emit_status(a);
+  const uint32_t b = blockIdx.x, x = b & 7, g = b >> 3, G = gridDim.x >> 3;
+  const uint32_t n = a.n_rows[0] + a.n_rows[1], r_end = min(n, (x + 1) * a.per_xcd);
+  uint32_t r = x * a.per_xcd + g;
+  if (r >= r_end) return;
+  const uint32_t n2 = uint32_t(a.row_words / 2);
+  uint32_t pl;
+  uint2 pi = emit_row_of(a, r, pl);
+  const u64x2* si = reinterpret_cast<const u64x2*>(emit_src(a, pl, pi));
+  while (true) {
+    u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.row_words);
+    u64x2 v[UNROLL];
+    if (si) {
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++)
+        if (threadIdx.x + u * 256 < n2) v[u] = si[threadIdx.x + u * 256];
+    }
+    // the next row's chain, issued behind this row's loads (in-order counters: waiting for this
+    // row's data does not wait for it)
+    const uint32_t rn = r + G;
+    const bool more = rn < r_end;
+    uint32_t pln = 0;
+    const uint2 pin = more ? emit_row_of(a, rn, pln) : make_uint2(0, 0);
+    const u64x2* sin = more ? reinterpret_cast<const u64x2*>(emit_src(a, pln, pin)) : nullptr;
+    if (si) {
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++)
+        if (threadIdx.x + u * 256 < n2) emit_store(v[u], &di[threadIdx.x + u * 256]);
+    }
+    if (!more) break;
+    r = rn;
+    pl = pln;
+    pi = pin;
+    si = sin;
+  }
+}
+
 // Planes whose rows differ in length (a source shard: ingress rows of every destination over the
 // shard's words, egress rows of its sources over all words) in ONE launch: the unit list is plane 0's
 // rows in groups of unit_rows[0], then plane 1's in groups of unit_rows[1], each group about one
