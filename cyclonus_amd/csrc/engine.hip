@@ -3019,49 +3019,6 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   }
 }
 
-// Rows of 16-32 KB (config #4: 25 KB), persistent: G blocks per XCD walk their XCD's segment of the
-// row list with a stride of G, each loading the NEXT row's (pod, identity) pair and class while it
-// copies the current row, so a row's index chain is off the critical path and a block is
-// dispatched once per ~dozens of rows instead of once per row.  UNROLL x 256 x 16 B covers a row.
-template <int UNROLL>
-__global__ __launch_bounds__(256) void k_emit_persist(EmitArgs a) {
-  emit_status(a);
-  const uint32_t b = blockIdx.x, x = b & 7, g = b >> 3, G = gridDim.x >> 3;
-  const uint32_t n = a.n_rows[0] + a.n_rows[1], r_end = min(n, (x + 1) * a.per_xcd);
-  uint32_t r = x * a.per_xcd + g;
-  if (r >= r_end) return;
-  const uint32_t n2 = uint32_t(a.row_words / 2);
-  uint32_t pl;
-  uint2 pi = emit_row_of(a, r, pl);
-  const u64x2* si = reinterpret_cast<const u64x2*>(emit_src(a, pl, pi));
-  while (true) {
-    u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.row_words);
-    u64x2 v[UNROLL];
-    if (si) {
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++)
-        if (threadIdx.x + u * 256 < n2) v[u] = si[threadIdx.x + u * 256];
-    }
-    // the next row's chain, issued behind this row's loads (in-order counters: waiting for this
-    // row's data does not wait for it)
-    const uint32_t rn = r + G;
-    const bool more = rn < r_end;
-    uint32_t pln = 0;
-    const uint2 pin = more ? emit_row_of(a, rn, pln) : make_uint2(0, 0);
-    const u64x2* sin = more ? reinterpret_cast<const u64x2*>(emit_src(a, pln, pin)) : nullptr;
-    if (si) {
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++)
-        if (threadIdx.x + u * 256 < n2) emit_store(v[u], &di[threadIdx.x + u * 256]);
-    }
-    if (!more) break;
-    r = rn;
-    pl = pln;
-    pi = pin;
-    si = sin;
-  }
-}
-
 // Planes whose rows differ in length (a source shard: ingress rows of every destination over the
 // shard's words, egress rows of its sources over all words) in ONE launch: the unit list is plane 0's
 // rows in groups of unit_rows[0], then plane 1's in groups of unit_rows[1], each group about one
@@ -3547,6 +3504,7 @@ struct cyc_ctx {
   // address (host keys for the binary searches; the pod order on the device), and per direction the
   // range-built rows
   std::vector<uint32_t> ip4_key, ipsort_host;
+  std::vector<uint8_t> word_aff;  // per 64-pod word: bit f set when family f's pods there are affine (or absent)
   std::vector<std::array<uint32_t, 4>> ip6_key;
   DevBuf ipsort, ipr_tests, ipr_iv;
   uint32_t rr_off[3] = {0, 0, 0}, Rr = 0;
@@ -3562,7 +3520,8 @@ struct cyc_ctx {
                         // events, -1 = auto: 2 when the fused front applies (its launches on one
                         // stream start ~8 us sooner after the previous step's emit than a graph
                         // replay: profiles/r01_front_fused_ab.txt), else 1
-  int ip_range = -1;    // "ip_range": IP rows of few, close pods from the address index (-1 auto, 0 never)
+  int ip_range = -1;    // "ip_range": IP rows of few, close pods from the address index: -1 auto (where the
+                        // words are not affine), 1 wherever they fit, 0 never
   int pod_rows = -1;    // "pod_rows": pod-peer PM rows per pod directly (1), through identity outcomes
                         // and word runs (0), or -1 = direct when identities >= pods / 2
   int member_wave = -1; // "member_wave": membership with a wave (1) or a thread (0) per identity,
@@ -3976,6 +3935,7 @@ static void prepare_device(cyc_ctx* c) {
     {  // per-word, per-family address intervals for k_ip_rows_fast, then one record per 64-word chunk
       const uint32_t NC = (pb.W + 63) / 64;
       std::vector<DWordIP> wi(pb.W + NC);
+      c->word_aff.assign(pb.W, 3);
       for (uint32_t w = 0; w < pb.W; w++) {
         DWordIP d{};
         d.min4 = 0xFFFFFFFFu;
@@ -4018,6 +3978,7 @@ static void prepare_device(cyc_ctx* c) {
         }
         for (int f = 0; f < 2; f++)
           if (first[f] >= 0 && aff[f]) d.aff |= (uint32_t(first[f]) | 0x80u) << (8 * f);
+        c->word_aff[w] = uint8_t((first[0] < 0 || aff[0] ? 1u : 0u) | (first[1] < 0 || aff[1] ? 2u : 0u));
         wi[w] = d;
       }
       for (uint32_t ch = 0; ch < NC; ch++) {
@@ -4405,6 +4366,13 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
         whi = std::max(whi, c->ipsort_host[x] / 64);
       }
     if (n && whi - wlo >= IPR_SPAN) return false;
+    // words whose pods of the family hold affine addresses get the network's lanes from its bounds
+    // in k_ip_rows_fast (no per-pod test): keep those rows there (config #4: range-built rows
+    // made launch B 64 -> 70 us; config #2's addresses step by 256, so its words are not affine)
+    const uint8_t fbit = t.cidr.fam == 4 ? 1u : 2u;
+    bool all_aff = c->word_aff.size() == pb.W;
+    for (uint32_t w = wlo; all_aff && n && w <= whi; w++) all_aff = (c->word_aff[w] & fbit) != 0;
+    if (all_aff && c->ip_range < 0) return false;
     out = DIPRange{t.peer, uint32_t(riv.size()), uint32_t(iv.size()), n ? wlo : 0u};
     riv.insert(riv.end(), iv.begin(), iv.end());
     return true;
@@ -6033,7 +6001,7 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "pod_words") range(-1, 1), c->pod_words = int(value);
     else if (n == "pod_rows") range(-1, 1), c->pod_rows = int(value);
     else if (n == "ip_range") {
-      range(-1, 0);
+      range(-1, 1);
       c->ip_range = int(value);
       c->order_lo = c->order_hi = -1;  // the next run re-plans which IP rows are range-built
     }

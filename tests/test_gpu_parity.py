@@ -369,10 +369,11 @@ def _ip_stride_problem(seed, n_ns=6, per_ns=90):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_ip_interval_words(gpu, seed):
-    """IP rows by a test per word (ip_range = 0) and, where an IPBlock matches few close pods, from
-    the address index (auto), on affine addresses and on addresses stepping by 256, against the oracle."""
+    """IP rows by a test per word (ip_range = 0), from the address index wherever an IPBlock matches
+    few close pods (1), and by the auto rule (index only over non-affine words), on affine addresses
+    and on addresses stepping by 256, against the oracle."""
     for pols, res, probes in (_ip_interval_problem(seed), _ip_stride_problem(seed)):
-        for ipr in (-1, 0):
+        for ipr in (-1, 0, 1):
             eng = Engine(0)
             eng.set_option("ip_range", ipr)
             assert eng.get_option("ip_range") == ipr
@@ -730,7 +731,7 @@ def test_launch_modes_and_knobs(gpu):
     assert_same(want, eng.run_host(), "DAG graph")
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
-    for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_range", 1), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
+    for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_range", 2), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
