@@ -2288,7 +2288,6 @@ __device__ __forceinline__ uint64_t expand_runs32(const uint32_t* sq, uint32_t r
 }
 
 constexpr uint32_t IDO_RPB_MAX = 64;  // class_rpb's upper bound
-constexpr uint32_t IDO_STG = 8;       // identity-set rows a wave stages at once (class_rows_ido_blk)
 constexpr uint32_t IDO_IPL = 16;      // IP peers per representative staged in LDS (row, span, port bits)
 // Grid rows of the IDO class rows per (slot chunk, representative group): 256-word chunks (staging
 // once for 2 / 4 / 7 chunks per block measured slower on config #3: profiles/r03_ido_rows_ab.txt).
@@ -2385,27 +2384,16 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
 #pragma unroll
   for (int kk = 0; kk < KC; kk++) ud[kk] = EGRESS && UNI ? a.udesc[min(k0 + kk, a.K - 1)] : 0;
   __syncthreads();
-  // the IP-list entry of this thread's first staging pass (below), loaded here so its round trip
-  // overlaps the identity sets' loads
-  const bool stage_ip = !EGRESS || a.portbits != nullptr;
-  uint4 jp0 = make_uint4(0u, 0u, 0u, 0u);
-  bool ok0 = false;
-  if (stage_ip) {
-    const RepHead<KC>& h = s_rep[min(threadIdx.x / IDO_IPL, nr - 1)];
-    ok0 = threadIdx.x < nr * IDO_IPL && threadIdx.x % IDO_IPL < h.m;
-    jp0 = *(ok0 ? a.ip_list + h.ipoff + threadIdx.x % IDO_IPL : reinterpret_cast<const uint4*>(a.zero));
-  }
-  {  // identity sets: a wave per (representative, row) at a time, lanes over the row's words, IDO_STG
-     // rows' loads in flight (16 representatives x 4 rows: one round trip per wave); (representative,
-     // row) is wave-uniform, so the transposing index math is scalar
+  {  // identity sets: a wave per (representative, row) at a time, lanes over the row's words, 4 rows'
+     // loads in flight; (representative, row) is wave-uniform, so the transposing index math is scalar
     const uint32_t nrows = nr * nrow, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t r0 = wv; r0 < nrows; r0 += IDO_STG * nw)
+    for (uint32_t r0 = wv; r0 < nrows; r0 += 4 * nw)
       for (uint32_t j0 = 0; j0 < a.EW; j0 += 64) {
         const uint32_t j = min(j0 + lane, a.EW - 1);
-        uint64_t v[IDO_STG];
+        uint64_t v[4];
 #pragma unroll
-        for (uint32_t u = 0; u < IDO_STG; u++) {
+        for (uint32_t u = 0; u < 4; u++) {
           const uint32_t qr = min(r0 + u * nw, nrows - 1), q = qr / nrow, row = qr - q * nrow;
           const uint64_t i = s_rep[q].i;
           int32_t d = EGRESS ? int32_t(row) : int32_t(k0 + row);  // the set's row in B
@@ -2417,7 +2405,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
           v[u] = a.B[(i * a.NB + uint32_t(d)) * a.EW + j];
         }
 #pragma unroll
-        for (uint32_t u = 0; u < IDO_STG; u++) {
+        for (uint32_t u = 0; u < 4; u++) {
           const uint32_t qr = r0 + u * nw, q = qr / nrow, row = qr - q * nrow;
           if (qr >= nrows || j0 + lane >= a.EW) continue;
           uint32_t* dst = sB32 + (q * EW32 + 2 * j) * NS + row;
@@ -2430,6 +2418,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   // egress: the descriptor bit row; ingress: a bit per block slot), so the row loop issues only the
   // PM loads (no list -> port table chain per batch)
   uint4* s_il = reinterpret_cast<uint4*>(sB32 + ((nr * EW32 * NS + 3) & ~3u));  // 16-byte aligned
+  const bool stage_ip = !EGRESS || a.portbits != nullptr;
   // per representative: which staged peers have nonzero PM words inside the block's words (a CIDR
   // covers a few namespaces' pods, so most (representative, 256-word chunk) pairs have none)
   __shared__ uint32_t s_ipm[IDO_RPB_MAX];
@@ -2439,9 +2428,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     for (uint32_t t = threadIdx.x; t < ((nr * IDO_IPL + 63) & ~63u); t += blockDim.x) {
       const RepHead<KC>& h = s_rep[min(t / IDO_IPL, nr - 1)];
       const uint32_t x = t % IDO_IPL;
-      const bool first = t == threadIdx.x;  // (pass 1: loaded above)
-      const bool ok = first ? ok0 : t < nr * IDO_IPL && x < h.m;
-      const uint4 jp = first ? jp0 : *(ok ? a.ip_list + h.ipoff + x : reinterpret_cast<const uint4*>(a.zero));
+      const bool ok = t < nr * IDO_IPL && x < h.m;
+      const uint4 jp = *(ok ? a.ip_list + h.ipoff + x : reinterpret_cast<const uint4*>(a.zero));
       const uint64_t hit = __ballot(ok && jp.z <= whi && jp.w >= wlo);
       if (x == 0 && t < nr * IDO_IPL) s_ipm[t / IDO_IPL] = uint32_t(hit >> (t & 63 & ~(IDO_IPL - 1))) & ((1u << IDO_IPL) - 1);
       uint32_t bits = 0;
