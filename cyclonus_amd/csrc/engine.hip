@@ -3019,6 +3019,35 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   }
 }
 
+// Rows of 16-32 KB through buffer loads / stores: the chunk offsets u x BS x 16 B go to the scalar
+// offset, so a lane keeps one offset register and all its data in flight (128 x 13: 53 VGPRs, 8
+// waves a SIMD, 13 x 16 B a lane; the flat-address form needs an address pair per chunk: 84 VGPRs);
+// offsets past the row (the last pass's idle lanes) fall outside the buffer's range and are dropped.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int BUF_RSRC_W3 = 0x00020000;  // buffer resource word 3 for gfx9 raw buffers
+template <int BS, int UNROLL>
+__global__ __launch_bounds__(BS) void k_emit_wide_buf(EmitArgs a) {
+  emit_status(a);
+  const uint32_t b = blockIdx.x, n = a.n_rows[0] + a.n_rows[1], x = b & 7;
+  const uint32_t r = x * a.per_xcd + (b >> 3);
+  if (r >= min(n, (x + 1) * a.per_xcd)) return;
+  uint32_t pl;
+  const uint2 pi = emit_row_of(a, r, pl);
+  const uint64_t* si = emit_src(a, pl, pi);
+  if (!si) return;  // in-place class row: already written
+  uint64_t* di = a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.row_words;
+  const uint32_t bytes = uint32_t(a.row_words * 8);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(si), 0, bytes, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(di, 0, bytes, BUF_RSRC_W3);
+  for (uint32_t x0 = 0; x0 < bytes; x0 += BS * UNROLL * 16) {
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, x0 + u * BS * 16, 0);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, threadIdx.x * 16, x0 + u * BS * 16, 2);  // nt
+  }
+}
+
 // Planes whose rows differ in length (a source shard: ingress rows of every destination over the
 // shard's words, egress rows of its sources over all words) in ONE launch: the unit list is plane 0's
 // rows in groups of unit_rows[0], then plane 1's in groups of unit_rows[1], each group about one
@@ -4748,10 +4777,13 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     return;
   }
   const uint64_t row_bytes = ea.row_words * 8;
-  // 16-byte chunks per thread and pass <= 8 keeps a block at <= 48 VGPRs (8 waves a SIMD): a 512 x 13
-  // one-pass block held 84 VGPRs, 5 waves a SIMD, and ran config #3 3.5 % slower per step on a slow
-  // box (profiles/r03_emit_ab.txt; 512 x 7 in two passes was slower still)
-  if (row_bytes > 512 * 7 * 16) {  // > 56 KB: 1024 x 7 (config #3: 98 KB rows, one pass)
+  // A 512 x 13 one-pass block with flat addresses held 84 VGPRs, 5 waves a SIMD, and ran config #3
+  // 3.5 % slower per step (profiles/r03_emit_ab.txt); through buffer ops it holds 54 (8 waves a
+  // SIMD) and beats 1024 x 7: config #3 emit 3000 vs 3058-3070 us (profiles/r04_emit_buf_ab.txt).
+  // (128 x 13 buffer blocks for config #4's 25 KB rows lost: 442-447 vs 419-424 us.)
+  if (row_bytes > 512 * 7 * 16 && row_bytes <= 512 * 13 * 16) {  // 56-104 KB: config #3's 98 KB rows, one pass
+    k_emit_wide_buf<512, 13><<<g, 512, 0, st>>>(ea);
+  } else if (row_bytes > 512 * 7 * 16) {  // > 104 KB: 1024 x 7 passes
     k_emit_wide<1024, 7><<<g, 1024, 0, st>>>(ea);
   } else if (row_bytes > 256 * 8 * 16) {  // 32-56 KB: 512 x 7 (source shards at N = 2)
     k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
