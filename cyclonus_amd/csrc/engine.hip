@@ -1107,23 +1107,29 @@ struct MemberArgs {
   uint32_t* cnt;
   uint64_t* hash;
   uint8_t* err;               // a target selector panics on this identity
-  unsigned long long* ht_key; // hash table (capacity ht_cap, power of two), 0 = empty
-  uint32_t* ht_rep;           // min identity per key
+  unsigned long long* ht_key; // hash table (capacity ht_cap, power of two) of 16-byte entries:
+                              // u64 key (~0 = empty), u32 min identity per key, u32 unused
   uint32_t ht_cap;
   const uint32_t* act;        // identities used by the rows of this run (range plan)
+  const uint4* actrec;        // per act[] entry: (label set, namespace targets lo, hi, list offset)
   uint32_t n_act;
   uint32_t* reps;             // class representatives, act[] order within each block (k_classify)
   uint32_t* rep_cnt;          // set to ~0 by k_member: ends at count - 1
   const uint32_t* id_blk;     // batched blocks: each identity's block (classes never span blocks), else null
 };
 
-__device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* keys, uint32_t cap, uint64_t h) {
+// Entry s: words 2s (key) and 2s + 1 (low half: representative); a probe reads both in one load.
+__device__ __forceinline__ uint32_t* ht_rep_at(unsigned long long* ht, uint32_t s) {
+  return reinterpret_cast<uint32_t*>(ht + 2 * uint64_t(s) + 1);
+}
+
+__device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* ht, uint32_t cap, uint64_t h) {
   uint32_t s = uint32_t(h) & (cap - 1);
   for (uint32_t probe = 0; probe < cap; probe++) {
-    unsigned long long cur = keys[s];
+    unsigned long long cur = ht[2 * uint64_t(s)];
     if (cur == h) return s;
     if (cur == ~0ull) {
-      unsigned long long old = atomicCAS(&keys[s], ~0ull, (unsigned long long)h);
+      unsigned long long old = atomicCAS(&ht[2 * uint64_t(s)], ~0ull, (unsigned long long)h);
       if (old == ~0ull || old == h) return s;
     }
     s = (s + 1) & (cap - 1);
@@ -1131,12 +1137,13 @@ __device__ __forceinline__ uint32_t ht_find_or_insert(unsigned long long* keys, 
   return 0xFFFFFFFFu;  // unreachable: cap >= 2 * n_ident
 }
 
-__device__ __forceinline__ uint32_t ht_find(const unsigned long long* keys, uint32_t cap, uint64_t h) {
+// The representative stored under key h (plain 16-byte loads of whole entries), or ~0 when absent.
+__device__ __forceinline__ uint32_t ht_find_rep(const unsigned long long* ht, uint32_t cap, uint64_t h) {
   uint32_t s = uint32_t(h) & (cap - 1);
   for (uint32_t probe = 0; probe < cap; probe++) {
-    unsigned long long k = keys[s];
-    if (k == h) return s;
-    if (k == ~0ull) return 0xFFFFFFFFu;
+    const ulonglong2 e = reinterpret_cast<const ulonglong2*>(ht)[s];
+    if (e.x == h) return uint32_t(e.y);
+    if (e.x == ~0ull) return 0xFFFFFFFFu;
     s = (s + 1) & (cap - 1);
   }
   return 0xFFFFFFFFu;
@@ -1148,10 +1155,9 @@ __device__ __forceinline__ uint32_t ht_find(const unsigned long long* keys, uint
 // otherwise the CAS insert + atomicMin (identities sharing a class then cost one read each
 // instead of a serialised atomic on one address).
 __device__ __forceinline__ void ht_elect(const MemberArgs& a, uint64_t h, uint32_t i) {
-  const uint32_t s0 = ht_find(a.ht_key, a.ht_cap, h);
-  if (s0 != 0xFFFFFFFFu && a.ht_rep[s0] <= i) return;
+  if (ht_find_rep(a.ht_key, a.ht_cap, h) <= i) return;  // (absent: ~0)
   const uint32_t s = ht_find_or_insert(a.ht_key, a.ht_cap, h);
-  atomicMin(&a.ht_rep[s], i);
+  atomicMin(ht_rep_at(a.ht_key, s), i);
 }
 
 __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t nblk_) {
@@ -1159,9 +1165,9 @@ __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t
   uint32_t ii = bid_ * blockDim.x + threadIdx.x;
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
-  uint32_t ns = a.id_ns[i], ls = a.id_ls[i];
-  uint32_t lo = a.tns_lo[ns], hi = a.tns_hi[ns];
-  uint32_t n = 0, off = a.list_off[i];
+  const uint4 rec = a.actrec[ii];
+  const uint32_t ls = rec.x, lo = rec.y, hi = rec.z, off = rec.w;
+  uint32_t n = 0;
   uint8_t e = 0;
   uint64_t h = 0x5bd1e9955bd1e995ull;
   constexpr uint32_t MB = 8;  // targets whose selector results are loaded at once
@@ -1213,8 +1219,8 @@ __device__ __forceinline__ void member_wave_blk(MemberArgs a, uint32_t bid_, uin
   const uint32_t lane = threadIdx.x & 63, ii = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6));  // wave-uniform
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
-  const uint32_t ns = a.id_ns[i], ls = a.id_ls[i];
-  const uint32_t lo = a.tns_lo[ns], hi = a.tns_hi[ns], off = a.list_off[i];
+  const uint4 rec = a.actrec[ii];
+  const uint32_t ls = rec.x, lo = rec.y, hi = rec.z, off = rec.w;
   uint32_t n = 0;
   bool e = false;
   uint64_t h = 0x5bd1e9955bd1e995ull;
@@ -1248,14 +1254,14 @@ __global__ __launch_bounds__(256) void k_member_wave(MemberArgs a) { member_wave
 // 8 list entries / job slots of both identities per batch, every load of a batch issued before any
 // compare (one memory round trip per batch instead of one per entry).  id_desc null: egress.
 __device__ __forceinline__ uint32_t class_of_identity(uint32_t i, const uint8_t* __restrict__ err, const uint64_t* __restrict__ hash,
-                                                      const unsigned long long* ht_key, const uint32_t* ht_rep, uint32_t ht_cap,
+                                                      const unsigned long long* ht_key, uint32_t ht_cap,
                                                       const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ list_off,
                                                       const uint32_t* __restrict__ list, const uint32_t* __restrict__ id_blk,
                                                       const uint8_t* __restrict__ id_status, const int32_t* __restrict__ id_desc,
                                                       uint32_t K) {
   if (err[i]) return i;
-  const uint32_t s = ht_find(ht_key, ht_cap, hash[i]);
-  const uint32_t r = s == 0xFFFFFFFFu ? i : ht_rep[s];
+  const uint32_t r0 = ht_find_rep(ht_key, ht_cap, hash[i]);
+  const uint32_t r = r0 == 0xFFFFFFFFu ? i : r0;
   if (r == i) return i;
   const uint32_t n = cnt[i], oi = list_off[i], orr = list_off[r];
   bool eq = cnt[r] == n && (!id_blk || id_blk[r] == id_blk[i]);
@@ -1295,7 +1301,7 @@ __device__ __forceinline__ void classify_blk(MemberArgs a, uint32_t* __restrict_
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool live = ii < a.n_act;
   const uint32_t i = live ? a.act[ii] : 0;
-  const uint32_t c = live ? class_of_identity(i, a.err, a.hash, a.ht_key, a.ht_rep, a.ht_cap, a.cnt, a.list_off, a.list, a.id_blk,
+  const uint32_t c = live ? class_of_identity(i, a.err, a.hash, a.ht_key, a.ht_cap, a.cnt, a.list_off, a.list, a.id_blk,
                                               a.id_status, a.id_desc, a.K)
                           : i;
   if (live) class_of[i] = c;
@@ -2614,6 +2620,7 @@ __global__ __launch_bounds__(256) void k_class_rows_ido(RowArgs a) { class_rows_
 // directions' blocks share every launch.
 //   A: IP word spans reset | port table | slot words | selectors        (independent)
 //   B: IP rows (both directions) | pod-peer identity sets (both) | membership in | membership eg
+//      (membership dispatched first unless the IP rows fill the chip: FrontB::member_first)
 //   C: class election in | eg           D: identity sets in | eg         E: class rows in | eg
 struct FrontA {
   uint32_t nb[4];
@@ -2688,9 +2695,29 @@ struct FrontB {
   const uint32_t *id_ns, *id_nsls, *id_ls;
   MemberArgs ma[2];
   uint32_t member_wave[2];  // 1: a wave per identity (k_member_wave), 0: a thread per identity
+  // membership blocks dispatched first (1) or after the pod-peer rows (0): few blocks, each a chain
+  // of dependent loads, which first start at once instead of waiting for slots behind thousands of
+  // short pod-row blocks (config #2: B 23.1 -> 16.5 us); behind a chip-full of IP rows they go last,
+  // filling the tail instead of holding slots the IP rows need (config #4: first 66.6, last 64.1 us)
+  uint32_t member_first;
 };
+__device__ __forceinline__ void front_b_member(const FrontB& f, uint32_t b) {
+  if (b < f.nb[4]) {
+    if (f.member_wave[0]) member_wave_blk(f.ma[0], b, f.nb[4]);
+    else member_blk(f.ma[0], b, f.nb[4]);
+    return;
+  }
+  b -= f.nb[4];
+  if (f.member_wave[1]) member_wave_blk(f.ma[1], b, f.nb[5]);
+  else member_blk(f.ma[1], b, f.nb[5]);
+}
 __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   uint32_t b = blockIdx.x;
+  const uint32_t nm = f.nb[4] + f.nb[5];
+  if (f.member_first) {
+    if (b < nm) return front_b_member(f, b);
+    b -= nm;
+  }
 #pragma unroll
   for (int x = 0; x < 2; x++) {
     if (b < f.nb[x])
@@ -2709,14 +2736,9 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
     }
     b -= f.nb[2 + x];
   }
-#pragma unroll
-  for (int d = 0; d < 2; d++) {
-    if (b < f.nb[4 + d]) {
-      if (f.member_wave[d]) member_wave_blk(f.ma[d], b, f.nb[4 + d]);
-      else member_blk(f.ma[d], b, f.nb[4 + d]);
-      return;
-    }
-    b -= f.nb[4 + d];
+  if (!f.member_first) {
+    if (b < nm) return front_b_member(f, b);
+    b -= nm;
   }
   if (b < f.nb[6]) {  // for the identity sets and the class rows
     if (f.bits_direct) return portbits_direct_blk(f.M, f.D, f.pre.pms, f.pre.pents, f.pre.descs, f.portbits, b);
@@ -3483,7 +3505,7 @@ struct DirDev {
   uint32_t n = 0, ht_cap = 0;
   // hash table buffer = [cap] u64 keys, [cap] u32 reps, 1 u32 representative counter: one
   // 0xFF memset per run empties the table and sets the counter to ~0 (= count - 1 for 0)
-  uint32_t* rep_cnt() { return reinterpret_cast<uint32_t*>(static_cast<char*>(ht_key.p) + uint64_t(ht_cap) * 12); }
+  uint32_t* rep_cnt() { return reinterpret_cast<uint32_t*>(static_cast<char*>(ht_key.p) + uint64_t(ht_cap) * 16); }
 };
 }  // namespace
 
@@ -3539,7 +3561,7 @@ struct cyc_ctx {
   uint32_t rr_off[3] = {0, 0, 0}, Rr = 0;
   uint32_t rpu_off[3] = {0, 0, 0};  // sub-lists of pod_peers_u: one pod peer per distinct matcher
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
-  DevBuf act[2], sel_list;
+  DevBuf act[2], actrec[2], sel_list;
   DevBuf arow[2];  // per identity: its first pod's row in the run's row range (in-place class rows)
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
   double act_targets[2] = {0, 0};  // mean namespace targets per active identity (range plan)
@@ -4082,7 +4104,7 @@ static void prepare_device(cyc_ctx* c) {
     dd.cnt.alloc(std::max<uint64_t>(dd.n * 4ull, 16));
     dd.hash.alloc(std::max<uint64_t>(dd.n * 8ull, 16));
     dd.err.alloc(std::max<uint64_t>(dd.n, 16));
-    dd.ht_key.alloc(uint64_t(dd.ht_cap) * 12 + 16);  // [cap] u64 keys (empty = ~0), [cap] u32 reps, counter
+    dd.ht_key.alloc(uint64_t(dd.ht_cap) * 16 + 16);  // [cap] 16-byte entries (key ~0 = empty, rep), counter
     HIPCHK(hipMemset(dd.ht_key.p, 0xFF, dd.ht_key.bytes));  // empty; afterwards every run's class rows empty it
     if (!c->zeros.p) {
       c->zeros.alloc(256);
@@ -4192,9 +4214,9 @@ static MemberArgs member_args(cyc_ctx* c, int d) {
   a.hash = dd.hash.as<uint64_t>();
   a.err = dd.err.as<uint8_t>();
   a.ht_key = dd.ht_key.as<unsigned long long>();
-  a.ht_rep = reinterpret_cast<uint32_t*>(dd.ht_key.as<uint64_t>() + dd.ht_cap);
   a.ht_cap = dd.ht_cap;
   a.act = c->act[d].as<uint32_t>();
+  a.actrec = c->actrec[d].as<uint4>();
   a.n_act = c->n_act[d];
   a.reps = dd.reps.as<uint32_t>();
   a.rep_cnt = dd.rep_cnt();
@@ -4289,6 +4311,17 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
     for (uint32_t i : act) tsum += pb.tns_hi[d][I.ns[i]] - pb.tns_lo[d][I.ns[i]];
     c->act_targets[d] = act.empty() ? 0.0 : double(tsum) / double(act.size());
     upload(c->act[d], act);
+    // the membership's per-identity inputs in one 16-byte record (one load instead of the chain
+    // act -> id_ls / id_ns / list_off -> tns_lo / tns_hi)
+    std::vector<uint32_t> rec(act.size() * 4);
+    for (size_t x = 0; x < act.size(); x++) {
+      const uint32_t i = act[x], ns = I.ns[i];
+      rec[4 * x] = I.ls[i];
+      rec[4 * x + 1] = pb.tns_lo[d][ns];
+      rec[4 * x + 2] = pb.tns_hi[d][ns];
+      rec[4 * x + 3] = I.list_off[i];
+    }
+    upload(c->actrec[d], rec);
   }
   // selectors the range can reach: its targets' pod selectors and their peers' selectors
   std::vector<uint8_t> sel_needed(pb.S, 0);
@@ -4701,7 +4734,7 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.NB = d == 0 ? K : D;
   // the first kernel below empties the hash table for the next run (keys + reps; not the counter)
   ra.ht_clear = reinterpret_cast<uint32_t*>(dd.ht_key.p);
-  ra.ht_clear_words = uint64_t(dd.ht_cap) * 3;
+  ra.ht_clear_words = uint64_t(dd.ht_cap) * 4;
   ra.rpb = 1;
   return ra;
 }
@@ -5110,6 +5143,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     if (d == 1 && fe.ra[d].udesc) lds_uni = e_per[d] * fe.ra[d].rpb;
     else lds = std::max<size_t>(lds, e_per[d] * fe.ra[d].rpb);
   }
+  // membership ahead of the rest of launch B unless the IP rows alone fill the chip (~2k resident blocks)
+  fb.member_first = uint64_t(fb.nb[0]) + fb.nb[1] < 2048;
   const bool bits = fa.nb[1] && port_bits_on(c);
   const uint32_t nb_bits = bits ? blocks((uint64_t(M) + 255) / 256) : 0u;
   fb.M = M;
