@@ -1033,17 +1033,29 @@ __device__ __forceinline__ void portbits_direct_blk(uint32_t M, uint32_t D, cons
   const uint32_t m = bid_ * 256 + threadIdx.x;
   if (m >= M) return;
   const DPortM pm = pms[m];
-  uint32_t bits = 0;
-  for (uint32_t e = 0; e < D; e++) {
-    const DDesc d = descs[e];
-    bool ok = pm.all != 0;
-    for (uint32_t j = 0; j < pm.ecnt && !ok; j++) {
-      const DPortEntry pe = pents[pm.eoff + j];
-      if (pe.proto != d.proto) continue;  // raw protocol string compare ("tcp" != "TCP")
-      ok = pe.kind == PE_PROTO ? true : pe.kind == PE_INT ? pe.a == d.port : pe.kind == PE_NAME ? uint32_t(pe.a) == d.name
-                                                                          : pe.a <= d.port && d.port <= pe.b;
+  uint32_t bits = pm.all ? (D >= 32 ? ~0u : (1u << D) - 1u) : 0u;
+  // the matcher's entries PB_ENT at a time, all loaded before any test (one memory round trip per
+  // batch, not one per (descriptor, entry)), each tested against every descriptor (block-uniform
+  // loads): launch B config #3 81.4 -> 79.9 us, its N = 8 source shard 33 -> 26.5 us (the port bits
+  // were that shard's longest chain); 4 at a time: the same times at +5 VGPRs for all of launch B
+  // (profiles/r04_front_b_ab.txt)
+  constexpr uint32_t PB_ENT = 2;
+  for (uint32_t j0 = 0; !pm.all && j0 < pm.ecnt; j0 += PB_ENT) {
+    DPortEntry pe[PB_ENT];
+#pragma unroll
+    for (uint32_t x = 0; x < PB_ENT; x++) pe[x] = pents[pm.eoff + min(j0 + x, pm.ecnt - 1)];
+    for (uint32_t e = 0; e < D; e++) {
+      const DDesc d = descs[e];
+      bool ok = false;
+#pragma unroll
+      for (uint32_t x = 0; x < PB_ENT; x++)  // raw protocol string compare ("tcp" != "TCP")
+        ok = ok || (pe[x].proto == d.proto &&
+                    (pe[x].kind == PE_PROTO ? true
+                     : pe[x].kind == PE_INT ? pe[x].a == d.port
+                     : pe[x].kind == PE_NAME ? uint32_t(pe[x].a) == d.name
+                                             : pe[x].a <= d.port && d.port <= pe[x].b));
+      bits |= ok ? 1u << e : 0u;
     }
-    bits |= ok ? 1u << e : 0u;
   }
   portbits[m] = bits;
 }
