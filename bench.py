@@ -171,28 +171,11 @@ def main():
         # (BuildNetworkPolicies + Simplify, from the k8s NetworkPolicy JSON), the probe model through
         # the flat tables a cgo binding passes (cyc_resources_load: no JSON) and cyc_probe_prepare_configs
         # (interning, job expansion, table upload) — paid once per probe model, outside `value`
-        from cyclonus_amd import flat
+        from cyclonus_amd.flat import prepare_flat
 
-        pols_json = json.dumps(data["policies"])
-        t_m = time.perf_counter()
-        res_tables = flat.ResourceTables(data["resources"])  # the binding's marshalling (Python here, Go there)
-        cfgs = flat.ProbeConfigs(data["probes"])
-        marshal_s = time.perf_counter() - t_m
-        t_prep = time.perf_counter()
-        eng.build_policies(pols_json)
-        t_built = time.perf_counter()
-        eng.load_resources_tables(res_tables)
-        t_loaded = time.perf_counter()
-        shape = eng.prepare_configs(cfgs)
+        shape = prepare_flat(eng, data["policies"], data["resources"], data["probes"])
         torch.cuda.synchronize()
-        t_prepared = time.perf_counter()
-        prepare_s = {"policy_build_s": t_built - t_prep, "resources_load_s": t_loaded - t_built,
-                     "probe_prepare_s": t_prepared - t_loaded, "total_s": t_prepared - t_prep,
-                     "path": "cyc_policy_build_json + cyc_resources_load (flat tables) + cyc_probe_prepare_configs",
-                     "tables_marshal_s": marshal_s,
-                     "note": "tables_marshal_s = building the flat tables in Python from the synthetic dicts (a Go "
-                             "binding fills them from its structs); not in total_s"}
-        del res_tables
+        prepare_s = shape.pop("prepare_s")
         P, K, W = shape["pods"], shape["slots"], shape["words"]
         lo, hi = shard_range(P, world, rank, part)
         rows = hi - lo
@@ -268,6 +251,9 @@ def main():
             del out_in, out_eg
         except Exception as e:  # the assembled figure is informational; never lose the bench line
             assembled = {"error": f"{type(e).__name__}: {e}"}
+
+    # the emit as the library launched it in the timed steps (cyc_last_emit: kernel name(s), launches)
+    emit_kernel, launches = eng.last_emit()
 
     # per-kernel device times from HIP events on the launch stream (separate, synchronised runs)
     launch_mode, fused = eng.get_option("launch"), eng.get_option("front_fused_active")
@@ -349,28 +335,15 @@ def main():
     if bt is not None:  # k_emit_blocks: every block's slabs (answered cells' bits) and its status rows
         ri = re_ = P
         wi = we = W
-        launches = 1
         inplace = False
         emit_rows = 2 * P
         emit_bytes = 2 * int(bt.layout[-1][0]) * 8 + int(bt.layout[-1][1])
     else:
-        launches = 1 if (ri, wi) == (re_, we) else 2
         inplace = eng.get_option("class_inplace_active") == 1
         emit_rows = ri + re_ - (classes_in + classes_eg if inplace else 0)
         emit_bytes = (ri - (classes_in if inplace else 0)) * K * wi * 8 + (re_ - (classes_eg if inplace else 0)) * K * we * 8
-    emit_launch_ms = emit_ms  # both launches when there are two (HIP events around the emit phase)
-    achieved = emit_bytes / (emit_launch_ms * 1e-3) / 1e9
-
-    def kernel_of(words):  # the emit kernel the library picks by plane-row length (engine.hip enq_emit_launch)
-        row_bytes = K * words * 8
-        return ("k_emit_words (8-byte copies)" if (K * words) % 2 else
-                "k_emit_wide<1024,7> (a block per row, 7 x 16 B a thread per pass)" if row_bytes > 512 * 7 * 16 else
-                "k_emit_wide<512,7> (a block per row, one pass)" if row_bytes > 256 * 8 * 16 else
-                "k_emit_wide<256,U> (a block per row, one pass)" if row_bytes >= 16384 else
-                "k_emit_flat (multi-row blocks)")
-    emit_kernel = kernel_of(we) if launches == 1 else f"ingress {kernel_of(wi)}; egress {kernel_of(we)}"
-    if bt is not None:
-        emit_kernel = "k_emit_blocks (a workgroup per block: its slabs, bits relative to its first pod)"
+    emit_launch_ms = emit_ms / max(launches, 1)  # HIP events bracket the emit phase (all its launches)
+    achieved = emit_bytes / (emit_ms * 1e-3) / 1e9
 
     # HBM traffic of k_emit from the committed PMC passes for this same workload (rocprofv3
     # --pmc FETCH_SIZE / WRITE_SIZE, corrected per MI355X_MICROARCH.md; scripts/pmc_summary.py)
@@ -437,7 +410,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": emit_bytes,
+                "algorithmic_bytes_per_launch": emit_bytes / max(launches, 1),
+                "algorithmic_bytes_per_step": emit_bytes,
                 "emit_rows_per_launch": emit_rows,
                 "class_rows_in_place": inplace,
                 "emit_ms_per_launch": emit_launch_ms,

@@ -39,6 +39,7 @@ EXPORTS = [
     "cyc_probe_run_host",
     "cyc_last_timings",
     "cyc_last_classes",
+    "cyc_last_emit",
     "cyc_set_option",
     "cyc_get_option",
     "cyc_query_traffic",
@@ -124,6 +125,7 @@ def lib():
         L.cyc_probe_run_host.argtypes = [vp, vp, vp, vp, i64, i64]
         L.cyc_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i]
         L.cyc_last_classes.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), i]
+        L.cyc_last_emit.argtypes = [vp, cp, sz, ctypes.POINTER(i64)]
         L.cyc_set_option.argtypes = [vp, cp, i64]
         L.cyc_get_option.argtypes = [vp, cp, ctypes.POINTER(i64)]
         L.cyc_query_traffic.argtypes = [vp, cp, sz, vp, i64]

@@ -3606,6 +3606,13 @@ struct cyc_ctx {
                         // first (0); -1 = lazy on the fused front of PM builds
   int front_fused = 1;  // "front_fused": the front as block-range-fused launches on one stream
                         // (enq_front_fused), 0 = the two-branch DAG
+  int emit_interleave = -1;  // "emit_interleave": a target-row emit's row list alternates the planes'
+                             // rows (1) or is [plane 0][plane 1] (0); -1 = auto (planes >= 8 GB)
+  int emit_split = 1;   // "emit_split": a target-row emit as this many launches over consecutive parts
+                        // of each plane's row list (1..8)
+  // what the last enqueued emit launched (cyc_last_emit): kernel name(s) and launch count
+  std::string emit_kernel;
+  int emit_launches = 0;
   hipStream_t cap_stream = nullptr, cap_stream2 = nullptr, cap_stream3 = nullptr;  // graph capture branches
   hipEvent_t fork_ev = nullptr, join_ev = nullptr, sel_ev = nullptr, ports_ev = nullptr;
   hipGraphExec_t graph_exec = nullptr;
@@ -4800,7 +4807,7 @@ constexpr uint64_t EMIT_WIDE_MIN = 16384;  // shortest plane row (bytes) emitted
 // k_emit_units over ea.n_rows[] rows of ea.pl_words[] words per plane (16-byte aligned planes, even
 // row words): units of about one 1024 x 7 x 16 B block pass (114 KB) — whole rows of up to that, or
 // several shorter rows — so a block resolves its rows' order -> identity -> class chains together
-static void enq_emit_units(EmitArgs ea, hipStream_t st) {
+static const char* enq_emit_units(EmitArgs ea, hipStream_t st) {
   constexpr uint64_t pass = 1024 * 7 * 16;
   for (int pl = 0; pl < 2; pl++) {
     const uint64_t rb = std::max<uint64_t>(ea.pl_words[pl] * 8, 1);
@@ -4809,17 +4816,18 @@ static void enq_emit_units(EmitArgs ea, hipStream_t st) {
   }
   ea.per_xcd = (ea.n_units[0] + ea.n_units[1] + 7) / 8;
   k_emit_units<1024, 7><<<ea.per_xcd * 8, 1024, 0, st>>>(ea);
+  return "k_emit_units<1024,7>";
 }
 
 
-static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out_in, uint64_t* out_eg) {
+static const char* enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out_in, uint64_t* out_eg) {
   EmitArgs ea = ea_in;
   ea.per_xcd = (ea.n_rows[0] + ea.n_rows[1] + 7) / 8;
   const bool aligned = reinterpret_cast<uintptr_t>(out_in) % 16 == 0 && reinterpret_cast<uintptr_t>(out_eg) % 16 == 0;
   const unsigned g = ea.per_xcd * 8;  // one block per row slot of the 8 XCD segments
   if (ea.row_words % 2 || !aligned) {
     k_emit_words<<<g, 256, 0, st>>>(ea);
-    return;
+    return "k_emit_words";
   }
   const uint64_t row_bytes = ea.row_words * 8;
   // A 512 x 13 one-pass block with flat addresses held 84 VGPRs, 5 waves a SIMD, and ran config #3
@@ -4828,10 +4836,13 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
   // (128 x 13 buffer blocks for config #4's 25 KB rows lost: 442-447 vs 419-424 us.)
   if (row_bytes > 512 * 7 * 16 && row_bytes <= 512 * 13 * 16) {  // 56-104 KB: config #3's 98 KB rows, one pass
     k_emit_wide_buf<512, 13><<<g, 512, 0, st>>>(ea);
+    return "k_emit_wide_buf<512,13>";
   } else if (row_bytes > 512 * 7 * 16) {  // > 104 KB: 1024 x 7 passes
     k_emit_wide<1024, 7><<<g, 1024, 0, st>>>(ea);
+    return "k_emit_wide<1024,7>";
   } else if (row_bytes > 256 * 8 * 16) {  // 32-56 KB: 512 x 7 (source shards at N = 2)
     k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
+    return "k_emit_wide<512,7>";
   } else if (row_bytes >= EMIT_WIDE_MIN) {  // 256-thread single pass (16-32 KB rows)
     const uint64_t need = (ea.row_words / 2 + 255) / 256;
     if (need <= 2) k_emit_wide<256, 2><<<g, 256, 0, st>>>(ea);
@@ -4839,9 +4850,12 @@ static void enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out
     else if (need <= 6) k_emit_wide<256, 6><<<g, 256, 0, st>>>(ea);
     else if (need <= 7) k_emit_wide<256, 7><<<g, 256, 0, st>>>(ea);
     else k_emit_wide<256, 8><<<g, 256, 0, st>>>(ea);
+    return need <= 2 ? "k_emit_wide<256,2>" : need <= 4 ? "k_emit_wide<256,4>" : need <= 6 ? "k_emit_wide<256,6>"
+         : need <= 7 ? "k_emit_wide<256,7>" : "k_emit_wide<256,8>";
   } else {  // flat multi-row sweep over ~32 KB per block
     ea.chunk = uint32_t(std::min<uint64_t>(EMIT_FLAT_MAX_ROWS, std::max<uint64_t>(1, 32768 / row_bytes)));
     k_emit_flat<256, 8><<<(ea.per_xcd + ea.chunk - 1) / ea.chunk * 8, 256, 0, st>>>(ea);
+    return "k_emit_flat<256,8>";
   }
 }
 
@@ -4880,7 +4894,13 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   const uint64_t rw[2] = {uint64_t(K) * c->win_wa, uint64_t(K) * pb.W};  // words per plane row
   uint32_t nr[2];
   for (int d = 0; d < 2; d++) nr[d] = rw[d] ? uint32_t(c->rh[d] - c->rl[d]) : 0u;
-  if (!pb.blocks.empty()) return enq_emit_blocks(c, st, out_in, out_eg, d_status);
+  c->emit_kernel.clear();
+  c->emit_launches = 0;
+  if (!pb.blocks.empty()) {
+    const bool r = enq_emit_blocks(c, st, out_in, out_eg, d_status);
+    if (r && pb.K && d_status) c->emit_kernel = "k_emit_blocks", c->emit_launches = 1;
+    return r;
+  }
   if (!nr[0] && !nr[1]) return false;
   EmitArgs ea{};
   ea.st_src = c->slot_status.as<uint8_t>();
@@ -4900,14 +4920,28 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.out[1] = out_eg;
   ea.pl_words[0] = rw[0];
   ea.pl_words[1] = rw[1];
+  auto note = [&](const char* k) {  // what cyc_last_emit reports
+    if (c->emit_kernel.find(k) == std::string::npos) c->emit_kernel += (c->emit_kernel.empty() ? "" : " + ") + std::string(k);
+    c->emit_launches++;
+  };
   if (rw[0] == rw[1] && nr[0] == nr[1]) {  // target rows: both planes in one launch
-    ea.n_rows[0] = ea.n_rows[1] = nr[0];
     ea.row_words = rw[0];
     // alternate the planes' rows when each plane is >= 8 GB (config #3 on one GPU: emit 3.42 ->
     // 3.11 ms on two of three boxes, -1 % on the third; 1-4 % slower for planes of <= 5 GB — 2, 4
     // and 8 shards — profiles/r01_emit_interleave_sweep.txt)
-    ea.interleave = uint64_t(nr[0]) * rw[0] * 8 >= (8ull << 30) ? 1u : 0u;
-    enq_emit_launch(ea, st, out_in, out_eg);
+    ea.interleave = c->emit_interleave >= 0 ? uint32_t(c->emit_interleave)
+                                            : uint64_t(nr[0]) * rw[0] * 8 >= (8ull << 30) ? 1u : 0u;
+    // emit_split > 1: consecutive parts of both planes' row lists (class-clustered, so nearly address
+    // order) as separate launches, the first carrying the status copy and the span reset
+    const uint32_t parts = uint32_t(std::max(1, std::min<int>(c->emit_split, int(std::max<uint32_t>(nr[0], 1)))));
+    for (uint32_t h = 0; h < parts; h++) {
+      const uint32_t r0 = uint32_t(uint64_t(nr[0]) * h / parts), r1 = uint32_t(uint64_t(nr[0]) * (h + 1) / parts);
+      EmitArgs e1 = ea;
+      e1.n_rows[0] = e1.n_rows[1] = r1 - r0;
+      for (int pl = 0; pl < 2; pl++) e1.order[pl] = ea.order[pl] + r0;
+      if (h) e1.st_bytes = e1.reset_n = 0;
+      note(enq_emit_launch(e1, st, out_in, out_eg));
+    }
     return true;
   }
   // rows of different lengths (a source shard): ONE launch over units of about one block pass each
@@ -4915,7 +4949,7 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   if (aligned && rw[0] % 2 == 0 && rw[1] % 2 == 0) {
     ea.n_rows[0] = nr[0];
     ea.n_rows[1] = nr[1];
-    enq_emit_units(ea, st);
+    note(enq_emit_units(ea, st));
     return true;
   }
   bool first = true;
@@ -4927,7 +4961,7 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
     e1.row_words = rw[pl];
     if (!first) e1.st_bytes = e1.reset_n = 0;
     first = false;
-    enq_emit_launch(e1, st, pl == 0 ? out_in : reinterpret_cast<uint64_t*>(16), pl == 1 ? out_eg : reinterpret_cast<uint64_t*>(16));
+    note(enq_emit_launch(e1, st, pl == 0 ? out_in : reinterpret_cast<uint64_t*>(16), pl == 1 ? out_eg : reinterpret_cast<uint64_t*>(16)));
   }
   return true;
 }
@@ -5643,14 +5677,27 @@ int cyc_policy_load_ir_json(cyc_ctx* c, const char* js, size_t len) {
   });
 }
 
+// The JSON dumps: bytes needed (+1), the text copied when buf holds it all; -(cyc_status) on failure
+// (nothing loaded, or the dump itself failed, e.g. out of memory) with cyc_last_error set.
+static int64_t json_out(cyc_ctx* c, bool have, const char* what, const std::function<std::string()>& dump, char* buf,
+                        size_t cap) {
+  if (!c) return -int64_t(CYC_ERR_ARG);
+  if (!have) return -int64_t(fail(c, CYC_ERR_ARG, std::string("no ") + what + " loaded"));
+  int64_t need = 0;
+  const int rc = guarded(c, [&] {
+    const std::string s = dump();
+    if (buf && cap > s.size()) {
+      memcpy(buf, s.data(), s.size());
+      buf[s.size()] = 0;
+    }
+    need = int64_t(s.size()) + 1;
+    return (int)CYC_OK;
+  });
+  return rc == CYC_OK ? need : -int64_t(rc);
+}
+
 int64_t cyc_policy_ir_json(cyc_ctx* c, char* buf, size_t cap) {
-  if (!c || !c->have_policy) return -1;
-  std::string s = dump_policy_ir(c->policy);
-  if (buf && cap > s.size()) {
-    memcpy(buf, s.data(), s.size());
-    buf[s.size()] = 0;
-  }
-  return int64_t(s.size()) + 1;
+  return json_out(c, c && c->have_policy, "policy", [&] { return dump_policy_ir(c->policy); }, buf, cap);
 }
 
 int cyc_resources_load_json(cyc_ctx* c, const char* js, size_t len) {
@@ -5664,13 +5711,7 @@ int cyc_resources_load_json(cyc_ctx* c, const char* js, size_t len) {
 }
 
 int64_t cyc_resources_json(cyc_ctx* c, char* buf, size_t cap) {
-  if (!c || !c->have_res) return -1;
-  std::string s = dump_resources(c->res);
-  if (buf && cap > s.size()) {
-    memcpy(buf, s.data(), s.size());
-    buf[s.size()] = 0;
-  }
-  return int64_t(s.size()) + 1;
+  return json_out(c, c && c->have_res, "resources", [&] { return dump_resources(c->res); }, buf, cap);
 }
 
 int cyc_resources_load(cyc_ctx* c, const cyc_resource_tables* t) {
@@ -6066,6 +6107,18 @@ int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
   });
 }
 
+int cyc_last_emit(cyc_ctx* c, char* name, size_t cap, int64_t* launches) {
+  if (!c) return CYC_ERR_ARG;
+  if (!c->ran) return fail(c, CYC_ERR_ARG, "no run yet");
+  if (name && cap) {
+    const size_t n = std::min(cap - 1, c->emit_kernel.size());
+    std::memcpy(name, c->emit_kernel.data(), n);
+    name[n] = 0;
+  }
+  if (launches) *launches = c->emit_launches;
+  return CYC_OK;
+}
+
 int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
   if (!c || !name) return CYC_ERR_ARG;
   std::unique_ptr<DeviceGuard> dg;
@@ -6091,6 +6144,8 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "pr_group") range(-1, 64), c->pr_group = int(value == 0 ? -1 : value);
     else if (n == "class_inplace") range(-1, 1), c->class_inplace = int(value);
     else if (n == "step_events") range(0, 1), c->step_events = int(value);
+    else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
+    else if (n == "emit_split") range(1, 8), c->emit_split = int(value);
     else if (n == "plvt_max_mb") {
       range(0, 1 << 20);
       c->plvt_max_mb = value;
@@ -6121,6 +6176,8 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
     *value = inplace_ok(c, reinterpret_cast<const uint64_t*>(16), reinterpret_cast<const uint64_t*>(16)) ? 1 : 0;
   }
   else if (n == "step_events") *value = c->step_events;
+  else if (n == "emit_interleave") *value = c->emit_interleave;
+  else if (n == "emit_split") *value = c->emit_split;
   else if (n == "plvt_max_mb") *value = c->plvt_max_mb;
   else if (n == "plvt_active") *value = c->plvt_ready ? 1 : 0;
   else if (n == "pl_wave_active") {

@@ -748,6 +748,8 @@ PolicyIR load_policy_tables(const cyc_policy_tables& t) {
     }
   } ck;
   // strings
+  constexpr int64_t U32 = int64_t(1) << 32;  // ids, counts and offsets are kept as 32-bit values
+  if (t.str.n >= U32) ck.bad("str.n = " + std::to_string(t.str.n) + ": more than 2^32 - 1 strings");
   ck.offsets(t.str.off, t.str.n, "str.off");
   if (t.str.n && t.str.off[t.str.n] > t.str.off[0]) ck.need(t.str.bytes, "str.bytes");
   auto S = [&](int64_t i, const char* name, int64_t at) {
@@ -972,13 +974,16 @@ Resources load_resources(const Node& n) {
       r.pod_ns.push_back((x = p.sval("Namespace")) ? S(x->str()) : empty);
       r.pod_name.push_back((x = p.sval("Name")) ? S(x->str()) : empty);
       r.pod_ip.push_back((x = p.sval("IP")) ? S(x->str()) : empty);
-      if (auto ls = p.val("Labels"); ls && ls->is_obj())
+      const Node* ls = p.val("Labels");
+      const Node* cs = p.val("Containers");
+      r.pod_nil.push_back(uint8_t((ls && ls->is_obj() ? 0 : 1) | (cs && cs->is_arr() ? 0 : 2)));
+      if (ls && ls->is_obj())
         for (auto& kv : ls->o) {
           r.lab_key.push_back(S(kv.first));
           r.lab_val.push_back(kv.second.null() ? empty : S(kv.second.str()));
         }
       r.pod_lab_off.push_back(uint32_t(r.lab_key.size()));
-      if (auto cs = p.val("Containers"); cs && cs->is_arr())
+      if (cs && cs->is_arr())
         for (auto& c : cs->a) {
           Container ct;
           ct.name = (x = c.sval("Name")) ? S(x->str()) : empty;
@@ -995,7 +1000,7 @@ Resources load_resources(const Node& n) {
 
 // json.Marshal(*probe.Resources) of the fields the verdict path reads (Pod.ServiceIP and
 // Container.BatchJobs are not kept); map keys sorted as encoding/json writes them, a label map with
-// a repeated key as Go would hold it (last value).  Nil and empty label maps are one value here.
+// a repeated key as Go would hold it (last value); nil maps and slices as null.
 std::string dump_resources(const Resources& r) {
   auto labels = [&](const std::vector<uint32_t>& key, const std::vector<uint32_t>& val, uint32_t lo, uint32_t hi) {
     std::map<std::string, std::string> m;
@@ -1015,9 +1020,15 @@ std::string dump_resources(const Resources& r) {
   }
   o += "},\"Pods\":[";
   for (size_t p = 0; p < r.pods(); p++) {
+    const uint8_t nil = p < r.pod_nil.size() ? r.pod_nil[p] : 0;
     o += (p ? "," : "") + std::string("{\"Namespace\":") + quote(r.s(r.pod_ns[p])) + ",\"Name\":" + quote(r.s(r.pod_name[p])) +
-         ",\"Labels\":" + labels(r.lab_key, r.lab_val, r.pod_lab_off[p], r.pod_lab_off[p + 1]) + ",\"IP\":" + quote(r.s(r.pod_ip[p])) +
-         ",\"Containers\":[";
+         ",\"Labels\":" + (nil & 1 ? std::string("null") : labels(r.lab_key, r.lab_val, r.pod_lab_off[p], r.pod_lab_off[p + 1])) +
+         ",\"IP\":" + quote(r.s(r.pod_ip[p])) + ",\"Containers\":";
+    if (nil & 2) {
+      o += "null}";
+      continue;
+    }
+    o += "[";
     for (uint32_t i = 0; i < r.n_conts(p); i++) {
       const Container& c = r.cont(p, i);
       o += (i ? "," : "") + std::string("{\"Name\":") + quote(r.s(c.name)) + ",\"Port\":" + std::to_string(c.port) +
@@ -1058,6 +1069,8 @@ Resources load_resources_tables(const cyc_resource_tables& t) {
   Resources r;
   // the caller's string table may repeat a string: every index maps to one canonical entry, so equal
   // ids <=> equal strings (Resources' invariant, which the name groups of the table build rely on)
+  constexpr int64_t U32 = int64_t(1) << 32;  // ids, counts and offsets are kept as 32-bit values
+  if (t.str.n >= U32) ck.bad("str.n = " + std::to_string(t.str.n) + ": more than 2^32 - 1 strings");
   ck.offsets(t.str.off, t.str.n, "str.off");
   if (t.str.n && t.str.off[t.str.n] > t.str.off[0]) ck.need(t.str.bytes, "str.bytes");
   std::vector<uint32_t> canon(size_t(t.str.n));
@@ -1072,9 +1085,12 @@ Resources load_resources_tables(const cyc_resource_tables& t) {
   const int64_t n_str = t.str.n;
   auto id = [&](int64_t v, const char* name, int64_t at) { return canon[ck.index(v, n_str, name, at)]; };
   if (t.n_namespaces < 0 || t.n_pods < 0) ck.bad("negative count");
+  if (t.n_namespaces >= U32) ck.bad("n_namespaces = " + std::to_string(t.n_namespaces) + ": more than 2^32 - 1 namespaces");
+  if (t.n_pods >= U32) ck.bad("n_pods = " + std::to_string(t.n_pods) + ": more than 2^32 - 1 pods");
   if (t.n_namespaces) {
     ck.need(t.ns_name, "ns_name");
     const int64_t nl = ck.offsets(t.ns_label_off, t.n_namespaces, "ns_label_off");
+    if (nl - t.ns_label_off[0] >= U32) ck.bad("more than 2^32 - 1 namespace labels");
     if (nl) {
       ck.need(t.ns_label_key, "ns_label_key");
       ck.need(t.ns_label_val, "ns_label_val");
@@ -1112,18 +1128,24 @@ Resources load_resources_tables(const cyc_resource_tables& t) {
       ck.need(t.cont_proto, "cont_proto");
       ck.need(t.cont_port_name, "cont_port_name");
     }
-    if (nl - l0 >= (int64_t(1) << 32) || nc - c0 >= (int64_t(1) << 32)) ck.bad("more than 2^32 labels or containers");
+    if (nl - l0 >= U32 || nc - c0 >= U32) ck.bad("more than 2^32 - 1 labels or containers");
     r.pod_ns.resize(size_t(P));
     r.pod_name.resize(size_t(P));
     r.pod_ip.resize(size_t(P));
     r.pod_lab_off.assign(size_t(P) + 1, 0);
     r.pod_cont_off.assign(size_t(P) + 1, 0);
+    r.pod_nil.assign(size_t(P), 0);
     for (int64_t p = 0; p < P; p++) {
       r.pod_ns[size_t(p)] = id(t.pod_ns[p], "pod_ns", p);
       r.pod_name[size_t(p)] = id(t.pod_name[p], "pod_name", p);
       r.pod_ip[size_t(p)] = id(t.pod_ip[p], "pod_ip", p);
       r.pod_lab_off[size_t(p) + 1] = uint32_t(t.pod_label_off[p + 1] - l0);
       r.pod_cont_off[size_t(p) + 1] = uint32_t(t.pod_cont_off[p + 1] - c0);
+      if (t.pod_nil) {  // a nil map / slice holds nothing
+        r.pod_nil[size_t(p)] = t.pod_nil[p] & 3;
+        if ((t.pod_nil[p] & 1) && t.pod_label_off[p + 1] > t.pod_label_off[p]) ck.bad("pod_nil[" + std::to_string(p) + "]: nil Labels with labels");
+        if ((t.pod_nil[p] & 2) && t.pod_cont_off[p + 1] > t.pod_cont_off[p]) ck.bad("pod_nil[" + std::to_string(p) + "]: nil Containers with containers");
+      }
     }
     r.lab_key.resize(size_t(nl - l0));
     r.lab_val.resize(size_t(nl - l0));
@@ -1169,10 +1191,15 @@ std::vector<ProbeConfig> load_probe_configs(const cyc_probe_config* cfgs, int64_
     ProbeConfig& c = out[size_t(i)];
     c.all_available = cfgs[i].all_available != 0;
     if (c.all_available) continue;
+    auto str = [&](const char* p, int64_t n, const char* name) {
+      if (n < 0 || (n && !p))
+        throw Panic{CYC_ERR_ARG, "cyc_probe_config[" + std::to_string(i) + "]." + name + ": null pointer or negative length"};
+      return std::string(p ? p : "", size_t(n));
+    };
     c.port.is_str = cfgs[i].port_is_name != 0;
-    if (c.port.is_str) c.port.s = cfgs[i].port_name ? cfgs[i].port_name : "";
+    if (c.port.is_str) c.port.s = str(cfgs[i].port_name, cfgs[i].port_name_len, "port_name");
     else c.port.i = cfgs[i].port;
-    c.proto = cfgs[i].protocol ? cfgs[i].protocol : "";
+    c.proto = str(cfgs[i].protocol, cfgs[i].protocol_len, "protocol");
   }
   return out;
 }

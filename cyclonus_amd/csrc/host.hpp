@@ -156,6 +156,7 @@ struct Resources {
   std::vector<uint32_t> pod_lab_off{0}, lab_key, lab_val;  // a Go map: duplicate keys, if given, last wins
   std::vector<uint32_t> pod_cont_off{0};
   std::vector<Container> conts;
+  std::vector<uint8_t> pod_nil;  // per pod: bit 0 Labels == nil, bit 1 Containers == nil (json.Marshal: null)
   size_t pods() const { return pod_ns.size(); }
   uint32_t n_conts(size_t p) const { return pod_cont_off[p + 1] - pod_cont_off[p]; }
   const Container& cont(size_t p, uint32_t i) const { return conts[pod_cont_off[p] + i]; }

@@ -52,13 +52,19 @@ class Engine:
         check(self._ctx, lib().cyc_policy_load_ir_json(self._ctx, b, len(b)))
         return self
 
-    def policy_ir(self) -> dict:
-        n = lib().cyc_policy_ir_json(self._ctx, None, 0)
+    def _dump(self, fn) -> dict:
+        """A JSON dump entry point (bytes needed, or -(cyc_status) with cyc_last_error set)."""
+        n = fn(self._ctx, None, 0)
         if n < 0:
-            raise _lib.CyclonusError(_lib.ERR_ARG, "no policy loaded")
+            check(self._ctx, int(-n))
         buf = ctypes.create_string_buffer(int(n))
-        lib().cyc_policy_ir_json(self._ctx, buf, int(n))
+        m = fn(self._ctx, buf, int(n))
+        if m < 0:
+            check(self._ctx, int(-m))
         return json.loads(buf.value.decode())
+
+    def policy_ir(self) -> dict:
+        return self._dump(lib().cyc_policy_ir_json)
 
     def load_resources(self, resources) -> "Engine":
         b = _bytes(resources)
@@ -94,12 +100,7 @@ class Engine:
 
     def resources_json(self) -> dict:
         """The loaded probe model (cyc_resources_json: json.Marshal(*probe.Resources) of the kept fields)."""
-        n = lib().cyc_resources_json(self._ctx, None, 0)
-        if n < 0:
-            raise _lib.CyclonusError(_lib.ERR_ARG, "no resources loaded")
-        buf = ctypes.create_string_buffer(int(n))
-        lib().cyc_resources_json(self._ctx, buf, int(n))
-        return json.loads(buf.value.decode())
+        return self._dump(lib().cyc_resources_json)
 
     def prepare(self, probes) -> dict:
         b = _bytes(probes)
@@ -224,6 +225,13 @@ class Engine:
         out = (ctypes.c_int64 * 2)()
         check(self._ctx, lib().cyc_last_classes(self._ctx, out, 2))
         return int(out[0]), int(out[1])
+
+    def last_emit(self):
+        """(kernel name(s), launch count) of the last run's emit, as the library launched it."""
+        buf = ctypes.create_string_buffer(256)
+        n = ctypes.c_int64(0)
+        check(self._ctx, lib().cyc_last_emit(self._ctx, buf, 256, ctypes.byref(n)))
+        return buf.value.decode(), int(n.value)
 
     def set_option(self, name: str, value: int):
         check(self._ctx, lib().cyc_set_option(self._ctx, name.encode(), int(value)))

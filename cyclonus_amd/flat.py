@@ -28,12 +28,13 @@ class ResourceTablesC(ctypes.Structure):
                 ("ns_label_off", i64p), ("ns_label_key", i32p), ("ns_label_val", i32p), ("n_pods", ctypes.c_int64),
                 ("pod_ns", i32p), ("pod_name", i32p), ("pod_ip", i32p), ("pod_label_off", i64p), ("label_key", i32p),
                 ("label_val", i32p), ("pod_cont_off", i64p), ("cont_name", i32p), ("cont_port", i32p),
-                ("cont_proto", i32p), ("cont_port_name", i32p)]
+                ("cont_proto", i32p), ("cont_port_name", i32p), ("pod_nil", u8p)]
 
 
 class ProbeConfigC(ctypes.Structure):
     _fields_ = [("all_available", ctypes.c_int32), ("port_is_name", ctypes.c_int32), ("port", ctypes.c_int32),
-                ("port_name", ctypes.c_char_p), ("protocol", ctypes.c_char_p)]
+                ("port_name", ctypes.c_char_p), ("port_name_len", ctypes.c_int64),
+                ("protocol", ctypes.c_char_p), ("protocol_len", ctypes.c_int64)]
 
 
 class PolicyTablesC(ctypes.Structure):
@@ -103,11 +104,12 @@ class ResourceTables:
             ns_k += [S(k) for k in labels]
             ns_v += [S(v) for v in labels.values()]
         pods = resources.get("Pods") or []
-        pns, pname, pip, lcnt, lk, lv, ccnt, cn, cp, cpr, cpn = ([] for _ in range(11))
+        pns, pname, pip, lcnt, lk, lv, ccnt, cn, cp, cpr, cpn, pnil = ([] for _ in range(12))
         for p in pods:
             pns.append(S(p.get("Namespace")))
             pname.append(S(p.get("Name")))
             pip.append(S(p.get("IP")))
+            pnil.append((1 if p.get("Labels") is None else 0) | (2 if p.get("Containers") is None else 0))
             labels = p.get("Labels") or {}
             lcnt.append(len(labels))
             lk += [S(k) for k in labels]
@@ -139,6 +141,7 @@ class ResourceTables:
         t.cont_port = _arr(keep, cp, np.int32, i32p)
         t.cont_proto = _arr(keep, cpr, np.int32, i32p)
         t.cont_port_name = _arr(keep, cpn, np.int32, i32p)
+        t.pod_nil = _arr(keep, pnil, np.uint8, u8p)
         self.c, self._keep = t, keep
 
 
@@ -159,11 +162,11 @@ class ProbeConfigs:
             pp = p.get("PortProtocol") or p
             port, proto = pp.get("Port"), (pp.get("Protocol") or "").encode()
             self._keep.append(proto)
-            self.c[i].protocol = proto
+            self.c[i].protocol, self.c[i].protocol_len = proto, len(proto)
             if isinstance(port, str):
                 b = port.encode()
                 self._keep.append(b)
-                self.c[i].port_is_name, self.c[i].port_name = 1, b
+                self.c[i].port_is_name, self.c[i].port_name, self.c[i].port_name_len = 1, b, len(b)
             else:
                 self.c[i].port = int(port or 0)
 
@@ -340,3 +343,35 @@ def dump_probe_configs(probes, path):
                 f.write(f"name {c.port_name.decode()} {proto}\n")
             else:
                 f.write(f"int {c.port} {proto}\n")
+
+
+def prepare_flat(eng, policies, resources, probes) -> dict:
+    """The drop-in's host path as bench.py times it (analyze --mode probe, pkg/cli/analyze.go:121,
+    232-243): BuildNetworkPolicies + Simplify from the NetworkPolicy JSON (cyc_policy_build_json),
+    the probe model through the flat tables a cgo binding passes (cyc_resources_load, no JSON) and
+    cyc_probe_prepare_configs.  Returns the probe shape plus a "prepare_s" dict of the phase times
+    (tables_marshal_s = building the flat tables in Python from the dicts, which a Go binding does from
+    its structs; not in total_s)."""
+    import json
+    import time
+
+    pols_json = json.dumps(policies)
+    t_m = time.perf_counter()
+    res_tables = ResourceTables(resources)
+    cfgs = ProbeConfigs(probes)
+    marshal_s = time.perf_counter() - t_m
+    t0 = time.perf_counter()
+    eng.build_policies(pols_json)
+    t_built = time.perf_counter()
+    eng.load_resources_tables(res_tables)
+    t_loaded = time.perf_counter()
+    shape = eng.prepare_configs(cfgs)
+    t_prepared = time.perf_counter()
+    shape = dict(shape)
+    shape["prepare_s"] = {"policy_build_s": t_built - t0, "resources_load_s": t_loaded - t_built,
+                          "probe_prepare_s": t_prepared - t_loaded, "total_s": t_prepared - t0,
+                          "path": "cyc_policy_build_json + cyc_resources_load (flat tables) + cyc_probe_prepare_configs",
+                          "tables_marshal_s": marshal_s,
+                          "note": "tables_marshal_s = building the flat tables in Python from the synthetic dicts (a Go "
+                                  "binding fills them from its structs); not in total_s"}
+    return shape

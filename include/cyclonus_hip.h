@@ -91,7 +91,9 @@ const char* cyc_version(void);
 int cyc_policy_build_json(cyc_ctx* ctx, int simplify, const char* netpols_json, size_t len);
 /* policy load: json.Marshal(*matcher.Policy) produced by the Go reference */
 int cyc_policy_load_ir_json(cyc_ctx* ctx, const char* policy_json, size_t len);
-/* export the compiled policy as json.Marshal(*matcher.Policy) would; returns bytes needed (+1) */
+/* export the compiled policy as json.Marshal(*matcher.Policy) would; returns bytes needed (+1) and
+ * writes the NUL-terminated text when cap holds it (a smaller cap writes nothing); returns
+ * -(cyc_status) on failure (no policy loaded, or the dump failed) with cyc_last_error set */
 int64_t cyc_policy_ir_json(cyc_ctx* ctx, char* buf, size_t cap);
 
 /* probe model: probe.Resources JSON ({"Namespaces": {...}, "Pods": [...]}) */
@@ -128,6 +130,8 @@ typedef struct {
   const int32_t *label_key, *label_val;
   const int64_t* pod_cont_off;   /* [n_pods + 1] into the container arrays (Containers) */
   const int32_t *cont_name, *cont_port, *cont_proto, *cont_port_name;  /* Name, Port, Protocol, PortName */
+  const uint8_t* pod_nil;        /* [n_pods] optional: bit 0 Labels == nil, bit 1 Containers == nil
+                                    (json.Marshal fidelity only: cyc_resources_json writes null) */
 } cyc_resource_tables;
 
 /* generator.ProbeConfig (pkg/generator/probeconfig.go): AllAvailable, or PortProtocol{Port intstr, Protocol} */
@@ -135,8 +139,11 @@ typedef struct {
   int32_t all_available;  /* 1: one job per destination container (resources.go:336-364) */
   int32_t port_is_name;   /* intstr.Type: 0 Int (port), 1 String (port_name) */
   int32_t port;
-  const char* port_name;  /* NUL-terminated; NULL = "" */
-  const char* protocol;   /* NUL-terminated raw protocol string (compared as is: "tcp" != "TCP"); NULL = "" */
+  /* Go strings as (pointer, byte length): any bytes, NUL included; NULL with length 0 = "" */
+  const char* port_name;  /* the named port */
+  int64_t port_name_len;
+  const char* protocol;   /* the raw protocol string (compared as is: "tcp" != "TCP") */
+  int64_t protocol_len;
 } cyc_probe_config;
 
 /* *matcher.Policy after BuildNetworkPolicies (+ Simplify) (pkg/matcher/policy.go:11-14,
@@ -193,7 +200,9 @@ int cyc_resources_load(cyc_ctx* ctx, const cyc_resource_tables* tables);
 int cyc_policy_load(cyc_ctx* ctx, const cyc_policy_tables* tables);
 int cyc_probe_prepare_configs(cyc_ctx* ctx, const cyc_probe_config* configs, int64_t n, cyc_probe_shape* shape);
 /* the loaded probe model as json.Marshal(*probe.Resources) would write it (Pod.ServiceIP and
- * Container.BatchJobs are not kept); returns bytes needed (+1), as cyc_policy_ir_json */
+ * Container.BatchJobs are not kept; nil label maps and container slices as null: from JSON input an
+ * absent or null field, from flat tables ns_nil / pod_nil); returns bytes needed (+1) or
+ * -(cyc_status), as cyc_policy_ir_json */
 int64_t cyc_resources_json(cyc_ctx* ctx, char* buf, size_t cap);
 
 /* Compute the verdict planes on the GPU for target-pod rows [row_lo, row_hi) (rows are pods in
@@ -313,6 +322,12 @@ int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
  * [1] egress (synchronises the device). */
 int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
 
+/* What the last enqueued run's emit launched: the kernel name(s) ("k_emit_wide_buf<512,13>",
+ * "k_emit_units<1024,7>", ...; several joined by " + ") into name (NUL-terminated, truncated to
+ * cap - 1 bytes) and the number of emit launches into *launches (either may be null).  Set when the
+ * run is enqueued (a captured graph replays what its capture recorded); CYC_ERR_ARG before any run. */
+int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
+
 /* Diagnostic path selectors (results never change; the GPU tests force every path):
  *   "graphs"      -1 (default: auto = 2 when the fused front applies, else 1); 1 replays the step as
  *                 one captured hipGraph when the inputs cannot panic (then cyc_last_timings reports
@@ -344,6 +359,10 @@ int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
  *                 membership and pod-peer rows / identity sets use them (1) instead of as the dense
  *                 selector x label-set table first (0); auto = 1 for identity-set builds and once
  *                 that table has >= 64M pairs
+ *   "emit_interleave" -1 (default: auto = 1 when a plane of a target-row run is >= 8 GB) / 0 / 1: the
+ *                 emit's row list alternates ingress and egress rows (1) or holds all ingress rows first
+ *   "emit_split"  1 (default) .. 8: a target-row run's emit as that many launches over consecutive
+ *                 parts of the planes' row lists
  * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
  * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
  * uses (0 or 1). */

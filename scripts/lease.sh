@@ -11,10 +11,12 @@
 #   scale CFG                  scripts/partition_scaling.py (one-GPU shard timings, both partitions)
 #   tl CFG [N]                 kernel timeline of back-to-back steps (scripts/graph_timeline.py)
 #   py SCRIPT [args]           any python script under scripts/ (180 s limit)
+#   counters                   rocprofv3 -L (the counters this box's gfx950 offers)
 #   bin PROBE [args]           a probe built from scripts/*.hip (scripts/PROBE, 180 s limit)
 #   dist N CFG [args]          bench.py as an N-rank torch.distributed.run job on this box (tokens:
 #                              CYC_BENCH_BACKEND=gloo for a one-GPU rehearsal, CYC_BENCH_FORCE_DIST=1)
 #   ab CFG SPEC...             kernel stats per library variant (scripts/ab_kernels.sh; REPS env, CYC_SHARD tokens)
+#   pmcab VARIANT...           emit PMC passes per scripts/emit_halves_ab.py variant (scripts/pmc_emit_ab.sh)
 #   pmc CFG [NAME=V ...]       per-kernel SQ instruction / wait mix, TCC hits, FETCH / WRITE passes (scripts/pmc_passes.sh)
 # Invocations are recorded in scripts/LEASES.md.
 set -e
@@ -55,6 +57,7 @@ for spec in "$@"; do
       prof_env
       timeout -k 10 120 rocprofv3 --kernel-trace -d $OUT/tl_$tag -o run -- python3 scripts/graph_timeline.py run "$@" > $OUT/tl_$tag.log 2>&1 ;;
     py) timeout -k 10 180 python -u scripts/"$@" > $OUT/py_$tag.log 2>&1 ;;
+    counters) prof_env; timeout -k 10 60 rocprofv3 -L > $OUT/counters.txt 2>&1 ;;
     bin) timeout -k 10 180 ./scripts/"$@" > $OUT/bin_$tag.log 2>&1 ;;
     dist)
       NP=$1; CFG=$2; shift 2
@@ -62,6 +65,7 @@ for spec in "$@"; do
         --master-port $((29500 + RANDOM % 400)) bench.py --gpus $NP --config $CFG "$@" > $OUT/dist_$tag.log 2>&1 ;;
     ab) timeout -k 10 900 bash scripts/ab_kernels.sh $NAME "$@" ;;
     pmc) timeout -k 10 700 bash scripts/pmc_passes.sh $NAME "$@" ;;
+    pmcab) timeout -k 10 900 bash scripts/pmc_emit_ab.sh $NAME "$@" ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
   for e in "${envs[@]}"; do unset "${e%%=*}"; done

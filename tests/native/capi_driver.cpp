@@ -117,6 +117,7 @@ static cyc_resource_tables resource_tables(const Dump& d) {
   I32(t, d, cont_port);
   I32(t, d, cont_proto);
   I32(t, d, cont_port_name);
+  U8(t, d, pod_nil);
   return t;
 }
 
@@ -189,10 +190,12 @@ struct Configs {
         c[i].all_available = 1;
         continue;
       }
-      c[i].protocol = protos[i].c_str();
+      c[i].protocol = protos[i].data();
+      c[i].protocol_len = int64_t(protos[i].size());
       if (kinds[i] == "name") {
         c[i].port_is_name = 1;
-        c[i].port_name = names[i].c_str();
+        c[i].port_name = names[i].data();
+        c[i].port_name_len = int64_t(names[i].size());
       } else {
         c[i].port = int32_t(std::stol(ports[i]));
       }

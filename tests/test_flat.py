@@ -39,6 +39,32 @@ def test_resources_tables_equal_json_config1_and_edges():
     a, b = _both(edge)
     assert a == b
     assert a["Namespaces"]["x"] is None and a["Pods"][1]["Name"] == "é\u0000b"
+    # nil label maps and container slices marshal as null (json.Marshal), empty ones as {} / []
+    assert a["Pods"][0]["Labels"] is None and a["Pods"][0]["Containers"] is None
+    edge["Pods"][0].update(Labels={}, Containers=[])
+    del edge["Pods"][1]["Labels"]
+    a, b = _both(edge)
+    assert a == b and a["Pods"][0]["Labels"] == {} and a["Pods"][0]["Containers"] == []
+    assert a["Pods"][1]["Labels"] is None  # an absent field decodes as nil
+
+
+def test_json_dumps_report_errors():
+    """cyc_resources_json / cyc_policy_ir_json: -(cyc_status) with a message when nothing is loaded; a
+    buffer smaller than the text gets nothing written (run under ASan by test_sanitized)."""
+    e = Engine(0)
+    with pytest.raises(_lib.CyclonusError, match="no resources loaded"):
+        e.resources_json()
+    with pytest.raises(_lib.CyclonusError, match="no policy loaded"):
+        e.policy_ir()
+    assert _lib.lib().cyc_resources_json(e._ctx, None, 0) == -_lib.ERR_ARG
+    e.load_resources(json.load(open(os.path.join(ROOT, "tests", "golden", "config1.json")))["resources"])
+    need = _lib.lib().cyc_resources_json(e._ctx, None, 0)
+    assert need > 1
+    small = ctypes.create_string_buffer(b"\x7f" * 16, 16)
+    assert _lib.lib().cyc_resources_json(e._ctx, small, 16) == need
+    assert small.raw == b"\x7f" * 16
+    full = ctypes.create_string_buffer(int(need))
+    assert _lib.lib().cyc_resources_json(e._ctx, full, int(need)) == need and full.raw[need - 1] == 0
 
 
 def test_policy_tables_roundtrip():
@@ -56,10 +82,15 @@ def test_probe_configs():
     pc = flat.ProbeConfigs([{"Port": 80, "Protocol": "TCP"}, {"Port": "serve-81-udp", "Protocol": "UDP"},
                             {"AllAvailable": True}, {"PortProtocol": {"Port": 53, "Protocol": "sctp"}}])
     assert pc.n == 4
-    assert (pc.c[0].port, pc.c[0].port_is_name, pc.c[0].protocol) == (80, 0, b"TCP")
-    assert (pc.c[1].port_is_name, pc.c[1].port_name) == (1, b"serve-81-udp")
+    assert (pc.c[0].port, pc.c[0].port_is_name, pc.c[0].protocol, pc.c[0].protocol_len) == (80, 0, b"TCP", 3)
+    assert (pc.c[1].port_is_name, pc.c[1].port_name, pc.c[1].port_name_len) == (1, b"serve-81-udp", 12)
     assert pc.c[2].all_available == 1
     assert (pc.c[3].port, pc.c[3].protocol) == (53, b"sctp")
+    # Go strings may hold NUL bytes: they travel as pointer + length, not as C strings
+    pc = flat.ProbeConfigs([{"Port": "a\u0000b", "Protocol": "T\u0000CP"}])
+    assert pc.c[0].port_name_len == 3 and pc.c[0].protocol_len == 4
+    addr = ctypes.c_void_p.from_buffer(pc.c[0], flat.ProbeConfigC.protocol.offset).value
+    assert ctypes.string_at(addr, 4) == b"T\x00CP"
 
 
 def test_malformed_tables_refused():
@@ -80,6 +111,20 @@ def test_malformed_tables_refused():
     assert rc == _lib.ERR_ARG and "decreases" in msg
     rc, msg = load(lambda c: setattr(c, "pod_ns", None))
     assert rc == _lib.ERR_ARG and "null pod_ns" in msg
+    # counts kept as 32-bit values are refused at 2^32, not truncated
+    rc, msg = load(lambda c: setattr(c, "n_pods", 1 << 32))
+    assert rc == _lib.ERR_ARG and "n_pods" in msg and "2^32" in msg
+    rc, msg = load(lambda c: setattr(c, "n_namespaces", 1 << 32))
+    assert rc == _lib.ERR_ARG and "n_namespaces" in msg
+    rc, msg = load(lambda c: setattr(c.str, "n", 1 << 32))
+    assert rc == _lib.ERR_ARG and "str.n" in msg
+    big = np.array([0, 1 << 32], np.int64)
+    rc, msg = load(lambda c: setattr(c, "ns_label_off", big.ctypes.data_as(flat.i64p)))
+    assert rc == _lib.ERR_ARG and "namespace labels" in msg
+    # a nil map or slice holds nothing
+    nil = np.array([1], np.uint8)
+    rc, msg = load(lambda c: setattr(c, "pod_nil", nil.ctypes.data_as(flat.u8p)))
+    assert rc == _lib.ERR_ARG and "nil Labels" in msg
     # a refused load leaves the earlier model in place
     e.load_resources(res)
     rc, _ = load(lambda c: setattr(c, "pod_ip", bad.ctypes.data_as(flat.i32p)))

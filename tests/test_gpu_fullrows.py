@@ -3,7 +3,10 @@ source, every slot) and egress rows (one source, every destination, every slot) 
 table equal the oracle's rows bit for bit — rows from the first / last positions, 64-pod word
 edges, the most populous identities (largest classes) and random positions, on the whole table, on
 target-row shards (row_lo > 0) and on source-row shards (the shard's egress rows, and its word slice
-of every picked destination's ingress row)."""
+of every picked destination's ingress row).  Every check runs through both ingestion paths: the JSON
+entry points and the flat tables bench.py times (flat.prepare_flat: cyc_policy_build_json +
+cyc_resources_load + cyc_probe_prepare_configs); test_config3_flat_planes_equal_json compares the two
+paths' whole planes at config #3's full size."""
 import json
 from collections import Counter
 
@@ -12,6 +15,7 @@ import pytest
 
 from cyclonus_amd import synth
 from cyclonus_amd.engine import Engine
+from cyclonus_amd.flat import prepare_flat
 from cyclonus_amd.shard import row_range, source_range
 from oracle.oracle import Oracle
 
@@ -32,12 +36,23 @@ def _pick_rows(res, lo, hi, n_random, seed):
     return sorted(lo + r for r in rows if 0 <= r < len(pods))
 
 
-def _check(name, kw, shards, source_shards=()):
+INGEST = pytest.mark.parametrize("ingest", ["json", "flat"])
+
+
+def _prepared(data, ingest):
+    """An engine prepared through the JSON entry points or through bench.py's flat path."""
+    if ingest == "flat":
+        eng = Engine(0)
+        return eng, prepare_flat(eng, data["policies"], data["resources"], data["probes"])
+    eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
+    return eng, eng.prepare(data["probes"])
+
+
+def _check(name, kw, shards, source_shards=(), ingest="json"):
     import torch
 
     data = synth.CONFIGS[name](**kw)
-    eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
-    sh = eng.prepare(data["probes"])
+    eng, sh = _prepared(data, ingest)
     P, K, W = sh["pods"], sh["slots"], sh["words"]
     orc = Oracle(data["policies"], data["resources"])
     for world, rank in source_shards:
@@ -49,6 +64,7 @@ def _check(name, kw, shards, source_shards=()):
         eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), torch.cuda.current_stream().cuda_stream, lo, hi,
                        "source")
         torch.cuda.synchronize()
+        assert eng.last_emit() == ("k_emit_units<1024,7>", 1), eng.last_emit()  # one launch over both planes
         dsts = _pick_rows(data["resources"], 0, P, 6, seed=world * 1000 + rank)  # any destination
         srcs = _pick_rows(data["resources"], lo, hi, 4, seed=world * 1000 + rank + 1)  # the shard's sources
         g_in = d_in[torch.as_tensor(dsts, device="cuda")].cpu().numpy().view(np.uint64)
@@ -90,18 +106,48 @@ def _check(name, kw, shards, source_shards=()):
                                            f"{bad.size} words differ, first at word {int(bad[0])}")
 
 
-def test_config2_full_rows():
+@INGEST
+def test_config2_full_rows(ingest):
     """Config #2 (per-pod PM rows, in-place class rows, the flat emit): whole table, a target shard
     and a source shard."""
-    _check("config2", {}, [(1, 0), (4, 2)], [(8, 5)])
+    _check("config2", {}, [(1, 0), (4, 2)], [(8, 5)], ingest)
 
 
-def test_config3_full_rows():
-    _check("config3", {}, [(1, 0), (8, 3)], [(8, 3)])
+@INGEST
+def test_config3_full_rows(ingest):
+    _check("config3", {}, [(1, 0), (8, 3)], [(8, 3)], ingest)
 
 
-def test_config4_full_rows():
-    _check("config4", {}, [(1, 0), (4, 3)], [(4, 1)])
+@INGEST
+def test_config4_full_rows(ingest):
+    _check("config4", {}, [(1, 0), (4, 3)], [(4, 1)], ingest)
+
+
+def test_config3_flat_planes_equal_json():
+    """The headline's exact preparation (bench.py: flat tables) and the JSON one give byte-identical
+    whole planes and status plane at config #3's full size (2 x 10 GB per path), the same shape and
+    classes, and the emit the bench line names (cyc_last_emit)."""
+    import torch
+
+    data = synth.CONFIGS["config3"]()
+    outs, shapes, emits = [], [], []
+    for ingest in ("flat", "json"):
+        eng, sh = _prepared(data, ingest)
+        sh = {k: v for k, v in sh.items() if k != "prepare_s"}
+        P, K, W = sh["pods"], sh["slots"], sh["words"]
+        d_in = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
+        d_eg = torch.empty((P, K, W), dtype=torch.int64, device="cuda")
+        d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
+        eng.run_device(d_in.data_ptr(), d_eg.data_ptr(), d_st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append((d_in, d_eg, d_st))
+        shapes.append((sh, eng.classes()))
+        emits.append(eng.last_emit())
+        eng.close()
+    assert shapes[0] == shapes[1]
+    for plane, a, b in zip(("ingress", "egress", "status"), outs[0], outs[1]):
+        assert torch.equal(a, b), f"config #3 {plane} plane: flat-prepared != JSON-prepared"
+    assert emits[0] == emits[1] == ("k_emit_wide_buf<512,13>", 1), emits
 
 
 def test_config3u_full_rows():

@@ -711,10 +711,14 @@ def test_launch_modes_and_knobs(gpu):
     assert eng.get_option("launch") == (2 if fused else 1)
     for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("class_rpb", 16), ("class_rpb", 0), ("graphs", 1), ("graphs", -1),
                     ("step_events", 1), ("step_events", 0), ("pr_group", 5), ("pr_group", -1), ("sel_lazy", 1),
-                    ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1)):
+                    ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1),
+                    ("emit_interleave", 1), ("emit_split", 3), ("emit_interleave", 0), ("emit_split", 2),
+                    ("emit_interleave", -1), ("emit_split", 1)):
         eng.set_option(name, v)
         assert eng.get_option(name) == v
         assert_same(want, eng.run_host(), f"{name}={v}")
+        if name == "emit_split":  # cyc_last_emit reports the launches the run made
+            assert eng.last_emit()[1] == v, eng.last_emit()
     # whole-step timing events: off by default for graph / fused-eager runs, always for eager runs
     with pytest.raises(Exception):
         eng.timings()
@@ -732,6 +736,7 @@ def test_launch_modes_and_knobs(gpu):
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
     for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_range", 2), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
+                    ("emit_split", 0), ("emit_split", 9), ("emit_interleave", 2),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
