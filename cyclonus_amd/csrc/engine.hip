@@ -1438,12 +1438,22 @@ __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t 
                                                    const DPeer* __restrict__ peers, const SelView& sv,
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                    const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t bid_, uint32_t nblk_,
-                                                   uint32_t ew0, uint32_t new_) {
+                                                   uint32_t ew0, uint32_t new_, const uint2* __restrict__ grp_ns,
+                                                   const uint2* __restrict__ word_ns) {
   // the wave index is wave-uniform: a scalar, so the peers' records below are scalar loads
   const uint32_t wv = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const uint32_t groups = (Rp + PB_GROUP - 1) / PB_GROUP;
   if (wv >= groups * new_) return;
   const uint32_t g = wv / new_, ew = ew0 + wv % new_;
+  {  // a group of exact-namespace peers (podpeermatcher.go:115-125: ns == the policy's namespace) whose
+     // namespaces the word's identities do not have matches none of them: zeros, no selector loads
+    const uint2 gr = grp_ns[g], wr = word_ns[ew];
+    if (gr.y < wr.x || gr.x > wr.y) {
+      const uint32_t p = g * PB_GROUP + lane;
+      if (lane < PB_GROUP && p < Rp) idob[uint64_t(p) * EW + ew] = 0;
+      return;
+    }
+  }
   const uint32_t e = ew * 64 + lane;
   const bool live = e < E;
   const uint32_t ns = live ? id_ns[e] : 0u, nsls = live ? id_nsls[e] : 0u, ls = live ? id_ls[e] : 0u;
@@ -1515,11 +1525,11 @@ __global__ __launch_bounds__(256) void k_peer_bits(uint32_t Rp, uint32_t E, uint
                                                    const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres, uint32_t L,
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                    const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t ew0,
-                                                   uint32_t new_) {
+                                                   uint32_t new_, const uint2* __restrict__ grp_ns, const uint2* __restrict__ word_ns) {
   SelView sv{};
   sv.selres = selres;
   sv.L = L;
-  peer_bits_blk(Rp, E, EW, pod_peers, peers, sv, id_ns, id_nsls, id_ls, idob, blockIdx.x, gridDim.x, ew0, new_);
+  peer_bits_blk(Rp, E, EW, pod_peers, peers, sv, id_ns, id_nsls, id_ls, idob, blockIdx.x, gridDim.x, ew0, new_, grp_ns, word_ns);
 }
 
 // Per class representative and NB index (ingress: job slot, egress: job descriptor): the set of
@@ -2702,6 +2712,8 @@ struct FrontB {
   uint32_t Ru_[2], ew0[2], new_[2];
   const uint32_t* pod_peers_u_[2];
   uint64_t* idob_[2];
+  const uint2* grp_ns_[2];   // per group of PB_GROUP rows: the namespace range of its exact-namespace peers
+  const uint2* word_ns;      // per egress identity word: its identities' namespace range
   const DPeer* peers;
   const uint8_t* selres;
   const uint32_t *id_ns, *id_nsls, *id_ls;
@@ -2744,7 +2756,7 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
         return pod_rows_direct_blk<false>(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls,
                                           f.id_ls, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
       return peer_bits_blk(f.Ru_[x], f.E, f.EW, f.pod_peers_u_[x], f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob_[x], b,
-                           f.nb[2 + x], f.ew0[x], f.new_[x]);
+                           f.nb[2 + x], f.ew0[x], f.new_[x], f.grp_ns_[x], f.word_ns);
     }
     b -= f.nb[2 + x];
   }
@@ -2857,6 +2869,8 @@ __global__ __launch_bounds__(256) void k_front_c(FrontC f) {
 struct FrontRows {
   uint32_t nb[2];
   RowArgs ra[2];
+  uint32_t mix;  // k_front_e_uni: the directions' blocks alternate (both directions' class rows are
+                 // written in step, newest last: see EmitArgs::sweep), else egress blocks first
 };
 __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   const uint32_t b = blockIdx.x;
@@ -2878,9 +2892,22 @@ constexpr int E_KC = 4;  // job slots per thread in the IDO class rows of the fu
 // Launch E as one kernel when the egress rows take the one-descriptor-per-slot form (UNI): both
 // bodies then stay near 60 VGPRs, so the fused launch keeps their occupancy and saves a launch.
 __global__ __launch_bounds__(256) void k_front_e_uni(FrontRows f) {
-  const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_ido_blk<true, E_KC, true>(f.ra[1], b, f.nb[1]);
-  else class_rows_ido_blk<false, E_KC>(f.ra[0], b - f.nb[1], f.nb[0]);
+  uint32_t b = blockIdx.x, eg;
+  if (f.mix) {
+    const uint32_t m = min(f.nb[0], f.nb[1]);
+    if (b < 2 * m) {
+      eg = b & 1;
+      b >>= 1;
+    } else {
+      eg = f.nb[1] > m ? 1u : 0u;
+      b = b - m;
+    }
+  } else {
+    eg = b < f.nb[1] ? 1u : 0u;
+    if (!eg) b -= f.nb[1];
+  }
+  if (eg) class_rows_ido_blk<true, E_KC, true>(f.ra[1], b, f.nb[1]);
+  else class_rows_ido_blk<false, E_KC>(f.ra[0], b, f.nb[0]);
 }
 
 // The HBM-bound kernel: every target pod's plane rows are a copy of its class rows.  ONE launch
@@ -2917,7 +2944,34 @@ struct EmitArgs {
   // (their readers are all done): no fill launch or memset node before the next front
   uint32_t* reset;
   uint64_t reset_n;
+  // k_emit_wide / k_emit_wide_buf: a block whose XCD segment starts a new class row `prefetch` rows
+  // ahead loads that class row into its XCD's L2 once its own stores are issued (0 = off), so the
+  // blocks that reach the new class find it there instead of all waiting for one HBM read behind the
+  // write stream
+  uint32_t prefetch;
+  // sweep (> 0, one-row-per-block kernels): the row list is dealt to the XCDs in chunks of `sweep`
+  // rows (chunk k on XCD k % 8) and swept from its END: all XCDs move through the identity order
+  // together, newest class rows first — launch E writes them in about identity order, so the last
+  // ~256 MB it wrote are still in the Infinity Cache when the emit starts, and a sweep from the end
+  // reads them there instead of from HBM (an LRU cache under a forward sweep of 400 MB of class rows
+  // keeps none of them); 0 = an XCD per contiguous eighth of the list
+  uint32_t sweep;
 };
+
+// Block blockIdx.x's row r of the n-row list and its XCD x; false when the block has no row.
+__device__ __forceinline__ bool emit_slot(const EmitArgs& a, uint32_t n, uint32_t& r, uint32_t& x) {
+  const uint32_t b = blockIdx.x;
+  x = b & 7;
+  if (!a.sweep) {
+    r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
+    return r < min(n, (x + 1) * a.per_xcd);
+  }
+  const uint32_t i = b >> 3, C = a.sweep;
+  const uint64_t q = (uint64_t(i / C) * 8 + x) * C + i % C;
+  if (q >= n) return false;
+  r = n - 1 - uint32_t(q);
+  return true;
+}
 
 // Row r of the row list -> (plane, (pod, identity)).
 __device__ __forceinline__ uint2 emit_row_of(const EmitArgs& a, uint32_t r, uint32_t& pl) {
@@ -2956,11 +3010,25 @@ __device__ __forceinline__ void emit_status(const EmitArgs& a) {
 // (plain stores: config #4 emit +45 %, profiles/r03_emit_ab.txt).
 __device__ __forceinline__ void emit_store(u64x2 v, u64x2* p) { __builtin_nontemporal_store(v, p); }
 
+// EmitArgs::prefetch: the class row of the row `prefetch` rows ahead in block b's XCD segment, when
+// it starts a new class row there (differs from the previous row of its plane and from the block's
+// own source si); null otherwise.
+__device__ __forceinline__ const uint64_t* emit_next_class_row(const EmitArgs& a, uint32_t r, uint32_t n, uint32_t x,
+                                                               const uint64_t* si) {
+  const uint32_t rn = r + a.prefetch, step = a.interleave ? 2u : 1u;
+  if (a.sweep || rn >= min(n, (x + 1) * a.per_xcd) || rn < step) return nullptr;
+  uint32_t pn, pp;
+  const uint2 qn = emit_row_of(a, rn, pn), qp = emit_row_of(a, rn - step, pp);
+  const uint64_t* sn = emit_src(a, pn, qn);
+  if (!sn || sn == emit_src(a, pp, qp) || sn == si) return nullptr;
+  return sn;
+}
+
 // Rows of an odd word count or planes not 16-byte aligned: 8-byte copies, one block per row.
 __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
   emit_status(a);
-  const uint32_t b = blockIdx.x, x = b & 7, r = x * a.per_xcd + (b >> 3);
-  if (r >= min(a.n_rows[0] + a.n_rows[1], (x + 1) * a.per_xcd)) return;
+  uint32_t r, x;
+  if (!emit_slot(a, a.n_rows[0] + a.n_rows[1], r, x)) return;
   uint32_t pl;
   const uint2 pi = emit_row_of(a, r, pl);
   const uint64_t* src = emit_src(a, pl, pi);
@@ -3033,9 +3101,9 @@ __global__ __launch_bounds__(BS) void k_emit_flat(EmitArgs a) {
 template <int BS, int UNROLL>
 __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   emit_status(a);
-  const uint32_t b = blockIdx.x, n = a.n_rows[0] + a.n_rows[1], x = b & 7;
-  const uint32_t r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
-  if (r >= min(n, (x + 1) * a.per_xcd)) return;
+  const uint32_t n = a.n_rows[0] + a.n_rows[1];
+  uint32_t r, x;
+  if (!emit_slot(a, n, r, x)) return;
   uint32_t pl;
   const uint2 pi = emit_row_of(a, r, pl);
   const u64x2* si = reinterpret_cast<const u64x2*>(emit_src(a, pl, pi));
@@ -3051,6 +3119,13 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
     for (int u = 0; u < UNROLL; u++)
       if (x0 + u * BS < n2) emit_store(v[u], &di[x0 + u * BS]);
   }
+  if (!a.prefetch) return;
+  const u64x2* sn = reinterpret_cast<const u64x2*>(emit_next_class_row(a, r, n, x, reinterpret_cast<const uint64_t*>(si)));
+  if (!sn) return;
+  for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS) {
+    const u64x2 t = sn[x0];
+    asm volatile("" ::"v"(t));  // kept: the load's only purpose is the L2 fill
+  }
 }
 
 // Rows of 16-32 KB through buffer loads / stores: the chunk offsets u x BS x 16 B go to the scalar
@@ -3062,9 +3137,9 @@ constexpr int BUF_RSRC_W3 = 0x00020000;  // buffer resource word 3 for gfx9 raw 
 template <int BS, int UNROLL>
 __global__ __launch_bounds__(BS) void k_emit_wide_buf(EmitArgs a) {
   emit_status(a);
-  const uint32_t b = blockIdx.x, n = a.n_rows[0] + a.n_rows[1], x = b & 7;
-  const uint32_t r = x * a.per_xcd + (b >> 3);
-  if (r >= min(n, (x + 1) * a.per_xcd)) return;
+  const uint32_t n = a.n_rows[0] + a.n_rows[1];
+  uint32_t r, x;
+  if (!emit_slot(a, n, r, x)) return;
   uint32_t pl;
   const uint2 pi = emit_row_of(a, r, pl);
   const uint64_t* si = emit_src(a, pl, pi);
@@ -3079,6 +3154,17 @@ __global__ __launch_bounds__(BS) void k_emit_wide_buf(EmitArgs a) {
     for (int u = 0; u < UNROLL; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, x0 + u * BS * 16, 0);
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, threadIdx.x * 16, x0 + u * BS * 16, 2);  // nt
+  }
+  if (!a.prefetch) return;
+  const uint64_t* sn = emit_next_class_row(a, r, n, x, si);
+  if (!sn) return;
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(sn), 0, bytes, BUF_RSRC_W3);
+  for (uint32_t x0 = 0; x0 < bytes; x0 += BS * UNROLL * 16) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rp, threadIdx.x * 16, x0 + u * BS * 16, 0);
+      asm volatile("" ::"v"(t));  // kept: the load's only purpose is the L2 fill
+    }
   }
 }
 
@@ -3572,6 +3658,8 @@ struct cyc_ctx {
   DevBuf ipsort, ipr_tests, ipr_iv;
   uint32_t rr_off[3] = {0, 0, 0}, Rr = 0;
   uint32_t rpu_off[3] = {0, 0, 0};  // sub-lists of pod_peers_u: one pod peer per distinct matcher
+  DevBuf ido_grp_ns, ido_word_ns;  // identity-set namespace skip (peer_bits_blk): per row group, per identity word
+  uint32_t ido_goff[2] = {0, 0};   // first group of each direction's sub-list in ido_grp_ns
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
   DevBuf act[2], actrec[2], sel_list;
   DevBuf arow[2];  // per identity: its first pod's row in the run's row range (in-place class rows)
@@ -3610,6 +3698,9 @@ struct cyc_ctx {
                              // rows (1) or is [plane 0][plane 1] (0); -1 = auto (planes >= 8 GB)
   int emit_split = 1;   // "emit_split": a target-row emit as this many launches over consecutive parts
                         // of each plane's row list (1..8)
+  int emit_sweep = 0;    // "emit_sweep": EmitArgs::sweep, rows per XCD chunk of a target-row emit (0 = off)
+  int emit_prefetch = 0;  // "emit_prefetch": rows ahead a k_emit_wide(_buf) block fetches a new class row
+                          // into its XCD's L2 (EmitArgs::prefetch; 0 = off)
   // what the last enqueued emit launched (cyc_last_emit): kernel name(s) and launch count
   std::string emit_kernel;
   int emit_launches = 0;
@@ -4501,20 +4592,53 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
     // IDOB rows depend on a pod peer only through (namespace matcher, pod selector)
     // (podpeermatcher.go:21-28; the port is checked per peer by the class rows), so peers sharing
     // them share one row: config #3 has 17k pod peers over 7.8k distinct matchers
+    // The rows are ordered exact-namespace matchers first, by namespace, so a group of PB_GROUP rows
+    // mostly names one or two namespaces: its identity-set waves over words of other namespaces'
+    // identities skip every selector (grp_ns / word_ns below).
     std::vector<uint32_t> pi(std::max<size_t>(pb.peers.size(), 1), 0), ppu;
+    std::vector<uint2> gns;
     for (int d = 0; d < 2; d++) {
       c->rpu_off[d] = uint32_t(ppu.size());
-      std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> row;
+      c->ido_goff[d] = uint32_t(gns.size());
+      std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> row;  // matcher -> its first peer
       for (uint32_t x = c->rp_off[d]; x < c->rp_off[d + 1]; x++) {
         const DPeer& pr = pb.peers[pp[x]];
-        auto it = row.emplace(std::make_tuple(pr.nskind, pr.nsval, pr.podsel), uint32_t(ppu.size())).first;
-        if (it->second == ppu.size()) ppu.push_back(pp[x]);
-        pi[pp[x]] = it->second;
+        row.emplace(std::make_tuple(pr.nskind, pr.nsval, pr.podsel), pp[x]);
+      }
+      const uint32_t u0 = uint32_t(ppu.size());
+      std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> at;
+      for (const auto& kv : row) {  // (nskind 0 = exact namespace sorts first, then by namespace)
+        at[kv.first] = uint32_t(ppu.size());
+        ppu.push_back(kv.second);
+      }
+      for (uint32_t x = c->rp_off[d]; x < c->rp_off[d + 1]; x++) {
+        const DPeer& pr = pb.peers[pp[x]];
+        pi[pp[x]] = at[std::make_tuple(pr.nskind, pr.nsval, pr.podsel)];
+      }
+      for (uint32_t g0 = u0; g0 < ppu.size(); g0 += PB_GROUP) {
+        uint2 r{0xFFFFFFFFu, 0u};
+        for (uint32_t x = g0; x < std::min<uint32_t>(g0 + PB_GROUP, uint32_t(ppu.size())); x++) {
+          const DPeer& pr = pb.peers[ppu[x]];
+          if (pr.nskind != 0) r = uint2{0u, 0xFFFFFFFFu};  // a namespace / all-namespace matcher: never skipped
+          if (r.x == 0 && r.y == 0xFFFFFFFFu) break;
+          r.x = std::min(r.x, pr.nsval);
+          r.y = std::max(r.y, pr.nsval);
+        }
+        gns.push_back(r);
       }
     }
     c->rpu_off[2] = uint32_t(ppu.size());
     upload(c->pod_peers_u, ppu);
     upload(c->peer_ido, pi);
+    gns.push_back(uint2{0u, 0xFFFFFFFFu});
+    upload(c->ido_grp_ns, gns);
+    const auto& ins = c->ids[1].ns;  // egress identities' namespaces, per 64-identity word
+    std::vector<uint2> wns(std::max<size_t>((ins.size() + 63) / 64, 1), uint2{0xFFFFFFFFu, 0u});
+    for (size_t e = 0; e < ins.size(); e++) {
+      wns[e / 64].x = std::min(wns[e / 64].x, ins[e]);
+      wns[e / 64].y = std::max(wns[e / 64].y, ins[e]);
+    }
+    upload(c->ido_word_ns, wns);
   }
   upload(c->ip_peers, ip);
   upload(c->ip_tests, tests);
@@ -4610,7 +4734,8 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
         k_peer_bits<<<unsigned((uint64_t((Ru + PB_GROUP - 1) / PB_GROUP) * new_ + 3) / 4), 256, 0, st>>>(
             Ru, E, EW, c->pod_peers_u.as<uint32_t>() + u0, c->peers.as<DPeer>(), c->selres.as<uint8_t>(), pb.L,
             c->dir[1].id_ns.as<uint32_t>(), c->id_nsls.as<uint32_t>(), c->dir[1].id_ls.as<uint32_t>(),
-            c->idob.as<uint64_t>() + uint64_t(u0) * EW, ew0, new_);
+            c->idob.as<uint64_t>() + uint64_t(u0) * EW, ew0, new_, c->ido_grp_ns.as<uint2>() + c->ido_goff[x],
+            c->ido_word_ns.as<uint2>());
     }
   } else if (Rp && E && nw && (c->pod_rows >= 0 ? c->pod_rows == 1 : uint64_t(E) * 2 >= P)) {
     const uint32_t* plist = c->pod_peers.as<uint32_t>() + r0;
@@ -4822,7 +4947,11 @@ static const char* enq_emit_units(EmitArgs ea, hipStream_t st) {
 
 static const char* enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64_t* out_in, uint64_t* out_eg) {
   EmitArgs ea = ea_in;
-  ea.per_xcd = (ea.n_rows[0] + ea.n_rows[1] + 7) / 8;
+  const uint32_t nr = ea.n_rows[0] + ea.n_rows[1];
+  ea.per_xcd = (nr + 7) / 8;
+  const uint64_t row_bytes0 = ea.row_words * 8;
+  if (row_bytes0 < EMIT_WIDE_MIN && ea.row_words % 2 == 0) ea.sweep = 0;  // (k_emit_flat: multi-row blocks)
+  if (ea.sweep) ea.per_xcd = (nr + 8 * ea.sweep - 1) / (8 * ea.sweep) * ea.sweep;  // whole rounds of 8 chunks
   const bool aligned = reinterpret_cast<uintptr_t>(out_in) % 16 == 0 && reinterpret_cast<uintptr_t>(out_eg) % 16 == 0;
   const unsigned g = ea.per_xcd * 8;  // one block per row slot of the 8 XCD segments
   if (ea.row_words % 2 || !aligned) {
@@ -4908,6 +5037,8 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
   ea.reset = c->ip_rng.as<uint32_t>();
   ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
+  ea.prefetch = uint32_t(c->emit_prefetch);
+  ea.sweep = uint32_t(c->emit_sweep);
   c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
     ea.row_lo[pl] = uint32_t(c->rl[pl]);
@@ -5072,11 +5203,13 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.id_nsls = c->id_nsls.as<uint32_t>();
   fb.id_ls = c->dir[1].id_ls.as<uint32_t>();
   fb.sv = sel_view(c);
+  fb.word_ns = c->ido_word_ns.as<uint2>();
   for (int x = 0; x < 2; x++) {  // identity sets per direction: the ingress ones over the window's identity words
     const uint32_t ux = c->rpu_off[x];
     fb.Ru_[x] = c->rpu_off[x + 1] - ux;
     fb.pod_peers_u_[x] = c->pod_peers_u.as<uint32_t>() + ux;
     fb.idob_[x] = c->idob.as<uint64_t>() + uint64_t(ux) * EW;
+    fb.grp_ns_[x] = c->ido_grp_ns.as<uint2>() + c->ido_goff[x];
     fb.ew0[x] = x == 0 ? c->ido_ew0 : 0u;
     fb.new_[x] = x == 0 ? c->ido_ew1 - c->ido_ew0 : EW;
     fb.nb[2 + x] = (fb.Ru_[x] && E && fb.new_[x]) ? blocks((uint64_t((fb.Ru_[x] + PB_GROUP - 1) / PB_GROUP) * fb.new_[x] + 3) / 4) : 0u;
@@ -5230,6 +5363,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
   if (fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
+    fe.mix = c->emit_sweep ? 1u : 0u;
     k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);
   } else {  // the directions' class rows as two launches, each at its own register budget (egress 101
             // VGPRs, ingress 61: one launch at 101 ran config #3 189 -> 170 us, profiles/r03_e_split_ab.txt)
@@ -6146,6 +6280,8 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "step_events") range(0, 1), c->step_events = int(value);
     else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
     else if (n == "emit_split") range(1, 8), c->emit_split = int(value);
+    else if (n == "emit_prefetch") range(0, 4096), c->emit_prefetch = int(value);
+    else if (n == "emit_sweep") range(0, 1 << 20), c->emit_sweep = int(value);
     else if (n == "plvt_max_mb") {
       range(0, 1 << 20);
       c->plvt_max_mb = value;
@@ -6178,6 +6314,8 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "step_events") *value = c->step_events;
   else if (n == "emit_interleave") *value = c->emit_interleave;
   else if (n == "emit_split") *value = c->emit_split;
+  else if (n == "emit_prefetch") *value = c->emit_prefetch;
+  else if (n == "emit_sweep") *value = c->emit_sweep;
   else if (n == "plvt_max_mb") *value = c->plvt_max_mb;
   else if (n == "plvt_active") *value = c->plvt_ready ? 1 : 0;
   else if (n == "pl_wave_active") {

@@ -31,8 +31,8 @@ from cyclonus_amd.engine import Engine
 from cyclonus_amd.flat import prepare_flat
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "time"
-pos = [a for a in sys.argv[2:] if "=" not in a]
-kw = dict(a.split("=") for a in sys.argv[2:] if "=" in a)
+pos = [a for a in sys.argv[2:] if "=" not in a or ":" in a]
+kw = dict(a.split("=") for a in sys.argv[2:] if "=" in a and ":" not in a)
 steps, reps, n_run = int(kw.get("steps", 20)), int(kw.get("reps", 3)), int(kw.get("n", 10))
 
 data = synth.CONFIGS["config3"]()
@@ -59,15 +59,25 @@ VARIANTS = {
 }
 
 
+def spec(name):
+    """A variant, optionally with options: "whole:emit_prefetch=128,emit_interleave=0"."""
+    base, _, extra = name.partition(":")
+    opts = dict(VARIANTS[base][0])
+    for kv in filter(None, extra.split(",")):
+        k, v = kv.split("=")
+        opts[k] = int(v)
+    return opts, VARIANTS[base][1]
+
+
 def setv(name):
-    eng.set_option("emit_interleave", -1)
-    eng.set_option("emit_split", 1)
-    for k, v in VARIANTS[name][0].items():
+    for k, v in (("emit_interleave", -1), ("emit_split", 1), ("emit_prefetch", 0)):
+        eng.set_option(k, v)
+    for k, v in spec(name)[0].items():
         eng.set_option(k, v)
 
 
 def step(name):
-    for lo, hi, at in VARIANTS[name][1]:
+    for lo, hi, at in spec(name)[1]:
         # a target-row run writes its rows from the given pointers' row 0: place them at row `at`
         eng.run_device(B_IN + at * row * 8, B_EG + at * row * 8, d_st.data_ptr(), st, lo, hi)
 
@@ -79,7 +89,7 @@ if mode == "run":  # for rocprofv3 --pmc passes: n eager steps (graphs = 0) of e
         for _ in range(n_run):
             step(name)
         torch.cuda.synchronize()
-        print(f"{name}: {n_run} steps, emit {eng.last_emit()} per run, {len(VARIANTS[name][1])} runs a step", flush=True)
+        print(f"{name}: {n_run} steps, emit {eng.last_emit()} per run, {len(spec(name)[1])} runs a step", flush=True)
     sys.exit(0)
 
 
@@ -101,7 +111,7 @@ def emit_events(name, n=5):
     out = []
     for _ in range(n):
         tot = 0.0
-        for lo, hi, at in VARIANTS[name][1]:
+        for lo, hi, at in spec(name)[1]:
             eng.run_device(B_IN + at * row * 8, B_EG + at * row * 8, d_st.data_ptr(), st, lo, hi)
             tot += eng.timings()[1]
         out.append(tot)
@@ -123,7 +133,8 @@ def fill_ms():
 
 
 names = pos or list(VARIANTS)
-print(f"config3 flat-prepared: P={P} K={K} W={W}, plane row {row * 8} B; steps={steps} reps={reps}", flush=True)
+print(f"config3 flat-prepared: P={P} K={K} W={W}, plane row {row * 8} B; steps={steps} reps={reps}; planes at "
+      f"{B_IN:#x} / {B_EG:#x} (mod 1 GiB {B_IN % (1 << 30):#x} / {B_EG % (1 << 30):#x})", flush=True)
 res = {n: [] for n in names}
 for r in range(reps):
     for n in names:
@@ -137,6 +148,6 @@ for n in names:
     ev, (kern, launches) = emit_events(n)
     t = min(res[n])
     rel = f" ({(t / base - 1) * 100:+.1f} % vs whole)" if base else ""
-    print(f"{n:11s}: {t:.3f} ms/step{rel}; emit events {ev:.3f} ms/step = {alg / ev / 1e6:.0f} GB/s "
+    print(f"{n:24s}: {t:.3f} ms/step{rel}; emit events {ev:.3f} ms/step = {alg / ev / 1e6:.0f} GB/s "
           f"({launches} x {kern})", flush=True)
 print(json.dumps({"ms_per_step": {n: min(v) for n, v in res.items()}, "fill_ms": fill}), flush=True)

@@ -20,9 +20,10 @@ for path in sorted(glob.glob(os.path.join(out, "pmcab_*", "**", "*counter_collec
     ids = sorted({int(r["Dispatch_Id"]) for r in rows})
     owner, at = {}, 0
     for v in variants:
-        for d in ids[at:at + N * PER_STEP[v]]:
+        k = PER_STEP[v.split(":")[0]]
+        for d in ids[at:at + N * k]:
             owner[d] = v
-        at += N * PER_STEP[v]
+        at += N * k
     for r in rows:
         v = owner.get(int(r["Dispatch_Id"]))
         if v:
