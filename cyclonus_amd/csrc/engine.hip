@@ -2944,11 +2944,6 @@ struct EmitArgs {
   // (their readers are all done): no fill launch or memset node before the next front
   uint32_t* reset;
   uint64_t reset_n;
-  // k_emit_wide / k_emit_wide_buf: a block whose XCD segment starts a new class row `prefetch` rows
-  // ahead loads that class row into its XCD's L2 once its own stores are issued (0 = off), so the
-  // blocks that reach the new class find it there instead of all waiting for one HBM read behind the
-  // write stream
-  uint32_t prefetch;
   // sweep (> 0, one-row-per-block kernels): the row list is dealt to the XCDs in chunks of `sweep`
   // rows (chunk k on XCD k % 8) and swept from its END: all XCDs move through the identity order
   // together, newest class rows first — launch E writes them in about identity order, so the last
@@ -3009,20 +3004,6 @@ __device__ __forceinline__ void emit_status(const EmitArgs& a) {
 // Plane stores are non-temporal: they do not displace the class rows the emit re-reads from L2
 // (plain stores: config #4 emit +45 %, profiles/r03_emit_ab.txt).
 __device__ __forceinline__ void emit_store(u64x2 v, u64x2* p) { __builtin_nontemporal_store(v, p); }
-
-// EmitArgs::prefetch: the class row of the row `prefetch` rows ahead in block b's XCD segment, when
-// it starts a new class row there (differs from the previous row of its plane and from the block's
-// own source si); null otherwise.
-__device__ __forceinline__ const uint64_t* emit_next_class_row(const EmitArgs& a, uint32_t r, uint32_t n, uint32_t x,
-                                                               const uint64_t* si) {
-  const uint32_t rn = r + a.prefetch, step = a.interleave ? 2u : 1u;
-  if (a.sweep || rn >= min(n, (x + 1) * a.per_xcd) || rn < step) return nullptr;
-  uint32_t pn, pp;
-  const uint2 qn = emit_row_of(a, rn, pn), qp = emit_row_of(a, rn - step, pp);
-  const uint64_t* sn = emit_src(a, pn, qn);
-  if (!sn || sn == emit_src(a, pp, qp) || sn == si) return nullptr;
-  return sn;
-}
 
 // Rows of an odd word count or planes not 16-byte aligned: 8-byte copies, one block per row.
 __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
@@ -3119,13 +3100,6 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
     for (int u = 0; u < UNROLL; u++)
       if (x0 + u * BS < n2) emit_store(v[u], &di[x0 + u * BS]);
   }
-  if (!a.prefetch) return;
-  const u64x2* sn = reinterpret_cast<const u64x2*>(emit_next_class_row(a, r, n, x, reinterpret_cast<const uint64_t*>(si)));
-  if (!sn) return;
-  for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS) {
-    const u64x2 t = sn[x0];
-    asm volatile("" ::"v"(t));  // kept: the load's only purpose is the L2 fill
-  }
 }
 
 // Rows of 16-32 KB through buffer loads / stores: the chunk offsets u x BS x 16 B go to the scalar
@@ -3154,17 +3128,6 @@ __global__ __launch_bounds__(BS) void k_emit_wide_buf(EmitArgs a) {
     for (int u = 0; u < UNROLL; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, x0 + u * BS * 16, 0);
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, threadIdx.x * 16, x0 + u * BS * 16, 2);  // nt
-  }
-  if (!a.prefetch) return;
-  const uint64_t* sn = emit_next_class_row(a, r, n, x, si);
-  if (!sn) return;
-  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(sn), 0, bytes, BUF_RSRC_W3);
-  for (uint32_t x0 = 0; x0 < bytes; x0 += BS * UNROLL * 16) {
-#pragma unroll
-    for (int u = 0; u < UNROLL; u++) {
-      const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rp, threadIdx.x * 16, x0 + u * BS * 16, 0);
-      asm volatile("" ::"v"(t));  // kept: the load's only purpose is the L2 fill
-    }
   }
 }
 
@@ -3698,9 +3661,9 @@ struct cyc_ctx {
                              // rows (1) or is [plane 0][plane 1] (0); -1 = auto (planes >= 8 GB)
   int emit_split = 1;   // "emit_split": a target-row emit as this many launches over consecutive parts
                         // of each plane's row list (1..8)
-  int emit_sweep = 0;    // "emit_sweep": EmitArgs::sweep, rows per XCD chunk of a target-row emit (0 = off)
-  int emit_prefetch = 0;  // "emit_prefetch": rows ahead a k_emit_wide(_buf) block fetches a new class row
-                          // into its XCD's L2 (EmitArgs::prefetch; 0 = off)
+  int emit_sweep = 0;    // "emit_sweep": EmitArgs::sweep, rows per XCD chunk of a target-row emit (0 = off):
+                         // -2 to -4 % per step on some plane placements, +6 % on others (config #3 over 5
+                         // placements in one process: mean +0.2 %, profiles/r05_plane_placement.txt)
   // what the last enqueued emit launched (cyc_last_emit): kernel name(s) and launch count
   std::string emit_kernel;
   int emit_launches = 0;
@@ -5037,7 +5000,6 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
   ea.reset = c->ip_rng.as<uint32_t>();
   ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
-  ea.prefetch = uint32_t(c->emit_prefetch);
   ea.sweep = uint32_t(c->emit_sweep);
   c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
@@ -5113,12 +5075,15 @@ static bool front_fused_ok(const cyc_ctx* c) {
 
 // In-place class rows: the fused front with both output planes given.
 // Auto (-1): when the rows' identities are >= 1/16 of the rows (PM builds: config #4 emit -8 %,
-// #3u -7 %); with few identities the rows saved are few while the class rows, scattered over the
-// planes, write slower (config #3: 2 % of the rows, net +1 %: profiles/r02_class_inplace_ab.txt).
+// #3u -7 %), and for identity-set (IDO) target-row runs: config #3's class rows are 2 % of its rows,
+// and writing them into the planes saves their 400 MB of separate writes (3.286 -> 3.191 ms/step,
+// profiles/r05_inplace_sweep_ab.txt; over 5 plane placements in one process -2.1 / -0.0 / -0.1 /
+// -2.8 / -2.2 %, never slower: profiles/r05_plane_placement.txt; in round 2, before the current
+// launch E, it lost 1 %).
 static bool inplace_ok(const cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg) {
   if (!c->class_inplace || !d_in || !d_eg || !front_fused_ok(c) || !c->pb.blocks.empty()) return false;
   const uint64_t rows = uint64_t(std::max<int64_t>((c->rh[0] - c->rl[0] + c->rh[1] - c->rl[1]) / 2, 1));
-  return c->class_inplace == 1 || uint64_t(c->n_act[0] + c->n_act[1]) * 16 >= 2 * rows;
+  return c->class_inplace == 1 || uint64_t(c->n_act[0] + c->n_act[1]) * 16 >= 2 * rows || (ido_mode(c) && !c->order_src);
 }
 
 // out_in / out_eg non-null: the class rows go straight into those planes (in-place class rows; the
@@ -6280,7 +6245,6 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "step_events") range(0, 1), c->step_events = int(value);
     else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
     else if (n == "emit_split") range(1, 8), c->emit_split = int(value);
-    else if (n == "emit_prefetch") range(0, 4096), c->emit_prefetch = int(value);
     else if (n == "emit_sweep") range(0, 1 << 20), c->emit_sweep = int(value);
     else if (n == "plvt_max_mb") {
       range(0, 1 << 20);
@@ -6314,7 +6278,6 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "step_events") *value = c->step_events;
   else if (n == "emit_interleave") *value = c->emit_interleave;
   else if (n == "emit_split") *value = c->emit_split;
-  else if (n == "emit_prefetch") *value = c->emit_prefetch;
   else if (n == "emit_sweep") *value = c->emit_sweep;
   else if (n == "plvt_max_mb") *value = c->plvt_max_mb;
   else if (n == "plvt_active") *value = c->plvt_ready ? 1 : 0;

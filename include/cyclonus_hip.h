@@ -209,7 +209,9 @@ int64_t cyc_resources_json(cyc_ctx* ctx, char* buf, size_t cap);
  * Resources.Pods order; pass 0, P for the whole table).  Device pointers; `hip_stream` is the
  * hipStream_t to enqueue on (NULL = the HIP default stream, as with every HIP API).  Asynchronous
  * unless the inputs can panic (then it synchronises to report the first panicking job in job
- * order, as the reference would). */
+ * order, as the reference would).  The planes must be device memory (hipMalloc and the like), read
+ * back by hipMemcpy or by kernels after the stream: the run's events release at device scope, so
+ * host-mapped, non-coherent memory is not made visible to the host by a stream synchronisation. */
 int cyc_probe_run(cyc_ctx* ctx, void* hip_stream, uint64_t* d_ingress, uint64_t* d_egress, uint8_t* d_status,
                   int64_t row_lo, int64_t row_hi);
 
@@ -353,7 +355,8 @@ int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
  *   "class_inplace" -1 (default: auto) / 0 / 1: on the fused front, each class's rows are written
  *                 straight into the output planes at its first member pod's row and the emit copies
  *                 them to the class's other pods (1), or they go to a buffer of their own the emit
- *                 copies from (0); auto = 1 when the rows' identities are >= 1/16 of the rows
+ *                 copies from (0); auto = 1 when the rows' identities are >= 1/16 of the rows or
+ *                 the run is a target-row run of an identity-set build
  *                 ("class_inplace_active" reports the choice of the last run's row range)
  *   "sel_lazy"    -1 (default: auto) / 0 / 1: on the fused front, label selectors are evaluated where
  *                 membership and pod-peer rows / identity sets use them (1) instead of as the dense
@@ -363,6 +366,9 @@ int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
  *                 emit's row list alternates ingress and egress rows (1) or holds all ingress rows first
  *   "emit_split"  1 (default) .. 8: a target-row run's emit as that many launches over consecutive
  *                 parts of the planes' row lists
+ *   "emit_sweep"  0 (default) / C > 0: a target-row run's emit deals its row list to the XCDs in chunks
+ *                 of C rows and sweeps it from the end (all XCDs move through the class order together,
+ *                 the class rows written last read first), instead of an XCD per contiguous eighth
  * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
  * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
  * uses (0 or 1). */

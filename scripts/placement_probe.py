@@ -4,7 +4,13 @@ caching allocator: one hipMalloc each), then whole-table steps timed round-robin
 torch fill_ of each pair — same library, same process, same front: only the planes' placement differs.
 
     python scripts/placement_probe.py [pairs=4] [steps=20] [reps=3] [NAME=VALUE ...]   (cyc_set_option)
+    python scripts/placement_probe.py pairs=4 "alt=class_inplace:0,emit_sweep:0;emit_sweep:0"   (each pair also
+                                                                   with each option set)
+    python scripts/placement_probe.py pairs=2 hip=2 contig=2     (+ pairs from hipExtMallocWithFlags: flags 0 /
+                                                                   hipDeviceMallocContiguous)
+The fill of each pair is hipMemsetD32Async over both planes (one kernel for every allocation kind).
 """
+import ctypes
 import os
 import sys
 import time
@@ -18,6 +24,9 @@ from cyclonus_amd.flat import prepare_flat
 
 kw = dict(a.split("=") for a in sys.argv[1:])
 pairs, steps, reps = int(kw.pop("pairs", 4)), int(kw.pop("steps", 20)), int(kw.pop("reps", 3))
+# alt=name:v,name:v[;name:v...]: option sets run on every pair besides the defaults
+alts = [dict(x.split(":") for x in grp.split(",") if x) for grp in kw.pop("alt", "").split(";") if grp]
+n_hip, n_contig = int(kw.pop("hip", 0)), int(kw.pop("contig", 0))
 data = synth.CONFIGS["config3"]()
 eng = Engine(0)
 sh = prepare_flat(eng, data["policies"], data["resources"], data["probes"])
@@ -27,11 +36,32 @@ P, K, W = sh["pods"], sh["slots"], sh["words"]
 n = P * K * W
 st = torch.cuda.current_stream().cuda_stream
 d_st = torch.empty((P, K), dtype=torch.uint8, device="cuda")
+hip = ctypes.CDLL("libamdhip64.so")
+
+
+class Raw:  # a device allocation of hipExtMallocWithFlags (data_ptr like a tensor's)
+    def __init__(self, flags):
+        p = ctypes.c_void_p()
+        rc = hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(n * 8), ctypes.c_uint(flags))
+        if rc != 0:
+            raise RuntimeError(f"hipExtMallocWithFlags(flags={flags}) failed: {rc}")
+        self.p = p.value
+
+    def data_ptr(self):
+        return self.p
+
+
 planes = [(torch.empty((n,), dtype=torch.int64, device="cuda"), torch.empty((n,), dtype=torch.int64, device="cuda"))
           for _ in range(pairs)]
+kinds = ["torch"] * pairs
+for flags, cnt, kind in ((0, n_hip, "hipMalloc"), (4, n_contig, "contiguous")):
+    for _ in range(cnt):
+        planes.append((Raw(flags), Raw(flags)))
+        kinds.append(kind)
+pairs = len(planes)
 print(f"config3: {pairs} plane pairs of 2 x {n * 8 / 1e9:.2f} GB, options {kw}", flush=True)
 for i, (a, b) in enumerate(planes):
-    print(f"pair {i}: ingress {a.data_ptr():#x} egress {b.data_ptr():#x} "
+    print(f"pair {i} ({kinds[i]}): ingress {a.data_ptr():#x} egress {b.data_ptr():#x} "
           f"(mod 1 GiB {a.data_ptr() % (1 << 30):#x} / {b.data_ptr() % (1 << 30):#x})", flush=True)
 
 
@@ -61,20 +91,34 @@ def fill_ms(a, b):
     best = 1e9
     for _ in range(3):
         e0.record()
-        a.fill_(0)
-        b.fill_(0)
+        for x in (a, b):
+            hip.hipMemsetD32Async(ctypes.c_void_p(x.data_ptr()), ctypes.c_int(0), ctypes.c_size_t(2 * n), ctypes.c_void_p(st))
         e1.record()
         torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1))
     return best
 
 
-res = [[] for _ in planes]
+base = {k: eng.get_option(k) for alt in alts for k in alt}
+sets = [("default", base)] + [(",".join(f"{k}={v}" for k, v in alt.items()), {**base, **{k: int(v) for k, v in alt.items()}})
+                              for alt in alts]
+
+
+def use(opts):
+    for k, v in opts.items():
+        eng.set_option(k, v)
+
+
+res = {(i, nm): [] for i in range(pairs) for nm, _ in sets}
 for r in range(reps):
+    for nm, opts in sets:
+        use(opts)
+        for i, (a, b) in enumerate(planes):
+            res[(i, nm)].append(step_ms(a, b))
+        print(f"rep {r} {nm}: " + ", ".join(f"pair {i} {res[(i, nm)][-1]:.3f}" for i in range(pairs)), flush=True)
+for nm, opts in sets:
+    use(opts)
     for i, (a, b) in enumerate(planes):
-        res[i].append(step_ms(a, b))
-    print(f"rep {r}: " + ", ".join(f"pair {i} {res[i][-1]:.3f}" for i in range(pairs)), flush=True)
-for i, (a, b) in enumerate(planes):
-    em, fm = emit_ms(a, b), fill_ms(a, b)
-    print(f"pair {i}: {min(res[i]):.3f} ms/step, emit {em:.3f} ms ({2 * n * 8 / em / 1e6:.0f} GB/s), "
-          f"fill {fm:.3f} ms ({2 * n * 8 / fm / 1e6:.0f} GB/s), emit / fill {em / fm:.3f}", flush=True)
+        em, fm = emit_ms(a, b), fill_ms(a, b)
+        print(f"{nm}: pair {i} ({kinds[i]}): {min(res[(i, nm)]):.3f} ms/step, emit {em:.3f} ms ({2 * n * 8 / em / 1e6:.0f} GB/s), "
+              f"fill {fm:.3f} ms ({2 * n * 8 / fm / 1e6:.0f} GB/s), emit / fill {em / fm:.3f}", flush=True)
