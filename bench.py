@@ -144,7 +144,8 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     part = args.partition
     t_prep = time.perf_counter()
-    eng = Engine(device)
+    eng = Engine(device)  # cyc_ctx_create: the context's HIP stream and events (once per process and GPU)
+    ctx_create_s = time.perf_counter() - t_prep
     for o in args.opt:
         k, v = o.split("=")
         eng.set_option(k, int(v))
@@ -176,6 +177,7 @@ def main():
         shape = prepare_flat(eng, data["policies"], data["resources"], data["probes"])
         torch.cuda.synchronize()
         prepare_s = shape.pop("prepare_s")
+        prepare_s["context_create_s"] = ctx_create_s  # (not in total_s: once per process, not per probe model)
         P, K, W = shape["pods"], shape["slots"], shape["words"]
         lo, hi = shard_range(P, world, rank, part)
         rows = hi - lo

@@ -986,6 +986,54 @@ __global__ __launch_bounds__(256) void k_ip_rows_fast(uint32_t Ri, uint32_t P, u
   ip_rows_fast_blk(Ri, P, W, tests, ip_ex, pod_ip, words, PM, rng, cnz, blockIdx.x, gridDim.x, grp, c0, nch);
 }
 
+// IP rows as work items (the fused front's default, cyc_set_option "ip_items"): the host lists, per
+// 64-word chunk of the run's window, the IP rows whose network meets the chunk's address range
+// (the test ip_rows_fast_blk makes per wave, made once per range plan), so a wave handles up to
+// IPI_TOUCH rows that all touch its chunk — its word records loaded once for all of them, their tests
+// held one per lane and broadcast with readlane — instead of a group of IP_GROUP rows of which a
+// few touch (config #4: ~1 in 5).  A "zero" item clears the chunk flag of up to 64 rows that miss it.
+struct DIPItem {
+  uint32_t chunk, off, cnt, touch;  // rows ilist[off .. off + cnt) (indices into the segment's tests)
+};
+constexpr uint32_t IPI_TOUCH = 16;  // touching rows per wave
+__device__ __forceinline__ void ip_rows_items_blk(uint32_t n_items, const DIPItem* __restrict__ items,
+                                                  const uint32_t* __restrict__ ilist, uint32_t P, uint32_t W,
+                                                  const DIPTest* __restrict__ tests, const DCidr* __restrict__ ip_ex,
+                                                  const DIP* __restrict__ pod_ip, const DWordIP* __restrict__ words,
+                                                  uint64_t* __restrict__ PM, uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz,
+                                                  uint32_t bid_) {
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  if (wv >= n_items) return;
+  const DIPItem it = items[wv];
+  const uint32_t cw = (W + 63) / 64;
+  const uint32_t mi = ilist[it.off + min(lane, it.cnt - 1)];
+  if (!it.touch) {
+    const uint32_t peer = tests[mi].peer;
+    if (lane < it.cnt) cnz[uint64_t(peer) * cw + it.chunk] = 0;
+    return;
+  }
+  const uint32_t w = it.chunk * 64 + lane;
+  const bool valid = w < W;
+  const DWordIP wd = words[min(w, W - 1)];
+  const DIPTest mine = tests[mi];  // lane x < cnt holds row x's test
+  for (uint32_t x = 0; x < it.cnt; x++) {
+    DIPTest t;
+    t.peer = __builtin_amdgcn_readlane(mine.peer, x);
+    t.exoff = __builtin_amdgcn_readlane(mine.exoff, x);
+    t.excnt = __builtin_amdgcn_readlane(mine.excnt, x);
+    t.pad = 0;
+    t.cidr.valid = __builtin_amdgcn_readlane(mine.cidr.valid, x);
+    t.cidr.fam = __builtin_amdgcn_readlane(mine.cidr.fam, x);
+    t.cidr.pad0 = t.cidr.pad1 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      t.cidr.net[i] = __builtin_amdgcn_readlane(mine.cidr.net[i], x);
+      t.cidr.mask[i] = __builtin_amdgcn_readlane(mine.cidr.mask[i], x);
+    }
+    ip_row_word(t, ip_ex + t.exoff, pod_ip, wd, valid, w, it.chunk, P, W, lane, PM, rng, cnz);
+  }
+}
+
 // Grid of k_ip_rows_fast / an IP-row range of k_front_b: peer groups x blocks of 4 of the nch chunks.
 __host__ __device__ inline uint64_t ip_rows_blocks(uint32_t Ri, uint32_t nch, uint32_t grp) {
   return uint64_t((Ri + grp - 1) / grp) * ((nch + 3) / 4);
@@ -2701,6 +2749,9 @@ struct FrontB {
   uint32_t Ri[2], P, W;
   const DIPTest* tests[2];
   uint32_t ic0[2], inch[2];  // IP rows: chunk window per segment
+  const DIPItem* ip_items[2];  // IP rows as work items (non-null: segments 0-1 are items, a wave each)
+  uint32_t n_ip_items[2];
+  const uint32_t* ip_ilist;
   const DCidr* ip_ex;
   const DIP* pod_ip;
   const DWordIP* words;
@@ -2744,9 +2795,13 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   }
 #pragma unroll
   for (int x = 0; x < 2; x++) {
-    if (b < f.nb[x])
+    if (b < f.nb[x]) {
+      if (f.ip_items[x])
+        return ip_rows_items_blk(f.n_ip_items[x], f.ip_items[x], f.ip_ilist, f.P, f.W, f.tests[x], f.ip_ex, f.pod_ip, f.words,
+                                 f.PM, f.rng, f.cnz, b);
       return ip_rows_fast_blk(f.Ri[x], f.P, f.W, f.tests[x], f.ip_ex, f.pod_ip, f.words, f.PM, f.rng, f.cnz, b, f.nb[x], f.ip_grp,
                               f.ic0[x], f.inch[x]);
+    }
     b -= f.nb[x];
   }
 #pragma unroll
@@ -2951,6 +3006,7 @@ struct EmitArgs {
   // reads them there instead of from HBM (an LRU cache under a forward sweep of 400 MB of class rows
   // keeps none of them); 0 = an XCD per contiguous eighth of the list
   uint32_t sweep;
+  uint32_t sweep_fwd;  // the chunks from the start of the list (emit_sweep < 0)
 };
 
 // Block blockIdx.x's row r of the n-row list and its XCD x; false when the block has no row.
@@ -2964,7 +3020,7 @@ __device__ __forceinline__ bool emit_slot(const EmitArgs& a, uint32_t n, uint32_
   const uint32_t i = b >> 3, C = a.sweep;
   const uint64_t q = (uint64_t(i / C) * 8 + x) * C + i % C;
   if (q >= n) return false;
-  r = n - 1 - uint32_t(q);
+  r = a.sweep_fwd ? uint32_t(q) : n - 1 - uint32_t(q);
   return true;
 }
 
@@ -3621,6 +3677,11 @@ struct cyc_ctx {
   DevBuf ipsort, ipr_tests, ipr_iv;
   uint32_t rr_off[3] = {0, 0, 0}, Rr = 0;
   uint32_t rpu_off[3] = {0, 0, 0};  // sub-lists of pod_peers_u: one pod peer per distinct matcher
+  DevBuf ipi_items, ipi_list;   // IP-row work items of the fused front (DIPItem; ip_rows_items_blk) and their rows
+  uint32_t ipi_off[3] = {0, 0, 0};  // items of segment x: [ipi_off[x], ipi_off[x + 1])
+  bool ip_items = false;        // the current plan's items are built (option "ip_items" on and fast IP rows present)
+  int ip_items_opt = -1;        // "ip_items": -1 auto (on) / 0 / 1
+  std::vector<DWordIP> ipw_h;   // host copy of the IP word and chunk records (ip_words)
   DevBuf ido_grp_ns, ido_word_ns;  // identity-set namespace skip (peer_bits_blk): per row group, per identity word
   uint32_t ido_goff[2] = {0, 0};   // first group of each direction's sub-list in ido_grp_ns
   PeerPlan plan;                 // all pod / IP peers (host); filtered per row range
@@ -4125,6 +4186,7 @@ static void prepare_device(cyc_ctx* c) {
         wi[pb.W + ch] = d;
       }
       upload(c->ip_words, wi);
+      c->ipw_h = wi;
       // namespace range of every word's and chunk's pods (pod_rows_sparse_blk)
       std::vector<DWordNS> nw(pb.W + NC, DWordNS{0xFFFFFFFFu, 0u, 0u, 0u});
       for (uint32_t q = 0; q < pb.P; q++) {
@@ -4313,6 +4375,25 @@ static uint32_t pl_blocks(const cyc_ctx* c, int d) { return std::min<uint32_t>(c
 // k): egress rows of sources [lo, hi) (full rows) and the ingress rows of EVERY destination, but
 // only their words [lo / 64, ceil(hi / 64)) — the shard's sources as peers.  lo must be a multiple
 // of 64 and hi too unless it is P (checked by the caller), so the windows of a partition tile the words.
+static void peer_chunks(const cyc_ctx* c, int d, uint32_t& c0, uint32_t& nch);
+static bool one_window(const cyc_ctx* c);
+// Host restatement of ip_rows_fast_blk's chunk test: false when network n misses the chunk's pods'
+// addresses of its family (or the chunk has none of that family).
+static bool ip_chunk_touch(const DCidr& n, const DWordIP& ck) {
+  if (!n.valid) return true;
+  if (n.fam == 4) {
+    const uint32_t lo = n.net[3] & n.mask[3], hi = lo | ~n.mask[3];
+    return ck.m4 && !(ck.max4 < lo || ck.min4 > hi);
+  }
+  uint32_t lo[4], hi[4];
+  for (int i = 0; i < 4; i++) {
+    lo[i] = n.net[i] & n.mask[i];
+    hi[i] = lo[i] | ~n.mask[i];
+  }
+  auto lt = [](const uint32_t* a, const uint32_t* b) { return std::lexicographical_compare(a, a + 4, b, b + 4); };
+  return ck.m6 && !(lt(ck.max6, lo) || lt(hi, ck.min6));
+}
+
 static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   if (c->order_lo == lo && c->order_hi == hi && c->order_src == src) return;
   Problem& pb = c->pb;
@@ -4606,6 +4687,42 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   upload(c->ip_peers, ip);
   upload(c->ip_tests, tests);
   upload(c->ip_ex, c->plan.ip_ex);
+  {  // IP-row work items of the fused front's segments (ip_rows_items_blk): per chunk of a segment's
+     // window, its rows whose network meets the chunk's addresses (the chunk test of
+     // ip_rows_fast_blk), IPI_TOUCH to a wave, and the others 64 to a wave (their chunk flags cleared)
+    std::vector<DIPItem> items;
+    std::vector<uint32_t> il;
+    const bool one = one_window(c);
+    const uint32_t NCH = (pb.W + 63) / 64;
+    const bool on = c->ip_items_opt != 0 && c->ipw_h.size() == size_t(pb.W) + NCH && !pb.may_err;
+    for (int x = 0; x < 2; x++) {
+      c->ipi_off[x] = uint32_t(items.size());
+      if (!on || (one && x)) continue;
+      const int dlo = one ? 0 : x, dhi = one ? 2 : x + 1;
+      const uint32_t i0 = c->ri_off[dlo], n = c->ri_off[dhi] - i0;
+      uint32_t c0, nch;
+      peer_chunks(c, one ? 1 : x, c0, nch);
+      std::vector<uint32_t> hit, miss;
+      for (uint32_t ch = c0; n && ch < c0 + nch; ch++) {
+        const DWordIP& ck = c->ipw_h[pb.W + ch];
+        hit.clear();
+        miss.clear();
+        for (uint32_t r = 0; r < n; r++) (ip_chunk_touch(tests[i0 + r].cidr, ck) ? hit : miss).push_back(r);
+        for (const auto* v : {&hit, &miss}) {
+          const uint32_t per = v == &hit ? IPI_TOUCH : 64u;
+          for (size_t a = 0; a < v->size(); a += per) {
+            const uint32_t cnt = uint32_t(std::min<size_t>(per, v->size() - a));
+            items.push_back(DIPItem{ch, uint32_t(il.size()), cnt, v == &hit ? 1u : 0u});
+            il.insert(il.end(), v->begin() + a, v->begin() + a + cnt);
+          }
+        }
+      }
+    }
+    c->ipi_off[2] = uint32_t(items.size());
+    c->ip_items = on && !items.empty();
+    upload(c->ipi_items, items);
+    upload(c->ipi_list, il);
+  }
   clk.lap("done");
   c->order_lo = lo;
   c->order_hi = hi;
@@ -5000,7 +5117,8 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
   ea.reset = c->ip_rng.as<uint32_t>();
   ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
-  ea.sweep = uint32_t(c->emit_sweep);
+  ea.sweep = uint32_t(std::abs(c->emit_sweep));
+  ea.sweep_fwd = c->emit_sweep < 0 ? 1u : 0u;
   c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
     ea.row_lo[pl] = uint32_t(c->rl[pl]);
@@ -5148,6 +5266,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.ip_grp = IP_GROUP;
   fb.ipr_iv = c->ipr_iv.as<uint2>();
   fb.ipsort = c->ipsort.as<uint32_t>();
+  fb.ip_ilist = c->ipi_list.as<uint32_t>();
   for (int x = 0; x < 2; x++) {
     const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
     const uint32_t i0 = c->ri_off[dlo];
@@ -5155,6 +5274,11 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fb.tests[x] = c->ip_tests.as<DIPTest>() + i0;
     peer_chunks(c, one_win ? 1 : x, fb.ic0[x], fb.inch[x]);
     fb.nb[x] = fb.Ri[x] && fb.inch[x] ? blocks(ip_rows_blocks(fb.Ri[x], fb.inch[x], fb.ip_grp)) : 0u;
+    if (c->ip_items && fb.nb[x]) {  // the range plan's work items of this segment
+      fb.ip_items[x] = c->ipi_items.as<DIPItem>() + c->ipi_off[x];
+      fb.n_ip_items[x] = c->ipi_off[x + 1] - c->ipi_off[x];
+      fb.nb[x] = blocks((uint64_t(fb.n_ip_items[x]) + 3) / 4);
+    }
     fb.Rr[x] = one_win && x ? 0u : c->rr_off[dhi] - c->rr_off[dlo];
     fb.rtests[x] = c->ipr_tests.as<DIPRange>() + c->rr_off[dlo];
     fb.nb[9 + x] = fb.Rr[x] && fb.inch[x] ? blocks((uint64_t(fb.Rr[x]) + 3) / 4) : 0u;
@@ -5725,10 +5849,29 @@ int cyc_ctx_create(int device_id, cyc_ctx** out) {
     return true;
   }();
   (void)trace;
-  // No HIP call here: policy compilation / IR export work on a host without a GPU; the device
-  // is initialised by the first call that needs it (cyc_probe_prepare).
+  // Policy compilation / IR export work on a host without a GPU: when the device is not there, the
+  // context is created without HIP state and the first call that needs it (cyc_probe_prepare) fails.
+  // When it is, the context's stream and events are made here — the first HIP stream of a process
+  // costs ~100 ms (queue creation), paid once per context instead of inside the first prepare.
   auto* c = new cyc_ctx();
   c->device = device_id;
+  int n_dev = 0;
+  if (hipGetDeviceCount(&n_dev) == hipSuccess && device_id >= 0 && device_id < n_dev) {
+    DeviceGuard dg(device_id, false);
+    int cur = -1;
+    bool ok = hipGetDevice(&cur) == hipSuccess && cur == device_id;
+    ok = ok && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+    for (auto& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, EV_TIMING) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&c->run_done, EV_SYNC) == hipSuccess;
+    if (!ok) {  // (left to the first prepare, which reports the error)
+      for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+      if (c->run_done) (void)hipEventDestroy(c->run_done), c->run_done = nullptr;
+      if (c->stream) (void)hipStreamDestroy(c->stream), c->stream = nullptr;
+    }
+  } else {
+    (void)hipGetLastError();  // (no device: nothing to initialise)
+  }
   *out = c;
   return (int)CYC_OK;
 }
@@ -5839,15 +5982,18 @@ static int probe_prepare(cyc_ctx* c, const std::function<std::vector<ProbeConfig
   if (!c) return CYC_ERR_ARG;
   if (!c->have_policy || !c->have_res) return fail(c, CYC_ERR_ARG, "load a policy and resources first");
   return guarded(c, [&] {
+    PhaseClock clk("prepare");
     DeviceGuard dg(c->device);
+    clk.lap("device");
     if (!c->stream) {
       HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       for (auto& e : c->ev) HIPCHK(hipEventCreateWithFlags(&e, EV_TIMING));
       HIPCHK(hipEventCreateWithFlags(&c->run_done, EV_SYNC));
     }
+    clk.lap("stream");
     const std::vector<ProbeConfig> probes = probes_of();
     c->prepared = false;
-    PhaseClock clk("prepare");
+    clk.lap("probe configs");
     c->pb = build_problem(c->policy, c->res, probes, blocks);
     clk.lap("build_problem");
     drop_graph(c);
@@ -6245,7 +6391,12 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "step_events") range(0, 1), c->step_events = int(value);
     else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
     else if (n == "emit_split") range(1, 8), c->emit_split = int(value);
-    else if (n == "emit_sweep") range(0, 1 << 20), c->emit_sweep = int(value);
+    else if (n == "emit_sweep") range(-(1 << 20), 1 << 20), c->emit_sweep = int(value);
+    else if (n == "ip_items") {
+      range(-1, 1);
+      c->ip_items_opt = int(value);
+      c->order_lo = c->order_hi = -1;  // the next run re-plans the items
+    }
     else if (n == "plvt_max_mb") {
       range(0, 1 << 20);
       c->plvt_max_mb = value;
@@ -6279,6 +6430,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "emit_interleave") *value = c->emit_interleave;
   else if (n == "emit_split") *value = c->emit_split;
   else if (n == "emit_sweep") *value = c->emit_sweep;
+  else if (n == "ip_items") *value = c->ip_items_opt;
   else if (n == "plvt_max_mb") *value = c->plvt_max_mb;
   else if (n == "plvt_active") *value = c->plvt_ready ? 1 : 0;
   else if (n == "pl_wave_active") {

@@ -371,14 +371,16 @@ def _ip_stride_problem(seed, n_ns=6, per_ns=90):
 def test_ip_interval_words(gpu, seed):
     """IP rows by a test per word (ip_range = 0), from the address index wherever an IPBlock matches
     few close pods (1), and by the auto rule (index only over non-affine words), on affine addresses
-    and on addresses stepping by 256, against the oracle."""
+    and on addresses stepping by 256, with the fused front's IP rows as per-chunk work items (ip_items
+    auto) or as groups of rows per wave (0), against the oracle."""
     for pols, res, probes in (_ip_interval_problem(seed), _ip_stride_problem(seed)):
-        for ipr in (-1, 0, 1):
+        for ipr, items in ((-1, -1), (0, -1), (1, -1), (0, 0), (-1, 0)):  # (ip_items 0: a group of rows per wave)
             eng = Engine(0)
             eng.set_option("ip_range", ipr)
+            eng.set_option("ip_items", items)
             assert eng.get_option("ip_range") == ipr
             o, g = run_both(pols, res, probes, engine=eng)
-            assert_same(o, g, f"ip intervals seed {seed} ip_range {ipr}")
+            assert_same(o, g, f"ip intervals seed {seed} ip_range {ipr} ip_items {items}")
             for opts in ({"front_fused": 0}, {"graphs": 0}):
                 for k, v in opts.items():
                     eng.set_option(k, v)
@@ -713,7 +715,8 @@ def test_launch_modes_and_knobs(gpu):
                     ("step_events", 1), ("step_events", 0), ("pr_group", 5), ("pr_group", -1), ("sel_lazy", 1),
                     ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1),
                     ("emit_interleave", 1), ("emit_split", 3), ("emit_interleave", 0), ("emit_split", 2),
-                    ("emit_interleave", -1), ("emit_split", 1), ("emit_sweep", 5), ("emit_sweep", 1), ("emit_sweep", 0)):
+                    ("emit_interleave", -1), ("emit_split", 1), ("emit_sweep", 5), ("emit_sweep", 1), ("emit_sweep", -3), ("emit_sweep", 0),
+                    ("ip_items", 0), ("ip_items", 1), ("ip_items", -1)):
         eng.set_option(name, v)
         assert eng.get_option(name) == v
         assert_same(want, eng.run_host(), f"{name}={v}")
@@ -736,7 +739,7 @@ def test_launch_modes_and_knobs(gpu):
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
     for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_range", 2), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
-                    ("emit_split", 0), ("emit_split", 9), ("emit_interleave", 2), ("emit_prefetch", 1), ("emit_sweep", -1),
+                    ("emit_split", 0), ("emit_split", 9), ("emit_interleave", 2), ("emit_prefetch", 1), ("emit_sweep", 1 << 21), ("ip_items", 2),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
