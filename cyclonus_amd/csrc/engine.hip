@@ -3007,6 +3007,7 @@ struct EmitArgs {
   // keeps none of them); 0 = an XCD per contiguous eighth of the list
   uint32_t sweep;
   uint32_t sweep_fwd;  // the chunks from the start of the list (emit_sweep < 0)
+  uint32_t buf;        // 56-104 KB rows through k_emit_wide_buf<512,13> (else k_emit_wide<1024,7>)
 };
 
 // Block blockIdx.x's row r of the n-row list and its XCD x; false when the block has no row.
@@ -3722,6 +3723,12 @@ struct cyc_ctx {
                              // rows (1) or is [plane 0][plane 1] (0); -1 = auto (planes >= 8 GB)
   int emit_split = 1;   // "emit_split": a target-row emit as this many launches over consecutive parts
                         // of each plane's row list (1..8)
+  int emit_buf = 2;      // "emit_buf": 56-104 KB plane rows through 1024 x 7 buffer-op blocks (2), 512 x 13
+                         // buffer-op blocks (1) or 1024 x 7 flat-address blocks (0).  The emit's rate depends
+                         // on the planes' physical placement; over 14 placements of config #3's planes 1024 x 7
+                         // averaged 3.389 ms per step against 3.542 for 512 x 13 (1-2 % behind on the best
+                         // placements, up to 8 % ahead on the worst; a target shard at N = 8 -5.7 %),
+                         // profiles/r05_plane_placement.txt, r05_shard_ab.txt
   int emit_sweep = 0;    // "emit_sweep": EmitArgs::sweep, rows per XCD chunk of a target-row emit (0 = off):
                          // -2 to -4 % per step on some plane placements, +6 % on others (config #3 over 5
                          // placements in one process: mean +0.2 %, profiles/r05_plane_placement.txt)
@@ -5041,17 +5048,27 @@ static const char* enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64
   const uint64_t row_bytes = ea.row_words * 8;
   // A 512 x 13 one-pass block with flat addresses held 84 VGPRs, 5 waves a SIMD, and ran config #3
   // 3.5 % slower per step (profiles/r03_emit_ab.txt); through buffer ops it holds 54 (8 waves a
-  // SIMD) and beats 1024 x 7: config #3 emit 3000 vs 3058-3070 us (profiles/r04_emit_buf_ab.txt).
+  // SIMD) and beats flat 1024 x 7 on a good plane placement: config #3 emit 3000 vs 3058-3070 us
+  // (profiles/r04_emit_buf_ab.txt) — but over many placements 1024 x 7 through buffer ops wins on
+  // average (cyc_ctx::emit_buf).
   // (128 x 13 buffer blocks for config #4's 25 KB rows lost: 442-447 vs 419-424 us.)
-  if (row_bytes > 512 * 7 * 16 && row_bytes <= 512 * 13 * 16) {  // 56-104 KB: config #3's 98 KB rows, one pass
+  if (row_bytes > 512 * 7 * 16 && row_bytes <= 512 * 13 * 16 && ea.buf == 1) {  // 56-104 KB: config #3's 98 KB rows, one pass
     k_emit_wide_buf<512, 13><<<g, 512, 0, st>>>(ea);
     return "k_emit_wide_buf<512,13>";
+  } else if (row_bytes > 512 * 7 * 16 && row_bytes <= 1024 * 7 * 16 && ea.buf == 2) {
+    k_emit_wide_buf<1024, 7><<<g, 1024, 0, st>>>(ea);
+    return "k_emit_wide_buf<1024,7>";
   } else if (row_bytes > 512 * 7 * 16) {  // > 104 KB: 1024 x 7 passes
     k_emit_wide<1024, 7><<<g, 1024, 0, st>>>(ea);
     return "k_emit_wide<1024,7>";
   } else if (row_bytes > 256 * 8 * 16) {  // 32-56 KB: 512 x 7 (source shards at N = 2)
     k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
     return "k_emit_wide<512,7>";
+  } else if (row_bytes >= EMIT_WIDE_MIN && row_bytes <= 32768 && ea.buf >= 3) {  // (diagnostic shapes, emit_buf 3-5)
+    if (ea.buf == 3) k_emit_wide_buf<256, 8><<<g, 256, 0, st>>>(ea);
+    else if (ea.buf == 4) k_emit_wide_buf<512, 4><<<g, 512, 0, st>>>(ea);
+    else k_emit_wide_buf<1024, 2><<<g, 1024, 0, st>>>(ea);
+    return ea.buf == 3 ? "k_emit_wide_buf<256,8>" : ea.buf == 4 ? "k_emit_wide_buf<512,4>" : "k_emit_wide_buf<1024,2>";
   } else if (row_bytes >= EMIT_WIDE_MIN) {  // 256-thread single pass (16-32 KB rows)
     const uint64_t need = (ea.row_words / 2 + 255) / 256;
     if (need <= 2) k_emit_wide<256, 2><<<g, 256, 0, st>>>(ea);
@@ -5119,6 +5136,7 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
   ea.sweep = uint32_t(std::abs(c->emit_sweep));
   ea.sweep_fwd = c->emit_sweep < 0 ? 1u : 0u;
+  ea.buf = uint32_t(c->emit_buf);
   c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
     ea.row_lo[pl] = uint32_t(c->rl[pl]);
@@ -5193,15 +5211,15 @@ static bool front_fused_ok(const cyc_ctx* c) {
 
 // In-place class rows: the fused front with both output planes given.
 // Auto (-1): when the rows' identities are >= 1/16 of the rows (PM builds: config #4 emit -8 %,
-// #3u -7 %), and for identity-set (IDO) target-row runs: config #3's class rows are 2 % of its rows,
+// #3u -7 %), and for identity-set (IDO) runs: config #3's class rows are 2 % of its rows,
 // and writing them into the planes saves their 400 MB of separate writes (3.286 -> 3.191 ms/step,
 // profiles/r05_inplace_sweep_ab.txt; over 5 plane placements in one process -2.1 / -0.0 / -0.1 /
-// -2.8 / -2.2 %, never slower: profiles/r05_plane_placement.txt; in round 2, before the current
-// launch E, it lost 1 %).
+// -2.8 / -2.2 %, never slower: profiles/r05_plane_placement.txt; a source shard at N = 8 -1.2 %,
+// r05_shard_ab.txt; in round 2, before the current launch E, it lost 1 %).
 static bool inplace_ok(const cyc_ctx* c, const uint64_t* d_in, const uint64_t* d_eg) {
   if (!c->class_inplace || !d_in || !d_eg || !front_fused_ok(c) || !c->pb.blocks.empty()) return false;
   const uint64_t rows = uint64_t(std::max<int64_t>((c->rh[0] - c->rl[0] + c->rh[1] - c->rl[1]) / 2, 1));
-  return c->class_inplace == 1 || uint64_t(c->n_act[0] + c->n_act[1]) * 16 >= 2 * rows || (ido_mode(c) && !c->order_src);
+  return c->class_inplace == 1 || uint64_t(c->n_act[0] + c->n_act[1]) * 16 >= 2 * rows || ido_mode(c);
 }
 
 // out_in / out_eg non-null: the class rows go straight into those planes (in-place class rows; the
@@ -6392,6 +6410,7 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
     else if (n == "emit_split") range(1, 8), c->emit_split = int(value);
     else if (n == "emit_sweep") range(-(1 << 20), 1 << 20), c->emit_sweep = int(value);
+    else if (n == "emit_buf") range(0, 5), c->emit_buf = int(value);
     else if (n == "ip_items") {
       range(-1, 1);
       c->ip_items_opt = int(value);
@@ -6431,6 +6450,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "emit_split") *value = c->emit_split;
   else if (n == "emit_sweep") *value = c->emit_sweep;
   else if (n == "ip_items") *value = c->ip_items_opt;
+  else if (n == "emit_buf") *value = c->emit_buf;
   else if (n == "plvt_max_mb") *value = c->plvt_max_mb;
   else if (n == "plvt_active") *value = c->plvt_ready ? 1 : 0;
   else if (n == "pl_wave_active") {

@@ -356,7 +356,9 @@ int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
  *                 straight into the output planes at its first member pod's row and the emit copies
  *                 them to the class's other pods (1), or they go to a buffer of their own the emit
  *                 copies from (0); auto = 1 when the rows' identities are >= 1/16 of the rows or
- *                 the run is a target-row run of an identity-set build
+ *                 the run is an identity-set build
+ *   "emit_buf"    2 (default) / 1 / 0: plane rows of 56-104 KB emitted by 1024 x 7 blocks through buffer
+ *                 loads / stores, 512 x 13 buffer blocks, or 1024 x 7 flat-address blocks
  *                 ("class_inplace_active" reports the choice of the last run's row range)
  *   "sel_lazy"    -1 (default: auto) / 0 / 1: on the fused front, label selectors are evaluated where
  *                 membership and pod-peer rows / identity sets use them (1) instead of as the dense

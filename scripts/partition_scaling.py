@@ -2,7 +2,7 @@
 (what bench.py times) of the slowest of ranks 0, N/2 and N-1 for N = 1, 2, 4, 8, target rows and
 source rows interleaved on one box.
 
-    python scripts/partition_scaling.py config3 [steps=20] [reps=2]
+    python scripts/partition_scaling.py config3 [steps=20] [reps=2] [parts=target,source] [NAME=VALUE ...]
 """
 import json
 import os
@@ -19,10 +19,13 @@ from cyclonus_amd.shard import shard_range
 
 name = sys.argv[1] if len(sys.argv) > 1 else "config3"
 kw = dict(a.split("=") for a in sys.argv[2:])
-steps, reps = int(kw.get("steps", 20)), int(kw.get("reps", 2))
+steps, reps = int(kw.pop("steps", 20)), int(kw.pop("reps", 2))
+parts = kw.pop("parts", "target,source").split(",")
 data = synth.CONFIGS[name]()
 eng = Engine(0).build_policies(json.dumps(data["policies"])).load_resources(json.dumps(data["resources"]))
 sh = eng.prepare(data["probes"])
+for k, v in kw.items():  # cyc_set_option NAME=VALUE
+    eng.set_option(k, int(v))
 P, K, W = sh["pods"], sh["slots"], sh["words"]
 d_in = torch.empty((P * K * W,), dtype=torch.int64, device="cuda")
 d_eg = torch.empty((P * K * W,), dtype=torch.int64, device="cuda")
@@ -44,7 +47,7 @@ def step_ms(lo, hi, part):
 print(f"{name}: P={P} K={K} W={W} steps={steps} reps={reps}", flush=True)
 base = {}
 for n in (1, 2, 4, 8):
-    for part in ("target", "source"):
+    for part in parts:
         worst, per = 0.0, []
         for rank in sorted({0, n // 2, n - 1}):
             lo, hi = shard_range(P, n, rank, part)
