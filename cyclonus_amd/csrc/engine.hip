@@ -5064,12 +5064,9 @@ static const char* enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64
   } else if (row_bytes > 256 * 8 * 16) {  // 32-56 KB: 512 x 7 (source shards at N = 2)
     k_emit_wide<512, 7><<<g, 512, 0, st>>>(ea);
     return "k_emit_wide<512,7>";
-  } else if (row_bytes >= EMIT_WIDE_MIN && row_bytes <= 32768 && ea.buf >= 3) {  // (diagnostic shapes, emit_buf 3-5)
-    if (ea.buf == 3) k_emit_wide_buf<256, 8><<<g, 256, 0, st>>>(ea);
-    else if (ea.buf == 4) k_emit_wide_buf<512, 4><<<g, 512, 0, st>>>(ea);
-    else k_emit_wide_buf<1024, 2><<<g, 1024, 0, st>>>(ea);
-    return ea.buf == 3 ? "k_emit_wide_buf<256,8>" : ea.buf == 4 ? "k_emit_wide_buf<512,4>" : "k_emit_wide_buf<1024,2>";
-  } else if (row_bytes >= EMIT_WIDE_MIN) {  // 256-thread single pass (16-32 KB rows)
+  } else if (row_bytes >= EMIT_WIDE_MIN) {  // 256-thread single pass (16-32 KB rows; buffer-op 256 x 8,
+                                            // 512 x 4 and 1024 x 2 blocks were no better over 4 plane
+                                            // placements of config #4, profiles/r05_plane_placement.txt)
     const uint64_t need = (ea.row_words / 2 + 255) / 256;
     if (need <= 2) k_emit_wide<256, 2><<<g, 256, 0, st>>>(ea);
     else if (need <= 4) k_emit_wide<256, 4><<<g, 256, 0, st>>>(ea);
@@ -6410,7 +6407,7 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
     else if (n == "emit_split") range(1, 8), c->emit_split = int(value);
     else if (n == "emit_sweep") range(-(1 << 20), 1 << 20), c->emit_sweep = int(value);
-    else if (n == "emit_buf") range(0, 5), c->emit_buf = int(value);
+    else if (n == "emit_buf") range(0, 2), c->emit_buf = int(value);
     else if (n == "ip_items") {
       range(-1, 1);
       c->ip_items_opt = int(value);

@@ -27,7 +27,8 @@ pairs, steps, reps = int(kw.pop("pairs", 4)), int(kw.pop("steps", 20)), int(kw.p
 # alt=name:v,name:v[;name:v...]: option sets run on every pair besides the defaults
 alts = [dict(x.split(":") for x in grp.split(",") if x) for grp in kw.pop("alt", "").split(";") if grp]
 n_hip, n_contig = int(kw.pop("hip", 0)), int(kw.pop("contig", 0))
-data = synth.CONFIGS["config3"]()
+name = kw.pop("config", "config3")
+data = synth.CONFIGS[name]()
 eng = Engine(0)
 sh = prepare_flat(eng, data["policies"], data["resources"], data["probes"])
 for k, v in kw.items():
@@ -59,7 +60,7 @@ for flags, cnt, kind in ((0, n_hip, "hipMalloc"), (4, n_contig, "contiguous")):
         planes.append((Raw(flags), Raw(flags)))
         kinds.append(kind)
 pairs = len(planes)
-print(f"config3: {pairs} plane pairs of 2 x {n * 8 / 1e9:.2f} GB, options {kw}", flush=True)
+print(f"{name}: {pairs} plane pairs of 2 x {n * 8 / 1e9:.2f} GB, options {kw}", flush=True)
 for i, (a, b) in enumerate(planes):
     print(f"pair {i} ({kinds[i]}): ingress {a.data_ptr():#x} egress {b.data_ptr():#x} "
           f"(mod 1 GiB {a.data_ptr() % (1 << 30):#x} / {b.data_ptr() % (1 << 30):#x})", flush=True)

@@ -739,7 +739,7 @@ def test_launch_modes_and_knobs(gpu):
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
     for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_range", 2), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
-                    ("emit_split", 0), ("emit_split", 9), ("emit_interleave", 2), ("emit_prefetch", 1), ("emit_sweep", 1 << 21), ("ip_items", 2), ("emit_buf", 6),
+                    ("emit_split", 0), ("emit_split", 9), ("emit_interleave", 2), ("emit_prefetch", 1), ("emit_sweep", 1 << 21), ("ip_items", 2), ("emit_buf", 3),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
