@@ -43,6 +43,7 @@ EXPORTS = [
     "cyc_set_option",
     "cyc_get_option",
     "cyc_query_traffic",
+    "cyc_query_traffic_tables",
     "cyc_query_traffic_targets",
     "cyc_query_targets",
     "cyc_table_run",
@@ -129,6 +130,7 @@ def lib():
         L.cyc_set_option.argtypes = [vp, cp, i64]
         L.cyc_get_option.argtypes = [vp, cp, ctypes.POINTER(i64)]
         L.cyc_query_traffic.argtypes = [vp, cp, sz, vp, i64]
+        L.cyc_query_traffic_tables.argtypes = [vp, vp, vp, i64]
         L.cyc_query_traffic_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]
         L.cyc_query_targets.argtypes = [vp, cp, sz, vp, sz, ctypes.POINTER(sz)]
         L.cyc_table_run.argtypes = [vp, i64, i64, ctypes.POINTER(vp)]

@@ -6597,6 +6597,17 @@ int cyc_query_traffic(cyc_ctx* c, const char* js, size_t len, uint8_t* out, int6
   });
 }
 
+int cyc_query_traffic_tables(cyc_ctx* c, const cyc_traffic_tables* t, uint8_t* out, int64_t n) {
+  if (!c || !t) return CYC_ERR_ARG;
+  if (!c->have_policy) return fail(c, CYC_ERR_ARG, "load a policy first");
+  return guarded(c, [&]() -> int {
+    auto ts = load_traffic_tables(*t);
+    if (int64_t(ts.size()) > n || (!ts.empty() && !out)) return fail(c, CYC_ERR_ARG, "output buffer smaller than the traffic list");
+    if (ts.empty()) return (int)CYC_OK;
+    return run_query(c, ts, out, nullptr);
+  });
+}
+
 static void json_str(std::string& o, const std::string& v) {
   o += '"';
   for (unsigned char ch : v) {

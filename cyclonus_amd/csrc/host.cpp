@@ -1895,6 +1895,58 @@ std::vector<QueryTraffic> load_traffics(const Node& n) {
   return out;
 }
 
+// The flat form of load_traffics (include/cyclonus_hip.h cyc_traffic_tables): every index and
+// offset validated, CYC_ERR_ARG naming the first bad one.
+std::vector<QueryTraffic> load_traffic_tables(const cyc_traffic_tables& t) {
+  const FlatCheck ck{"cyc_traffic_tables"};
+  if (t.n < 0 || t.n >= (int64_t(1) << 31)) ck.bad("n = " + std::to_string(t.n) + " out of range");
+  if (t.str.n < 0) ck.bad("negative str.n");
+  ck.offsets(t.str.off, t.str.n, "str.off");
+  if (t.str.n && t.str.off[t.str.n] > t.str.off[0]) ck.need(t.str.bytes, "str.bytes");
+  auto S = [&](int64_t i, const char* name, int64_t at) {
+    ck.index(i, t.str.n, name, at);
+    return std::string(t.str.bytes + t.str.off[i], size_t(t.str.off[i + 1] - t.str.off[i]));
+  };
+  std::vector<QueryTraffic> out(size_t(t.n));
+  if (!t.n) return out;
+  const int64_t ne = 2 * t.n;
+  ck.need(t.internal, "internal");
+  ck.need(t.ip, "ip");
+  ck.need(t.port, "port");
+  ck.need(t.port_name, "port_name");
+  ck.need(t.protocol, "protocol");
+  const int64_t nl = t.label_off ? ck.offsets(t.label_off, ne, "label_off") : 0;
+  const int64_t nn = t.ns_label_off ? ck.offsets(t.ns_label_off, ne, "ns_label_off") : 0;
+  if (t.label_off && nl > t.label_off[0]) {
+    ck.need(t.label_key, "label_key");
+    ck.need(t.label_val, "label_val");
+  }
+  if (t.ns_label_off && nn > t.ns_label_off[0]) {
+    ck.need(t.ns_label_key, "ns_label_key");
+    ck.need(t.ns_label_val, "ns_label_val");
+  }
+  for (int64_t e = 0; e < ne; e++) {
+    QueryTraffic& q = out[size_t(e / 2)];
+    QueryEnd& x = e % 2 ? q.dst : q.src;
+    x.ip = S(t.ip[e], "ip", e);
+    x.external = !t.internal[e];
+    if (x.external) continue;
+    ck.need(t.ns, "ns");
+    x.ns = S(t.ns[e], "ns", e);
+    if (t.label_off)  // a Go map: a repeated key, if given, keeps its last value
+      for (int64_t j = t.label_off[e]; j < t.label_off[e + 1]; j++) x.labels[S(t.label_key[j], "label_key", j)] = S(t.label_val[j], "label_val", j);
+    if (t.ns_label_off)
+      for (int64_t j = t.ns_label_off[e]; j < t.ns_label_off[e + 1]; j++)
+        x.ns_labels[S(t.ns_label_key[j], "ns_label_key", j)] = S(t.ns_label_val[j], "ns_label_val", j);
+  }
+  for (int64_t i = 0; i < t.n; i++) {
+    out[size_t(i)].port = t.port[i];
+    out[size_t(i)].port_name = S(t.port_name[i], "port_name", i);
+    out[size_t(i)].proto = S(t.protocol[i], "protocol", i);
+  }
+  return out;
+}
+
 // analyze --mode query-target input (analyze.go:163-187): a JSON list of QueryTargetPod
 // {Namespace, Labels}; each becomes a traffic from the pod to itself (only membership is used).
 std::vector<QueryTraffic> load_target_pods(const Node& n) {

@@ -250,6 +250,7 @@ struct QueryTraffic {
   std::string port_name, proto;
 };
 std::vector<QueryTraffic> load_traffics(const json::Node& n);
+std::vector<QueryTraffic> load_traffic_tables(const cyc_traffic_tables& t);
 std::vector<QueryTraffic> load_target_pods(const json::Node& n);
 Problem build_query_problem(const PolicyIR& pol, const std::vector<QueryTraffic>& ts, std::vector<uint32_t>& ext,
                             std::vector<uint32_t>& tdesc);

@@ -198,6 +198,15 @@ class Engine:
         check(self._ctx, lib().cyc_query_traffic(self._ctx, b, len(b), out.ctypes.data, n))
         return [(bool(o & 1), bool(o & 2)) for o in out[:n]]
 
+    def query_traffic_tables(self, traffics):
+        """query_traffic through the flat tables (cyc_query_traffic_tables: no JSON)."""
+        from . import flat
+
+        t = traffics if isinstance(traffics, flat.TrafficTables) else flat.TrafficTables(traffics)
+        out = np.zeros(max(t.n, 1), np.uint8)
+        check(self._ctx, lib().cyc_query_traffic_tables(self._ctx, ctypes.byref(t.c), out.ctypes.data, t.n))
+        return [(bool(o & 1), bool(o & 2)) for o in out[:t.n]]
+
     def _json_out(self, fn, doc):
         b = _bytes(doc)
         need = ctypes.c_size_t(0)

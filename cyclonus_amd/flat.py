@@ -31,6 +31,12 @@ class ResourceTablesC(ctypes.Structure):
                 ("cont_proto", i32p), ("cont_port_name", i32p), ("pod_nil", u8p)]
 
 
+class TrafficTablesC(ctypes.Structure):
+    _fields_ = [("str", Strings), ("n", ctypes.c_int64), ("internal", u8p), ("ip", i32p), ("ns", i32p),
+                ("label_off", i64p), ("label_key", i32p), ("label_val", i32p), ("ns_label_off", i64p),
+                ("ns_label_key", i32p), ("ns_label_val", i32p), ("port", i32p), ("port_name", i32p), ("protocol", i32p)]
+
+
 class ProbeConfigC(ctypes.Structure):
     _fields_ = [("all_available", ctypes.c_int32), ("port_is_name", ctypes.c_int32), ("port", ctypes.c_int32),
                 ("port_name", ctypes.c_char_p), ("port_name_len", ctypes.c_int64),
@@ -143,6 +149,50 @@ class ResourceTables:
         t.cont_port_name = _arr(keep, cpn, np.int32, i32p)
         t.pod_nil = _arr(keep, pnil, np.uint8, u8p)
         self.c, self._keep = t, keep
+
+
+class TrafficTables:
+    """cyc_traffic_tables of matcher.Traffic values {"Source": peer, "Destination": peer, "ResolvedPort",
+    "ResolvedPortName", "Protocol"}, peer = {"Internal": None | {"PodLabels", "NamespaceLabels",
+    "Namespace"}, "IP"} (pkg/matcher/traffic.go:11-18): what a Go JobRunner passes per []*Job."""
+
+    def __init__(self, traffics):
+        S, keep = _Interner(), []
+        internal, ip, ns, lcnt, lk, lv, ncnt, nk, nv = ([] for _ in range(9))
+        port, pname, proto = [], [], []
+        for t in traffics:
+            for end in (t.get("Source") or {}, t.get("Destination") or {}):
+                inner = end.get("Internal")
+                internal.append(0 if inner is None else 1)
+                ip.append(S(end.get("IP")))
+                inner = inner or {}
+                ns.append(S(inner.get("Namespace")))
+                labels, nsl = inner.get("PodLabels") or {}, inner.get("NamespaceLabels") or {}
+                lcnt.append(len(labels))
+                lk += [S(k) for k in labels]
+                lv += [S(v) for v in labels.values()]
+                ncnt.append(len(nsl))
+                nk += [S(k) for k in nsl]
+                nv += [S(v) for v in nsl.values()]
+            port.append(int(t.get("ResolvedPort") or 0))
+            pname.append(S(t.get("ResolvedPortName")))
+            proto.append(S(t.get("Protocol")))
+        c = TrafficTablesC()
+        c.str = S.table(keep)
+        c.n = len(port)
+        c.internal = _arr(keep, internal, np.uint8, u8p)
+        c.ip = _arr(keep, ip, np.int32, i32p)
+        c.ns = _arr(keep, ns, np.int32, i32p)
+        c.label_off = _arr(keep, _offsets(lcnt), np.int64, i64p)
+        c.label_key = _arr(keep, lk, np.int32, i32p)
+        c.label_val = _arr(keep, lv, np.int32, i32p)
+        c.ns_label_off = _arr(keep, _offsets(ncnt), np.int64, i64p)
+        c.ns_label_key = _arr(keep, nk, np.int32, i32p)
+        c.ns_label_val = _arr(keep, nv, np.int32, i32p)
+        c.port = _arr(keep, port, np.int32, i32p)
+        c.port_name = _arr(keep, pname, np.int32, i32p)
+        c.protocol = _arr(keep, proto, np.int32, i32p)
+        self.c, self.n, self._keep = c, len(port), keep
 
 
 class ProbeConfigs:

@@ -6,8 +6,8 @@
 
 Traffic objects are the reference's matcher.Traffic JSON shape (traffic.go:11-81): dicts with
 Source / Destination {"Internal": {"PodLabels", "NamespaceLabels", "Namespace"} | None, "IP"},
-"ResolvedPort", "ResolvedPortName", "Protocol".  Evaluation runs on the GPU (cyc_query_traffic);
-a Go panic of the reference surfaces as cyclonus_amd.CyclonusPanic with the same message.
+"ResolvedPort", "ResolvedPortName", "Protocol".  Evaluation runs on the GPU (cyc_query_traffic_tables,
+or cyc_query_traffic_targets for the target lists); a Go panic of the reference surfaces as cyclonus_amd.CyclonusPanic with the same message.
 """
 from __future__ import annotations
 
@@ -103,8 +103,8 @@ class Policy:
     def is_traffic_allowed_batch(self, traffics, targets: bool = False):
         """One GPU batch; targets=True also returns the DirectionResult target lists."""
         docs = [_traffic_json(t) for t in traffics]
-        if not targets:
-            res = self.engine.query_traffic(docs)
+        if not targets:  # the flat tables a Go JobRunner passes (cyc_query_traffic_tables), no JSON
+            res = self.engine.query_traffic_tables(docs)
             return [AllowedResult(DirectionResult(i), DirectionResult(e)) for i, e in res]
         out = []
         for r in self.engine.query_traffic_targets(docs):

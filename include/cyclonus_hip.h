@@ -382,6 +382,30 @@ int cyc_get_option(cyc_ctx* ctx, const char* name, int64_t* value);
  * out[i] = ingress | egress << 1 (allowed bits).  Needs only a loaded policy. */
 int cyc_query_traffic(cyc_ctx* ctx, const char* traffic_json, size_t len, uint8_t* out, int64_t n);
 
+/* matcher.Traffic values (pkg/matcher/traffic.go:11-18) as flat tables, the form a cgo
+ * SimulatedJobRunner.RunJobs over explicit []*Job (jobrunner.go:68-94, Job.Traffic job.go:81-103)
+ * passes without JSON.  Endpoint 2i is traffic i's Source, 2i + 1 its Destination; an endpoint is
+ * internal when internal[e] is 1 (TrafficPeer.Internal != nil: its namespace, pod labels and
+ * namespace labels are read), external otherwise (only its IP).  A nil label map is given as an
+ * empty range (the matchers read nil and empty maps alike); label_off / ns_label_off may be NULL
+ * when no endpoint has labels. */
+typedef struct {
+  cyc_strings str;
+  int64_t n;                         /* traffics */
+  const uint8_t* internal;           /* [2n] */
+  const int32_t* ip;                 /* [2n] TrafficPeer.IP */
+  const int32_t* ns;                 /* [2n] Internal.Namespace (internal endpoints) */
+  const int64_t* label_off;          /* [2n + 1] into label_key / label_val: Internal.PodLabels */
+  const int32_t *label_key, *label_val;
+  const int64_t* ns_label_off;       /* [2n + 1] into ns_label_key / ns_label_val: Internal.NamespaceLabels */
+  const int32_t *ns_label_key, *ns_label_val;
+  const int32_t* port;               /* [n] ResolvedPort */
+  const int32_t* port_name;          /* [n] ResolvedPortName */
+  const int32_t* protocol;           /* [n] Protocol (the raw string) */
+} cyc_traffic_tables;
+/* cyc_query_traffic over flat tables: out[i] = ingress | egress << 1; panics as cyc_query_traffic. */
+int cyc_query_traffic_tables(cyc_ctx* ctx, const cyc_traffic_tables* tables, uint8_t* out, int64_t n);
+
 /* query-traffic with the DirectionResult target lists (replaces Policy.IsTrafficAllowed's
  * AllowedResult, policy.go:84-96,131-174, as printed by analyze.go:209-225).  out_json gets a
  * JSON array, one object per traffic:

@@ -93,6 +93,26 @@ def test_probe_configs():
     assert ctypes.string_at(addr, 4) == b"T\x00CP"
 
 
+def test_traffic_tables():
+    """cyc_traffic_tables (the flat matcher.Traffic a Go JobRunner passes): endpoints, labels, ports as
+    indices; malformed tables are refused with the offending index before any device work."""
+    tr = [{"Source": {"Internal": {"PodLabels": {"a": "b"}, "NamespaceLabels": None, "Namespace": "x"}, "IP": "10.0.0.1"},
+           "Destination": {"Internal": None, "IP": "1.2.3.4"}, "ResolvedPort": 80, "ResolvedPortName": "", "Protocol": "TCP"}]
+    t = flat.TrafficTables(tr)
+    assert t.n == 1 and list(np.ctypeslib.as_array(t.c.internal, (2,))) == [1, 0]
+    e = Engine(0).build_policies(random_problem(8100)[0])
+    bad = np.array([99, 0], np.int32)
+    t.c.ip = bad.ctypes.data_as(flat.i32p)
+    out = (ctypes.c_uint8 * 1)()
+    rc = _lib.lib().cyc_query_traffic_tables(e._ctx, ctypes.byref(t.c), out, 1)
+    assert rc == _lib.ERR_ARG and "ip[0] = 99 out of range" in _lib.lib().cyc_last_error(e._ctx).decode()
+    t = flat.TrafficTables(tr)
+    rc = _lib.lib().cyc_query_traffic_tables(e._ctx, ctypes.byref(t.c), out, 0)  # output smaller than the list
+    assert rc == _lib.ERR_ARG and "smaller" in _lib.lib().cyc_last_error(e._ctx).decode()
+    rc = _lib.lib().cyc_query_traffic_tables(Engine(0)._ctx, ctypes.byref(t.c), out, 1)
+    assert rc == _lib.ERR_ARG  # no policy loaded
+
+
 def test_malformed_tables_refused():
     res = {"Namespaces": {"x": {"a": "b"}}, "Pods": [{"Namespace": "x", "Name": "p", "IP": "10.0.0.1",
                                                       "Labels": {"a": "b"}, "Containers": []}]}

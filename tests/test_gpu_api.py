@@ -62,12 +62,13 @@ def test_query_traffic_random(gpu, bad):
                 break
             want.append(res)
         pol = build_network_policies(True, pols)
-        if want_panic is not None:
-            with pytest.raises(CyclonusPanic) as e:
-                pol.engine.query_traffic(traffics)
-            assert e.value.msg == want_panic, seed
-        else:
-            assert pol.engine.query_traffic(traffics) == want, seed
+        for query in (pol.engine.query_traffic, pol.engine.query_traffic_tables):  # JSON and flat tables
+            if want_panic is not None:
+                with pytest.raises(CyclonusPanic) as e:
+                    query(traffics)
+                assert e.value.msg == want_panic, seed
+            else:
+                assert query(traffics) == want, seed
 
 
 def test_readme_queries_gpu(gpu):
