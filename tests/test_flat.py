@@ -109,7 +109,8 @@ def test_traffic_tables():
     t = flat.TrafficTables(tr)
     rc = _lib.lib().cyc_query_traffic_tables(e._ctx, ctypes.byref(t.c), out, 0)  # output smaller than the list
     assert rc == _lib.ERR_ARG and "smaller" in _lib.lib().cyc_last_error(e._ctx).decode()
-    rc = _lib.lib().cyc_query_traffic_tables(Engine(0)._ctx, ctypes.byref(t.c), out, 1)
+    bare = Engine(0)
+    rc = _lib.lib().cyc_query_traffic_tables(bare._ctx, ctypes.byref(t.c), out, 1)
     assert rc == _lib.ERR_ARG  # no policy loaded
 
 
