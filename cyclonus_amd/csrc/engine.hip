@@ -3062,6 +3062,16 @@ __device__ __forceinline__ void emit_status(const EmitArgs& a) {
 // (plain stores: config #4 emit +45 %, profiles/r03_emit_ab.txt).
 __device__ __forceinline__ void emit_store(u64x2 v, u64x2* p) { __builtin_nontemporal_store(v, p); }
 
+// i / n for i < 2^22 through a float reciprocal (n block-uniform): the exact quotient after one
+// correction either way — a 32-bit integer division by a run-time value is ~40 instructions, once per
+// 16-byte chunk in the multi-row emit kernels.
+__device__ __forceinline__ uint32_t div_small(uint32_t i, uint32_t n, float inv) {
+  uint32_t q = uint32_t(float(i) * inv);
+  if (q * n > i) q--;
+  else if ((q + 1) * n <= i) q++;
+  return q;
+}
+
 // Rows of an odd word count or planes not 16-byte aligned: 8-byte copies, one block per row.
 __global__ __launch_bounds__(256) void k_emit_words(EmitArgs a) {
   emit_status(a);
@@ -3116,13 +3126,14 @@ __global__ __launch_bounds__(BS) void k_emit_flat(EmitArgs a) {
   }
   __syncthreads();
   const uint32_t n2 = uint32_t(a.row_words / 2), tot = nr * n2;
+  const float inv = 1.0f / float(n2);
   for (uint32_t i0 = threadIdx.x; i0 < tot; i0 += BS * UNROLL) {
     u64x2 v[UNROLL];
     uint32_t row[UNROLL], col[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       const uint32_t i = i0 + u * BS;
-      row[u] = i / n2;
+      row[u] = div_small(i, n2, inv);
       col[u] = i - row[u] * n2;
       if (i < tot) v[u] = s_src[row[u]][col[u]];
     }
@@ -3220,14 +3231,30 @@ __global__ __launch_bounds__(BS) void k_emit_units(EmitArgs a) {
     }
   }
   __syncthreads();
+  if (a.unit_rows[pl] == 1) {  // a unit of one long row (a source shard's egress rows): the copy of
+                               // k_emit_wide_buf, chunk offsets in the scalar offset, no per-chunk division
+    if (!s_cnt) return;
+    const uint32_t bytes = uint32_t(a.pl_words[pl] * 8);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<u64x2*>(s_src[0]), 0, bytes, BUF_RSRC_W3);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(s_dst[0], 0, bytes, BUF_RSRC_W3);
+    for (uint32_t x0 = 0; x0 < bytes; x0 += BS * UNROLL * 16) {
+      u32x4 v[UNROLL];
+#pragma unroll
+      for (int q = 0; q < UNROLL; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, x0 + q * BS * 16, 0);
+#pragma unroll
+      for (int q = 0; q < UNROLL; q++) __builtin_amdgcn_raw_buffer_store_b128(v[q], rd, threadIdx.x * 16, x0 + q * BS * 16, 2);  // nt
+    }
+    return;
+  }
   const uint32_t n2 = uint32_t(a.pl_words[pl] / 2), tot = s_cnt * n2;
+  const float inv = 1.0f / float(n2);
   for (uint32_t i0 = threadIdx.x; i0 < tot; i0 += BS * UNROLL) {
     u64x2 v[UNROLL];
     uint32_t row[UNROLL], col[UNROLL];
 #pragma unroll
     for (int q = 0; q < UNROLL; q++) {
       const uint32_t i = i0 + q * BS;
-      row[q] = i / n2;
+      row[q] = div_small(i, n2, inv);
       col[q] = i - row[q] * n2;
       if (i < tot) v[q] = s_src[row[q]][col[q]];
     }

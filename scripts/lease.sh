@@ -2,7 +2,7 @@
 # and the first failing step ends the call (set -e; no GPU step runs after a fault or a timeout).
 #   gpurun -- 'bash scripts/lease.sh OUT "tests [-k EXPR]" "smoke" "bench CFG [bench args]" ...'
 # steps:
-#   tests [pytest args]        GPU test suite (-m gpu)
+#   tests [pytest args]        GPU test suite (-m gpu; K=a+or+b selects -k "a or b")
 #   smoke                      __graft_entry__.smoke()
 #   bench CFG [args]           python bench.py --config CFG [args]       -> bench_CFG[_TAG].log
 #   prof CFG                   bench line, rocprofv3 --kernel-trace --stats of the bench command,
@@ -37,7 +37,9 @@ for spec in "$@"; do
   [ -n "$CYC_HIP_LIB" ] && tag=${tag}_$(basename $(dirname $CYC_HIP_LIB))  # library variant runs apart
   echo "[lease] $(date +%T) $spec" >> $OUT/steps.log
   case $step in
-    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $OUT/gpu_tests.log 2>&1 ;;
+    tests)  # (K=a+or+b: pytest -k "a or b" — a step's words cannot hold spaces)
+      targs=(); for a in "$@"; do if [[ $a == K=* ]]; then targs+=(-k "$(echo "${a#K=}" | tr '+' ' ')"); else targs+=("$a"); fi; done
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${targs[@]}" > $OUT/gpu_tests.log 2>&1 ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 300 python -u bench.py --config "$@" > $OUT/bench_$tag.log 2>&1 ;;
     prof)
