@@ -31,17 +31,23 @@ def shard_range(P: int, world: int, rank: int, partition: str = "target"):
 
 
 def _gather(send, world, group):
-    """All-gather equal-shaped tensors -> list of world tensors (gloo: list form; RCCL: one buffer)."""
-    import torch
+    """All-gather equal-shaped tensors into one [world, ...] buffer: a single all_gather_into_tensor
+    (RCCL and gloo both take the concatenated [world * n0, ...] output form)."""
     import torch.distributed as dist
 
-    if dist.get_backend(group) == "gloo":
-        parts = [torch.empty_like(send) for _ in range(world)]
-        dist.all_gather(parts, send, group=group)
-        return parts
-    out = send.new_empty((world,) + tuple(send.shape))
+    out = send.new_empty((world * send.shape[0],) + tuple(send.shape[1:]))
     dist.all_gather_into_tensor(out, send, group=group)
-    return list(out.unbind(0))
+    return out.view((world,) + tuple(send.shape))
+
+
+def _send(local, n, shape, dim):
+    """The all-gather's send buffer: `local` itself when it already has the padded shape, else a zero
+    pad of `shape` with local's first n entries along `dim` copied in."""
+    if tuple(local.shape) == tuple(shape) and local.is_contiguous():
+        return local
+    send = local.new_zeros(shape)
+    send.narrow(dim, 0, n).copy_(local.narrow(dim, 0, n))
+    return send
 
 
 def assemble(local_rows, P: int, group=None, partition: str = "target"):
@@ -56,9 +62,11 @@ def assemble(local_rows, P: int, group=None, partition: str = "target"):
     maxrows = max(hi - lo for lo, hi in ranges)
     lo, hi = ranges[rank]
     K, W = local_rows.shape[1], local_rows.shape[2]
-    send = local_rows.new_zeros((max(maxrows, 1), K, W))
-    send[: hi - lo] = local_rows[: hi - lo]
-    parts = _gather(send, world, group)
+    if world == 1:  # the shard is the plane
+        return local_rows[:P]
+    parts = _gather(_send(local_rows, hi - lo, (max(maxrows, 1), K, W), 0), world, group)
+    if all(b - a == maxrows for a, b in ranges):
+        return parts.view(P, K, W)  # equal shards: the gathered buffer is already the plane's row order
     full = local_rows.new_empty((P, K, W))
     for r, (a, b) in enumerate(ranges):
         full[a:b] = parts[r][: b - a]
@@ -77,9 +85,9 @@ def assemble_sources(local_ingress, P: int, group=None):
     maxw = max(b - a for a, b in wr)
     K = local_ingress.shape[1]
     a, b = wr[rank]
-    send = local_ingress.new_zeros((P, K, max(maxw, 1)))
-    send[:, :, : b - a] = local_ingress[:, :, : b - a]
-    parts = _gather(send, world, group)
+    if world == 1:  # one rank computed every word of every row
+        return local_ingress[:, :, :W]
+    parts = _gather(_send(local_ingress, b - a, (P, K, max(maxw, 1)), 2), world, group)
     full = local_ingress.new_empty((P, K, W))
     for r, (a, b) in enumerate(wr):
         full[:, :, a:b] = parts[r][:, :, : b - a]

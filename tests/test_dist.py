@@ -76,7 +76,7 @@ def _worker_src(rank, world, port, P, K, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P,world", [(5, 2), (130, 2), (300, 3)])
+@pytest.mark.parametrize("P,world", [(5, 2), (130, 2), (300, 3), (256, 2), (70, 1)])
 def test_assemble_sources_gloo(P, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
