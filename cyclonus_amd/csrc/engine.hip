@@ -2924,8 +2924,6 @@ __global__ __launch_bounds__(256) void k_front_c(FrontC f) {
 struct FrontRows {
   uint32_t nb[2];
   RowArgs ra[2];
-  uint32_t mix;  // k_front_e_uni: the directions' blocks alternate (both directions' class rows are
-                 // written in step, newest last: see EmitArgs::sweep), else egress blocks first
 };
 __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
   const uint32_t b = blockIdx.x;
@@ -2947,20 +2945,9 @@ constexpr int E_KC = 4;  // job slots per thread in the IDO class rows of the fu
 // Launch E as one kernel when the egress rows take the one-descriptor-per-slot form (UNI): both
 // bodies then stay near 60 VGPRs, so the fused launch keeps their occupancy and saves a launch.
 __global__ __launch_bounds__(256) void k_front_e_uni(FrontRows f) {
-  uint32_t b = blockIdx.x, eg;
-  if (f.mix) {
-    const uint32_t m = min(f.nb[0], f.nb[1]);
-    if (b < 2 * m) {
-      eg = b & 1;
-      b >>= 1;
-    } else {
-      eg = f.nb[1] > m ? 1u : 0u;
-      b = b - m;
-    }
-  } else {
-    eg = b < f.nb[1] ? 1u : 0u;
-    if (!eg) b -= f.nb[1];
-  }
+  uint32_t b = blockIdx.x;
+  const bool eg = b < f.nb[1];
+  if (!eg) b -= f.nb[1];
   if (eg) class_rows_ido_blk<true, E_KC, true>(f.ra[1], b, f.nb[1]);
   else class_rows_ido_blk<false, E_KC>(f.ra[0], b, f.nb[0]);
 }
@@ -2999,14 +2986,6 @@ struct EmitArgs {
   // (their readers are all done): no fill launch or memset node before the next front
   uint32_t* reset;
   uint64_t reset_n;
-  // sweep (> 0, one-row-per-block kernels): the row list is dealt to the XCDs in chunks of `sweep`
-  // rows (chunk k on XCD k % 8) and swept from its END: all XCDs move through the identity order
-  // together, newest class rows first — launch E writes them in about identity order, so the last
-  // ~256 MB it wrote are still in the Infinity Cache when the emit starts, and a sweep from the end
-  // reads them there instead of from HBM (an LRU cache under a forward sweep of 400 MB of class rows
-  // keeps none of them); 0 = an XCD per contiguous eighth of the list
-  uint32_t sweep;
-  uint32_t sweep_fwd;  // the chunks from the start of the list (emit_sweep < 0)
   uint32_t buf;        // 56-104 KB rows through k_emit_wide_buf<512,13> (else k_emit_wide<1024,7>)
 };
 
@@ -3014,15 +2993,8 @@ struct EmitArgs {
 __device__ __forceinline__ bool emit_slot(const EmitArgs& a, uint32_t n, uint32_t& r, uint32_t& x) {
   const uint32_t b = blockIdx.x;
   x = b & 7;
-  if (!a.sweep) {
-    r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
-    return r < min(n, (x + 1) * a.per_xcd);
-  }
-  const uint32_t i = b >> 3, C = a.sweep;
-  const uint64_t q = (uint64_t(i / C) * 8 + x) * C + i % C;
-  if (q >= n) return false;
-  r = a.sweep_fwd ? uint32_t(q) : n - 1 - uint32_t(q);
-  return true;
+  r = x * a.per_xcd + (b >> 3);  // XCD x writes its own contiguous segment of the row list
+  return r < min(n, (x + 1) * a.per_xcd);
 }
 
 // Row r of the row list -> (plane, (pod, identity)).
@@ -3756,9 +3728,6 @@ struct cyc_ctx {
                          // averaged 3.389 ms per step against 3.542 for 512 x 13 (1-2 % behind on the best
                          // placements, up to 8 % ahead on the worst; a target shard at N = 8 -5.7 %),
                          // profiles/r05_plane_placement.txt, r05_shard_ab.txt
-  int emit_sweep = 0;    // "emit_sweep": EmitArgs::sweep, rows per XCD chunk of a target-row emit (0 = off):
-                         // -2 to -4 % per step on some plane placements, +6 % on others (config #3 over 5
-                         // placements in one process: mean +0.2 %, profiles/r05_plane_placement.txt)
   // what the last enqueued emit launched (cyc_last_emit): kernel name(s) and launch count
   std::string emit_kernel;
   int emit_launches = 0;
@@ -5064,8 +5033,6 @@ static const char* enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64
   const uint32_t nr = ea.n_rows[0] + ea.n_rows[1];
   ea.per_xcd = (nr + 7) / 8;
   const uint64_t row_bytes0 = ea.row_words * 8;
-  if (row_bytes0 < EMIT_WIDE_MIN && ea.row_words % 2 == 0) ea.sweep = 0;  // (k_emit_flat: multi-row blocks)
-  if (ea.sweep) ea.per_xcd = (nr + 8 * ea.sweep - 1) / (8 * ea.sweep) * ea.sweep;  // whole rounds of 8 chunks
   const bool aligned = reinterpret_cast<uintptr_t>(out_in) % 16 == 0 && reinterpret_cast<uintptr_t>(out_eg) % 16 == 0;
   const unsigned g = ea.per_xcd * 8;  // one block per row slot of the 8 XCD segments
   if (ea.row_words % 2 || !aligned) {
@@ -5158,8 +5125,6 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
   ea.reset = c->ip_rng.as<uint32_t>();
   ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
-  ea.sweep = uint32_t(std::abs(c->emit_sweep));
-  ea.sweep_fwd = c->emit_sweep < 0 ? 1u : 0u;
   ea.buf = uint32_t(c->emit_buf);
   c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
@@ -5494,7 +5459,6 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   }
   if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
   if (fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
-    fe.mix = c->emit_sweep ? 1u : 0u;
     k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);
   } else {  // the directions' class rows as two launches, each at its own register budget (egress 101
             // VGPRs, ingress 61: one launch at 101 ran config #3 189 -> 170 us, profiles/r03_e_split_ab.txt)
@@ -6433,7 +6397,6 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "step_events") range(0, 1), c->step_events = int(value);
     else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
     else if (n == "emit_split") range(1, 8), c->emit_split = int(value);
-    else if (n == "emit_sweep") range(-(1 << 20), 1 << 20), c->emit_sweep = int(value);
     else if (n == "emit_buf") range(0, 2), c->emit_buf = int(value);
     else if (n == "ip_items") {
       range(-1, 1);
@@ -6472,7 +6435,6 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "step_events") *value = c->step_events;
   else if (n == "emit_interleave") *value = c->emit_interleave;
   else if (n == "emit_split") *value = c->emit_split;
-  else if (n == "emit_sweep") *value = c->emit_sweep;
   else if (n == "ip_items") *value = c->ip_items_opt;
   else if (n == "emit_buf") *value = c->emit_buf;
   else if (n == "plvt_max_mb") *value = c->plvt_max_mb;

@@ -368,10 +368,6 @@ int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
  *                 emit's row list alternates ingress and egress rows (1) or holds all ingress rows first
  *   "emit_split"  1 (default) .. 8: a target-row run's emit as that many launches over consecutive
  *                 parts of the planes' row lists
- *   "emit_sweep"  0 (default) / C > 0: a target-row run's emit deals its row list to the XCDs in chunks
- *                 of C rows and sweeps it from the end (all XCDs move through the class order together,
- *                 the class rows written last read first), instead of an XCD per contiguous eighth;
- *                 -C: the same chunks swept from the start
  * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
  * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
  * uses (0 or 1). */

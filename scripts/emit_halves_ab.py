@@ -60,7 +60,7 @@ VARIANTS = {
 
 
 def spec(name):
-    """A variant, optionally with options: "whole:emit_sweep=16,emit_interleave=0"."""
+    """A variant, optionally with options: "whole:emit_split=2,emit_interleave=0"."""
     base, _, extra = name.partition(":")
     opts = dict(VARIANTS[base][0])
     for kv in filter(None, extra.split(",")):
@@ -70,7 +70,7 @@ def spec(name):
 
 
 def setv(name):
-    for k, v in (("emit_interleave", -1), ("emit_split", 1), ("emit_sweep", 0)):
+    for k, v in (("emit_interleave", -1), ("emit_split", 1)):
         eng.set_option(k, v)
     for k, v in spec(name)[0].items():
         eng.set_option(k, v)

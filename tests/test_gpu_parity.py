@@ -715,7 +715,7 @@ def test_launch_modes_and_knobs(gpu):
                     ("step_events", 1), ("step_events", 0), ("pr_group", 5), ("pr_group", -1), ("sel_lazy", 1),
                     ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1),
                     ("emit_interleave", 1), ("emit_split", 3), ("emit_interleave", 0), ("emit_split", 2),
-                    ("emit_interleave", -1), ("emit_split", 1), ("emit_sweep", 5), ("emit_sweep", 1), ("emit_sweep", -3), ("emit_sweep", 0),
+                    ("emit_interleave", -1), ("emit_split", 1),
                     ("ip_items", 0), ("ip_items", 1), ("ip_items", -1), ("emit_buf", 0), ("emit_buf", 1), ("emit_buf", 2)):
         eng.set_option(name, v)
         assert eng.get_option(name) == v
@@ -739,7 +739,7 @@ def test_launch_modes_and_knobs(gpu):
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
     for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_range", 2), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
-                    ("emit_split", 0), ("emit_split", 9), ("emit_interleave", 2), ("emit_prefetch", 1), ("emit_sweep", 1 << 21), ("ip_items", 2), ("emit_buf", 3),
+                    ("emit_split", 0), ("emit_split", 9), ("emit_interleave", 2), ("emit_prefetch", 1), ("emit_sweep", 16), ("ip_items", 2), ("emit_buf", 3),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
