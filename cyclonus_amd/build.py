@@ -3,7 +3,8 @@
     python -m cyclonus_amd.build        # or __graft_entry__.build()
 
 host.cpp (policy compiler, probe model, table flattening) is compiled with g++; engine.hip
-(kernels + C ABI) with hipcc --offload-arch=gfx950; both are linked by hipcc into one shared
+(kernels + C ABI, with its stage headers dev_*.hpp / ctx / plan / enqueue.hpp as one translation
+unit) with hipcc --offload-arch=gfx950; both are linked by hipcc into one shared
 library with plain C entry points declared in include/cyclonus_hip.h.
 """
 from __future__ import annotations
@@ -23,7 +24,9 @@ ARCH = "gfx950"
 
 SOURCES_CPP = ["host.cpp"]
 SOURCES_HIP = ["engine.hip"]
-HEADERS = ["cjson.hpp", "host.hpp", "tables.h"]
+# engine.hip's stage headers (one translation unit) and the host headers
+HEADERS = ["cjson.hpp", "host.hpp", "tables.h", "dev_select.hpp", "dev_peer_rows.hpp", "dev_slots.hpp", "dev_member.hpp",
+           "dev_class_rows.hpp", "dev_front.hpp", "dev_emit.hpp", "dev_query.hpp", "ctx.hpp", "plan.hpp", "enqueue.hpp"]
 
 
 def _newer(target, deps):

@@ -1,6 +1,6 @@
 """Build an A/B variant of libcyclonus_hip.so with extra -D flags (dev helper):
     python scripts/build_variant.py NAME -DMACRO=1          -> cyclonus_amd/_build/var_NAME/libcyclonus_hip.so
-    python scripts/build_variant.py NAME --rev HEAD           -> the engine.hip of a git revision
+    python scripts/build_variant.py NAME --rev HEAD           -> engine.hip (and its headers) of a git revision
     python scripts/build_variant.py NAME --src FILE           -> a patched copy of engine.hip (diagnostics)
 Run it with CYC_HIP_LIB=<that path> (cyclonus_amd/_lib.py)."""
 import os
@@ -18,10 +18,12 @@ src = os.path.join(b.CSRC, "engine.hip")
 if "--rev" in defs:
     rev = defs[defs.index("--rev") + 1]
     defs = [d for d in defs if d not in ("--rev", rev)]
-    src = os.path.join(out, "engine_rev.hip")
-    with open(src, "w") as f:
-        f.write(subprocess.run(["git", "-C", ROOT, "show", f"{rev}:cyclonus_amd/csrc/engine.hip"], check=True,
-                               capture_output=True, text=True).stdout)
+    # the revision's whole csrc/ (engine.hip includes its stage headers from its own directory)
+    rdir = os.path.join(out, "csrc_rev")
+    os.makedirs(rdir, exist_ok=True)
+    tar = subprocess.run(["git", "-C", ROOT, "archive", rev, "cyclonus_amd/csrc"], check=True, capture_output=True).stdout
+    subprocess.run(["tar", "-x", "-C", rdir, "--strip-components=2"], input=tar, check=True)
+    src = os.path.join(rdir, "engine.hip")
 if "--src" in defs:
     src = os.path.abspath(defs[defs.index("--src") + 1])
     defs = [d for d in defs if d not in ("--src", src) and os.path.abspath(d) != src]
