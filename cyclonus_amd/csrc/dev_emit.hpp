@@ -184,7 +184,10 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
   if (!si) return;  // in-place class row: already written
   u64x2* di = reinterpret_cast<u64x2*>(a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.row_words);
   const uint32_t n2 = uint32_t(a.row_words / 2);
-  for (uint32_t x0 = threadIdx.x; x0 < n2; x0 += BS * UNROLL) {
+  // stores aligned to the plane's 128-byte lines, as copy_row_buf: the head chunks first
+  const uint32_t h2 = (uint32_t(-reinterpret_cast<uintptr_t>(di)) & 127u) / 16;
+  if (threadIdx.x < h2 && threadIdx.x < n2) emit_store(si[threadIdx.x], &di[threadIdx.x]);
+  for (uint32_t x0 = h2 + threadIdx.x; x0 < n2; x0 += BS * UNROLL) {
     u64x2 v[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; u++)
@@ -201,6 +204,32 @@ __global__ __launch_bounds__(BS) void k_emit_wide(EmitArgs a) {
 // offsets past the row (the last pass's idle lanes) fall outside the buffer's range and are dropped.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int BUF_RSRC_W3 = 0x00020000;  // buffer resource word 3 for gfx9 raw buffers
+// One row copy through buffer ops, its stores aligned to the 128-byte lines of the plane: a row that
+// starts mid-line (config #3's 100,032-byte rows: every other one; config #4's 25,024: the same) first
+// stores its head up to the next line boundary (threads of the head's 16-byte chunks), then the rest
+// from that boundary, so every wave's 1 KB store covers whole lines and only the row's two ends are
+// partial lines.  Stores whose 1 KB straddled lines (rows copied from their own start) wrote ~1 line
+// in 9 in two halves, by two waves: pure stores of config #3's shape 3.5 % slower on every placement
+// measured (scripts/pitch_probe.hip, profiles/r05_row_alignment.txt).  Offsets past the row fall
+// outside the buffer's range and are dropped.
+template <int BS, int UNROLL>
+__device__ __forceinline__ void copy_row_buf(const uint64_t* si, uint64_t* di, uint32_t bytes) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(si), 0, bytes, BUF_RSRC_W3);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(di, 0, bytes, BUF_RSRC_W3);
+  const uint32_t head = uint32_t(-reinterpret_cast<uintptr_t>(di)) & 127u;  // bytes to the next line (16-byte multiple)
+  if (threadIdx.x * 16 < head) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rd, threadIdx.x * 16, 0, 2);  // nt
+  }
+  for (uint32_t x0 = head; x0 < bytes; x0 += BS * UNROLL * 16) {
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, x0 + u * BS * 16, 0);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, threadIdx.x * 16, x0 + u * BS * 16, 2);  // nt
+  }
+}
+
 template <int BS, int UNROLL>
 __global__ __launch_bounds__(BS) void k_emit_wide_buf(EmitArgs a) {
   emit_status(a);
@@ -212,16 +241,7 @@ __global__ __launch_bounds__(BS) void k_emit_wide_buf(EmitArgs a) {
   const uint64_t* si = emit_src(a, pl, pi);
   if (!si) return;  // in-place class row: already written
   uint64_t* di = a.out[pl] + uint64_t(pi.x - a.row_lo[pl]) * a.row_words;
-  const uint32_t bytes = uint32_t(a.row_words * 8);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(si), 0, bytes, BUF_RSRC_W3);
-  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(di, 0, bytes, BUF_RSRC_W3);
-  for (uint32_t x0 = 0; x0 < bytes; x0 += BS * UNROLL * 16) {
-    u32x4 v[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, x0 + u * BS * 16, 0);
-#pragma unroll
-    for (int u = 0; u < UNROLL; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, threadIdx.x * 16, x0 + u * BS * 16, 2);  // nt
-  }
+  copy_row_buf<BS, UNROLL>(si, di, uint32_t(a.row_words * 8));
 }
 
 // Planes whose rows differ in length (a source shard: ingress rows of every destination over the
@@ -259,16 +279,8 @@ __global__ __launch_bounds__(BS) void k_emit_units(EmitArgs a) {
   if (a.unit_rows[pl] == 1) {  // a unit of one long row (a source shard's egress rows): the copy of
                                // k_emit_wide_buf, chunk offsets in the scalar offset, no per-chunk division
     if (!s_cnt) return;
-    const uint32_t bytes = uint32_t(a.pl_words[pl] * 8);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<u64x2*>(s_src[0]), 0, bytes, BUF_RSRC_W3);
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(s_dst[0], 0, bytes, BUF_RSRC_W3);
-    for (uint32_t x0 = 0; x0 < bytes; x0 += BS * UNROLL * 16) {
-      u32x4 v[UNROLL];
-#pragma unroll
-      for (int q = 0; q < UNROLL; q++) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, x0 + q * BS * 16, 0);
-#pragma unroll
-      for (int q = 0; q < UNROLL; q++) __builtin_amdgcn_raw_buffer_store_b128(v[q], rd, threadIdx.x * 16, x0 + q * BS * 16, 2);  // nt
-    }
+    copy_row_buf<BS, UNROLL>(reinterpret_cast<const uint64_t*>(s_src[0]), reinterpret_cast<uint64_t*>(s_dst[0]),
+                             uint32_t(a.pl_words[pl] * 8));
     return;
   }
   const uint32_t n2 = uint32_t(a.pl_words[pl] / 2), tot = s_cnt * n2;
