@@ -146,7 +146,7 @@ struct cyc_ctx {
   DevBuf ipi_items, ipi_list;   // IP-row work items of the fused front (DIPItem; ip_rows_items_blk) and their rows
   uint32_t ipi_off[3] = {0, 0, 0};  // items of segment x: [ipi_off[x], ipi_off[x + 1])
   bool ip_items = false;        // the current plan's items are built (option "ip_items" on and fast IP rows present)
-  int ip_items_opt = -1;        // "ip_items": -1 auto (on) / 0 / 1
+  int ip_items_opt = -1;        // "ip_items": -1 auto (whole-table runs) / 0 / 1
   std::vector<DWordIP> ipw_h;   // host copy of the IP word and chunk records (ip_words)
   DevBuf ido_grp_ns, ido_word_ns;  // identity-set namespace skip (peer_bits_blk): per row group, per identity word
   uint32_t ido_goff[2] = {0, 0};   // first group of each direction's sub-list in ido_grp_ns

@@ -894,7 +894,12 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
     std::vector<uint32_t> il;
     const bool one = one_window(c);
     const uint32_t NCH = (pb.W + 63) / 64;
-    const bool on = c->ip_items_opt != 0 && c->ipw_h.size() == size_t(pb.W) + NCH && !pb.may_err;
+    // auto: whole-table runs only — a shard's few IP rows and windows ran launch B 2x slower as items
+    // (config #3 rank 0 of 8: B 45.5 vs 20.9 us source, 36.4 vs 17.0 target; whole step +20 us), while
+    // whole tables gain 0-1 % (profiles/r05_ip_items_ab.txt)
+    const bool whole = lo == 0 && hi == int64_t(pb.P);
+    const bool on = (c->ip_items_opt == 1 || (c->ip_items_opt == -1 && whole)) && c->ipw_h.size() == size_t(pb.W) + NCH &&
+                    !pb.may_err;
     for (int x = 0; x < 2; x++) {
       c->ipi_off[x] = uint32_t(items.size());
       if (!on || (one && x)) continue;

@@ -364,6 +364,9 @@ int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
  *                 membership and pod-peer rows / identity sets use them (1) instead of as the dense
  *                 selector x label-set table first (0); auto = 1 for identity-set builds and once
  *                 that table has >= 64M pairs
+ *   "ip_items"    -1 (default: auto = 1 for runs over every row) / 0 / 1: the fused front's IP rows as
+ *                 per-chunk work items of the rows that touch each chunk (1) or as groups of 16 rows a
+ *                 wave over 4 chunks (0)
  *   "emit_interleave" -1 (default: auto = 1 when a plane of a target-row run is >= 8 GB) / 0 / 1: the
  *                 emit's row list alternates ingress and egress rows (1) or holds all ingress rows first
  *   "emit_split"  1 (default) .. 8: a target-row run's emit as that many launches over consecutive
