@@ -233,7 +233,6 @@ struct cyc_ctx {
   bool ip_rng_clean = false;
   bool capturing = false;  // a hipGraph capture is in progress (captured steps always fill the spans themselves)
   bool ran = false;    // a run has been enqueued
-  hipEvent_t run_done = nullptr;  // recorded on the run's stream after every run (cyc_last_classes)
   // batched blocks (cyc_probe_prepare_blocks; pb.blocks non-empty)
   DevBuf blk, blk_off, id_blk[2], id_win[2], first_blk;
   uint32_t blk_wa_max = 0, blk_np_max = 0;

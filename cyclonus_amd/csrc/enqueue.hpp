@@ -942,7 +942,6 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     c->timed_graph = false;
   }
   c->ran = true;
-  HIPCHK(hipEventRecord(c->run_done, st));
 
   if (!pb.blocks.empty()) return blocks_status(c, st);
 
