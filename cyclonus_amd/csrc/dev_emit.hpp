@@ -35,6 +35,7 @@ struct EmitArgs {
   // words, rows per unit (a unit = one block's pass) and units; the unit list is [plane 0][plane 1]
   uint64_t pl_words[2];
   uint32_t unit_rows[2], n_units[2];
+  uint32_t unit_grp[2];  // k_emit_units: a unit's rows copied a thread group each (8 groups), else 0
   // the IP rows' word-span records (RowArgs::ip_rng), reset to ~0 for the NEXT run in block slices
   // (their readers are all done): no fill launch or memset node before the next front
   uint32_t* reset;
@@ -213,20 +214,20 @@ constexpr int BUF_RSRC_W3 = 0x00020000;  // buffer resource word 3 for gfx9 raw 
 // measured (scripts/pitch_probe.hip, profiles/r05_row_alignment.txt).  Offsets past the row fall
 // outside the buffer's range and are dropped.
 template <int BS, int UNROLL>
-__device__ __forceinline__ void copy_row_buf(const uint64_t* si, uint64_t* di, uint32_t bytes) {
+__device__ __forceinline__ void copy_row_buf(const uint64_t* si, uint64_t* di, uint32_t bytes, uint32_t tid = threadIdx.x) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(si), 0, bytes, BUF_RSRC_W3);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(di, 0, bytes, BUF_RSRC_W3);
   const uint32_t head = uint32_t(-reinterpret_cast<uintptr_t>(di)) & 127u;  // bytes to the next line (16-byte multiple)
-  if (threadIdx.x * 16 < head) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rd, threadIdx.x * 16, 0, 2);  // nt
+  if (tid * 16 < head) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rd, tid * 16, 0, 2);  // nt
   }
   for (uint32_t x0 = head; x0 < bytes; x0 += BS * UNROLL * 16) {
     u32x4 v[UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, threadIdx.x * 16, x0 + u * BS * 16, 0);
+    for (int u = 0; u < UNROLL; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, x0 + u * BS * 16, 0);
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, threadIdx.x * 16, x0 + u * BS * 16, 2);  // nt
+    for (int u = 0; u < UNROLL; u++) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, tid * 16, x0 + u * BS * 16, 2);  // nt
   }
 }
 
@@ -281,6 +282,15 @@ __global__ __launch_bounds__(BS) void k_emit_units(EmitArgs a) {
     if (!s_cnt) return;
     copy_row_buf<BS, UNROLL>(reinterpret_cast<const uint64_t*>(s_src[0]), reinterpret_cast<uint64_t*>(s_dst[0]),
                              uint32_t(a.pl_words[pl] * 8));
+    return;
+  }
+  if (a.unit_grp[pl]) {  // rows of 7-14 KB (a source shard's ingress rows at N = 8): a row per group of
+                         // BS / 8 threads (whole waves), each row one line-aligned buffer-op pass
+    constexpr uint32_t G = 8, GS = BS / G;
+    const uint32_t j = threadIdx.x / GS;
+    if (j < s_cnt)
+      copy_row_buf<GS, UNROLL>(reinterpret_cast<const uint64_t*>(s_src[j]), reinterpret_cast<uint64_t*>(s_dst[j]),
+                               uint32_t(a.pl_words[pl] * 8), threadIdx.x % GS);
     return;
   }
   const uint32_t n2 = uint32_t(a.pl_words[pl] / 2), tot = s_cnt * n2;

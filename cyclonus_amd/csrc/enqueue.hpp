@@ -276,6 +276,15 @@ static const char* enq_emit_units(EmitArgs ea, hipStream_t st) {
   for (int pl = 0; pl < 2; pl++) {
     const uint64_t rb = std::max<uint64_t>(ea.pl_words[pl] * 8, 1);
     ea.unit_rows[pl] = uint32_t(std::min<uint64_t>(EMIT_UNIT_MAX_ROWS, std::max<uint64_t>(1, pass / rb)));
+    // rows of 7-14 KB (a source shard's ingress rows at N = 8: 12.5 KB) as 8 rows a unit, a row per
+    // 128-thread group in one aligned buffer-op pass: config #3 rank 0 of 8 emit 384 vs 425 us, step
+    // -3 %; 512- and 256-thread groups for the 50 / 25 KB rows of N = 2 / 4 measured +1 % / ±0: not
+    // used (profiles/r05_row_alignment.txt)
+    ea.unit_grp[pl] = 0;
+    if (rb <= pass / 8 && rb > pass / 16 && rb % 16 == 0) {
+      ea.unit_grp[pl] = 8;
+      ea.unit_rows[pl] = 8;
+    }
     ea.n_units[pl] = (ea.n_rows[pl] + ea.unit_rows[pl] - 1) / ea.unit_rows[pl];
   }
   ea.per_xcd = (ea.n_units[0] + ea.n_units[1] + 7) / 8;
