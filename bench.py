@@ -228,7 +228,7 @@ def main():
             out_eg = torch.empty((world * d_eg.numel(),), dtype=torch.int64, device=dev)
             src_in, src_eg = (d_in, d_eg) if backend == "nccl" else (d_in.cpu(), d_eg.cpu())
 
-            def gather():  # one all-gather per plane of the padded shards (the relayout to [P][K][W] excluded)
+            def gather():  # torch's all-gather of the padded shards as they are (a raw xGMI rate, no relayout)
                 for src, out in ((src_in, out_in), (src_eg, out_eg)):
                     if backend == "nccl":
                         dist.all_gather_into_tensor(out, src)
@@ -252,32 +252,38 @@ def main():
             assembled = {"all_gather_ms": ga * 1e3, "bytes_received_per_rank": recv, "xgmi_GBs_per_rank": recv / ga / 1e9}
             del out_in, out_eg
             if backend == "nccl":
-                # the time to a usable whole table on every rank: the all-gathers AND the relayout of
-                # the shards into [P][K][W] planes (shard.assemble / assemble_sources), one warm call
-                from cyclonus_amd import shard
+                # the time to a usable whole table on every rank, through the library (cyc_comm_init +
+                # cyc_planes_allgather, comm.hpp: grouped RCCL broadcasts of the row shares straight into
+                # place, and for a source partition the chunked gather of the ingress slices + the HIP
+                # relayout kernel); rank 0's unique id goes to the others over the process group
+                uid = torch.tensor(list(Engine.comm_unique_id()) if rank == 0 else [0] * 128, dtype=torch.uint8,
+                                   device="cuda")
+                dist.broadcast(uid, 0)
+                eng.comm_init(world, rank, bytes(uid.cpu().tolist()))
+                assert eng.rows_shard(world, rank, part) == (lo, hi)
+                torch.cuda.empty_cache()
+                f_in = torch.empty((P * K * W,), dtype=torch.int64, device="cuda")
+                f_eg = torch.empty((P * K * W,), dtype=torch.int64, device="cuda")
 
                 def whole():
-                    if part == "source":
-                        a = shard.assemble_sources(d_in[: P * K * wi].view(P, K, wi), P)
-                    else:
-                        a = shard.assemble(d_in[: ri * K * wi].view(ri, K, wi), P)
-                    b = shard.assemble(d_eg[: re_ * K * we].view(re_, K, we), P, partition=part)
-                    return a, b
+                    eng.planes_allgather(d_in.data_ptr(), d_eg.data_ptr(), f_in.data_ptr(), f_eg.data_ptr(), stream, part)
 
-                torch.cuda.empty_cache()
                 whole()
                 torch.cuda.synchronize()
                 barrier()
                 tw = time.perf_counter()
-                full = whole()
+                for _ in range(reps):
+                    whole()
                 torch.cuda.synchronize()
                 barrier()
-                tt = torch.tensor([time.perf_counter() - tw], dtype=torch.float64, device="cuda")
+                tt = torch.tensor([(time.perf_counter() - tw) / reps], dtype=torch.float64, device="cuda")
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)
                 assembled["whole_table_ms"] = float(tt.item()) * 1e3
-                assembled["whole_table_note"] = ("all-gathers plus the relayout of every rank's shards into the "
-                                                 "[P][K][W] ingress and egress planes on every rank (max over ranks)")
-                del full
+                assembled["whole_table_note"] = ("cyc_planes_allgather (libcyclonus_hip's own RCCL communicator): both "
+                                                 "[P][K][W] planes whole on every rank, incl. the relayout of a source "
+                                                 "partition's ingress slices (max over ranks)")
+                eng.comm_destroy()
+                del f_in, f_eg
                 torch.cuda.empty_cache()
         except Exception as e:  # the assembled figure is informational; never lose the bench line
             assembled = {"error": f"{type(e).__name__}: {e}"}

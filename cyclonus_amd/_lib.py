@@ -12,6 +12,9 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 # CYC_HIP_LIB: another build of the same library (A/B timing of two builds in one GPU session)
 SO_PATH = os.environ.get("CYC_HIP_LIB") or os.path.join(_PKG, "libcyclonus_hip.so")
 
+# CYC_ABI_VERSION of the header these ctypes declarations mirror (include/cyclonus_hip.h)
+ABI_VERSION = 2
+
 # cyc_status
 OK, ERR_ARG, ERR_JSON, ERR_INVALID_POLICY, ERR_PANIC_IP, ERR_PANIC_CIDR, ERR_PANIC_SELECTOR = 0, 1, 2, 3, 4, 5, 6
 ERR_DUPLICATE_KEY, ERR_HIP, ERR_OOM, ERR_RCCL, ERR_PANIC_RUNTIME = 7, 8, 9, 10, 11
@@ -30,6 +33,7 @@ EXPORTS = [
     "cyc_ctx_destroy",
     "cyc_last_error",
     "cyc_version",
+    "cyc_abi_version",
     "cyc_policy_build_json",
     "cyc_policy_load_ir_json",
     "cyc_policy_ir_json",
@@ -57,6 +61,13 @@ EXPORTS = [
     "cyc_probe_run_host_rows",
     "cyc_table_run_rows",
     "cyc_table_wrap_rows",
+    "cyc_comm_unique_id",
+    "cyc_comm_init",
+    "cyc_comm_destroy",
+    "cyc_rows_shard",
+    "cyc_planes_allgather",
+    "cyc_table_allgather",
+    "cyc_rows_merge_sources",
     "cyc_probe_prepare_blocks",
     "cyc_blocks_layout",
     "cyc_probe_run_blocks",
@@ -116,6 +127,9 @@ def lib():
         L.cyc_last_error.argtypes = [vp]
         L.cyc_last_error.restype = cp
         L.cyc_version.restype = cp
+        L.cyc_abi_version.restype = i
+        if L.cyc_abi_version() != ABI_VERSION:
+            raise ImportError(f"{SO_PATH}: ABI {L.cyc_abi_version()}, these bindings expect ABI {ABI_VERSION} (rebuild)")
         L.cyc_policy_build_json.argtypes = [vp, i, cp, sz]
         L.cyc_policy_load_ir_json.argtypes = [vp, cp, sz]
         L.cyc_policy_ir_json.argtypes = [vp, cp, sz]
@@ -146,6 +160,13 @@ def lib():
         L.cyc_probe_run_host_rows.argtypes = [vp, vp, vp, vp, i, i64, i64]
         L.cyc_table_run_rows.argtypes = [vp, i, i64, i64, ctypes.POINTER(vp)]
         L.cyc_table_wrap_rows.argtypes = [vp, vp, vp, vp, i, i64, i64, ctypes.POINTER(vp)]
+        L.cyc_comm_unique_id.argtypes = [vp]
+        L.cyc_comm_init.argtypes = [vp, i, i, vp]
+        L.cyc_comm_destroy.argtypes = [vp]
+        L.cyc_rows_shard.argtypes = [vp, i, i, i, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        L.cyc_planes_allgather.argtypes = [vp, vp, i, vp, vp, vp, vp]
+        L.cyc_table_allgather.argtypes = [vp, vp, ctypes.POINTER(vp)]
+        L.cyc_rows_merge_sources.argtypes = [vp, vp, i, vp, vp]
         L.cyc_probe_prepare_blocks.argtypes = [vp, cp, sz, vp, vp, i64, ctypes.POINTER(ProbeShape)]
         L.cyc_blocks_layout.argtypes = [vp, vp, i64]
         L.cyc_probe_run_blocks.argtypes = [vp, vp, vp, vp, vp, vp]

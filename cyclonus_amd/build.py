@@ -26,7 +26,9 @@ SOURCES_CPP = ["host.cpp"]
 SOURCES_HIP = ["engine.hip"]
 # engine.hip's stage headers (one translation unit) and the host headers
 HEADERS = ["cjson.hpp", "host.hpp", "tables.h", "dev_select.hpp", "dev_peer_rows.hpp", "dev_slots.hpp", "dev_member.hpp",
-           "dev_class_rows.hpp", "dev_front.hpp", "dev_emit.hpp", "dev_query.hpp", "ctx.hpp", "plan.hpp", "enqueue.hpp"]
+           "dev_class_rows.hpp", "dev_front.hpp", "dev_emit.hpp", "dev_query.hpp", "dev_gather.hpp", "ctx.hpp", "plan.hpp",
+           "enqueue.hpp", "comm.hpp"]
+LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]  # RCCL: the table assembly's all-gathers (comm.hpp)
 
 
 def _newer(target, deps):
@@ -86,7 +88,7 @@ def build_asan(force: bool = False) -> str:
             _run([HIPCC, f"--offload-arch={ARCH}", *common, *host_san, "-munsafe-fp-atomics", "-c", src, "-o", obj])
         objs.append(obj)
     if force or _newer(ASAN_LIB, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *host_san, "-shared-libsan", "-o", ASAN_LIB, *objs])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *host_san, "-shared-libsan", "-o", ASAN_LIB, *objs, *LIBS])
     return ASAN_LIB
 
 
@@ -108,7 +110,7 @@ def build(verbose: bool = True, force: bool = False) -> str:
             _run([HIPCC, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics", "-c", src, "-o", obj])
         objs.append(obj)
     if force or _newer(OUT, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs, *LIBS])
     write_build_info()
     build_driver(force)
     return OUT

@@ -16,6 +16,9 @@ namespace {
 struct HipErr {
   std::string msg;
 };
+struct RcclErr {  // an RCCL call failed (CYC_ERR_RCCL)
+  std::string msg;
+};
 
 // Makes `device` current for the scope of an entry point and restores the caller's current device
 // afterwards: a binding calling in from a thread whose current device is another GPU (e.g. PyTorch
@@ -142,6 +145,12 @@ struct cyc_ctx {
   std::vector<std::array<uint32_t, 4>> ip6_key;
   DevBuf ipsort, ipr_tests, ipr_iv;
   uint32_t rr_off[3] = {0, 0, 0}, Rr = 0;
+  // IP rows as pod intervals (ip_rows_iv_blk): when a family's pods hold non-decreasing addresses in
+  // pod order (ip_mono[0] IPv4, [1] IPv6), a network less its excepts matches that family's pods in
+  // a few pod-index intervals; per direction the rows built that way
+  bool ip_mono[2] = {false, false};
+  DevBuf ipv_tests, ipv_iv;
+  uint32_t rv_off[3] = {0, 0, 0}, Rv = 0;
   uint32_t rpu_off[3] = {0, 0, 0};  // sub-lists of pod_peers_u: one pod peer per distinct matcher
   DevBuf ipi_items, ipi_list;   // IP-row work items of the fused front (DIPItem; ip_rows_items_blk) and their rows
   uint32_t ipi_off[3] = {0, 0, 0};  // items of segment x: [ipi_off[x], ipi_off[x + 1])
@@ -161,6 +170,8 @@ struct cyc_ctx {
                         // events, -1 = auto: 2 when the fused front applies (its launches on one
                         // stream start ~8 us sooner after the previous step's emit than a graph
                         // replay: profiles/r01_front_fused_ab.txt), else 1
+  int ip_iv = -1;       // "ip_iv": IP rows as pod intervals where the network's family is address-monotone
+                        // in pod order (-1 auto = 1), 0 never
   int ip_range = -1;    // "ip_range": IP rows of few, close pods from the address index: -1 auto (where the
                         // words are not affine), 1 wherever they fit, 0 never
   int pod_rows = -1;    // "pod_rows": pod-peer PM rows per pod directly (1), through identity outcomes
@@ -186,6 +197,9 @@ struct cyc_ctx {
                         // (enq_front_fused), 0 = the two-branch DAG
   int emit_interleave = -1;  // "emit_interleave": a target-row emit's row list alternates the planes'
                              // rows (1) or is [plane 0][plane 1] (0); -1 = auto (planes >= 8 GB)
+  int emit_footprint = 1;  // "emit_footprint": a target-row emit as F launches, launch h writing only rows
+                           // [h P / F, (h + 1) P / F) of both planes, class-clustered within them (the TLB
+                           // footprint test, VERDICT r5 ask 2); 1 = one launch over the whole planes
   int emit_split = 1;   // "emit_split": a target-row emit as this many launches over consecutive parts
                         // of each plane's row list (1..8)
   int emit_buf = 2;      // "emit_buf": 56-104 KB plane rows through 1024 x 7 buffer-op blocks (2), 512 x 13
@@ -233,15 +247,26 @@ struct cyc_ctx {
   bool ip_rng_clean = false;
   bool capturing = false;  // a hipGraph capture is in progress (captured steps always fill the spans themselves)
   bool ran = false;    // a run has been enqueued
+  hipStream_t last_stream = nullptr;  // the stream the last run was enqueued on
   // batched blocks (cyc_probe_prepare_blocks; pb.blocks non-empty)
   DevBuf blk, blk_off, id_blk[2], id_win[2], first_blk;
   uint32_t blk_wa_max = 0, blk_np_max = 0;
   std::vector<uint64_t> blk_off_h;          // per block: plane slab offset (words), status offset (bytes); then totals
   std::vector<int> blk_rc;                  // per block status of the last run
   std::vector<std::string> blk_msg;         // and its message
+  // multi-GPU table assembly (comm.hpp): the context's RCCL communicator, a second stream on which
+  // gathered chunks are relaid out under the next chunk's all-gather, and the chunks' double buffer
+  struct Comm {
+    ncclComm_t nccl = nullptr;
+    int nranks = 0, rank = -1;
+    hipStream_t merge = nullptr;
+    hipEvent_t full[2] = {nullptr, nullptr}, free_[2] = {nullptr, nullptr}, done = nullptr;
+    DevBuf scratch[2];
+  } comm;
 };
 
 int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t idx);
+static void comm_release(cyc_ctx* c);  // comm.hpp
 static bool rows_layout(const cyc_ctx* c, int part, int64_t lo, int64_t hi, int64_t v[5], std::string& why);
 
 static int fail(cyc_ctx* c, int code, const std::string& m) {
@@ -257,6 +282,8 @@ static int guarded(cyc_ctx* c, F&& f) {
     return fail(c, p.code, p.msg);
   } catch (HipErr& h) {
     return fail(c, CYC_ERR_HIP, h.msg);
+  } catch (RcclErr& r) {
+    return fail(c, CYC_ERR_RCCL, r.msg);
   } catch (std::bad_alloc&) {
     return fail(c, CYC_ERR_OOM, "host allocation failed");
   } catch (std::exception& e) {

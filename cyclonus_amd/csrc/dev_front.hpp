@@ -49,9 +49,12 @@ __global__ __launch_bounds__(256) void k_front_a(FrontA f) {
 // rows and of the per-pod pod-peer rows is one direction's sub-list (target-row runs put both
 // directions into segment 0: one window).
 struct FrontB {
-  uint32_t nb[11];      // IP rows x2 | pod-peer rows x2 (or identity sets, segment 2) | membership in | eg | port bits |
+  uint32_t nb[13];      // IP rows x2 | pod-peer rows x2 (or identity sets, segment 2) | membership in | eg | port bits |
                         // port table | slot words (the last two: runs without launch A, enq_front_fused) |
-                        // IP rows from address ranges x2
+                        // IP rows from address ranges x2 | IP rows as pod intervals x2
+  uint32_t Rv[2];       // interval-built IP rows per segment (ip_rows_iv_blk)
+  const DIPIv* vtests[2];
+  const uint2* ipv_iv;
   uint32_t Rr[2];       // range-built IP rows per segment (ip_rows_range_blk)
   const DIPRange* rtests[2];
   const uint2* ipr_iv;
@@ -115,6 +118,11 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   if (f.member_first) {
     if (b < nm) return front_b_member(f, b);
     b -= nm;
+  }
+#pragma unroll
+  for (int x = 0; x < 2; x++) {
+    if (b < f.nb[11 + x]) return ip_rows_iv_blk(f.Rv[x], f.W, f.vtests[x], f.ipv_iv, f.words, f.PM, f.rng, f.cnz, b, f.ic0[x], f.inch[x]);
+    b -= f.nb[11 + x];
   }
 #pragma unroll
   for (int x = 0; x < 2; x++) {

@@ -614,6 +614,75 @@ __global__ __launch_bounds__(256) void k_ip_rows_range(uint32_t Rr, uint32_t W, 
   ip_rows_range_blk(Rr, W, rt, iv, sorted, PM, rng, cnz, blockIdx.x, c0, nch);
 }
 
+// IP rows as pod intervals (no-panic runs whose network family is address-monotone in pod order, the
+// usual case: addresses handed out in pod order).  The host's address index turns the network less
+// its same-family excepts (ipaddress.go:22-40; ippeermatcher.go:43-50) into <= IPV_MAX pod-index
+// intervals [x, y) of that family's pods, once per range plan; a row word is then the family's pods of
+// the word (DWordIP::m4 / m6) AND the intervals' lanes — no pod address is loaded and no word
+// straddles.  A wave per row: the chunks outside the rows' pod span get their chunk flag cleared (one
+// vector store), each chunk of the span is one pass (lane = word) storing the chunk dense when it has
+// a bit, and the row's word span and chunk mask are plain stores (the row's only writer), as
+// ip_rows_range_blk leaves them.
+struct DIPIv {
+  uint32_t peer, fam, ivoff, ivcnt;  // fam 0 = IPv4, 1 = IPv6; intervals ipv_iv[ivoff .. ivoff + ivcnt), ascending
+};
+constexpr uint32_t IPV_MAX = 16;  // intervals an interval-built row may have (1 + its same-family excepts)
+__device__ __forceinline__ uint64_t pod_span_bits(uint32_t w, uint32_t x, uint32_t y) {  // pods [x, y) in word w
+  const uint32_t b0 = w * 64, a = max(x, b0), b = min(y, b0 + 64);
+  if (b <= a) return 0ull;
+  const uint32_t lo = a - b0, n = b - a;
+  return (n == 64 ? ~0ull : ((1ull << n) - 1)) << lo;
+}
+__device__ __forceinline__ void ip_rows_iv_blk(uint32_t Rv, uint32_t W, const DIPIv* __restrict__ rt,
+                                               const uint2* __restrict__ iv, const DWordIP* __restrict__ words,
+                                               uint64_t* __restrict__ PM, uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz,
+                                               uint32_t bid_, uint32_t c0, uint32_t nch) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t r = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6));  // wave-uniform
+  if (r >= Rv) return;
+  const DIPIv t = rt[r];
+  const uint32_t j = t.peer, cw = (W + 63) / 64;
+  // the rows' pod span [p0, p1) -> its chunks [s0, s1] (empty: s0 > s1)
+  const uint32_t p0 = t.ivcnt ? iv[t.ivoff].x : 0u, p1 = t.ivcnt ? iv[t.ivoff + t.ivcnt - 1].y : 0u;
+  const uint32_t s0 = max(c0, p0 / 4096), s1 = p1 > p0 ? min(c0 + nch, (p1 - 1) / 4096 + 1) : 0u;  // [s0, s1)
+  // chunks of the window outside the span: no bit (their PM words are not written)
+  for (uint32_t c = c0 + lane; c < c0 + nch; c += 64)
+    if (c < s0 || c >= s1) cnz[uint64_t(j) * cw + c] = 0;
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  uint64_t chunks = 0;
+  for (uint32_t c = s0; c < s1; c++) {
+    const uint32_t w = c * 64 + lane;
+    uint64_t v = 0;
+    if (w < W) {
+      const DWordIP& wd = words[w];
+      const uint64_t fm = t.fam ? wd.m6 : wd.m4;
+      for (uint32_t i = 0; i < t.ivcnt; i++) {  // (scalar loads: the intervals are wave-uniform)
+        const uint2 x = iv[t.ivoff + i];
+        v |= pod_span_bits(w, x.x, x.y);
+      }
+      v &= fm;
+    }
+    const uint64_t nz = __ballot(v != 0);
+    if (nz && w < W) PM[uint64_t(j) * W + w] = v;  // chunk-dense: every word of a chunk with a bit
+    if (lane == 0) cnz[uint64_t(j) * cw + c] = nz ? 1u : 0u;
+    if (nz) {
+      lo = min(lo, c * 64 + uint32_t(__ffsll((unsigned long long)nz) - 1));
+      hi = max(hi, c * 64 + 63 - uint32_t(__clzll((long long)nz)));
+      if (c < 64) chunks |= 1ull << c;
+    }
+  }
+  if (lane == 0) {
+    rng[4 * j] = lo;
+    rng[4 * j + 1] = lo == 0xFFFFFFFFu ? 0xFFFFFFFFu : ~hi;
+    reinterpret_cast<unsigned long long*>(rng)[2 * j + 1] = ~chunks;
+  }
+}
+__global__ __launch_bounds__(256) void k_ip_rows_iv(uint32_t Rv, uint32_t W, const DIPIv* __restrict__ rt, const uint2* __restrict__ iv,
+                                                    const DWordIP* __restrict__ words, uint64_t* __restrict__ PM,
+                                                    uint32_t* __restrict__ rng, uint32_t* __restrict__ cnz, uint32_t c0, uint32_t nch) {
+  ip_rows_iv_blk(Rv, W, rt, iv, words, PM, rng, cnz, blockIdx.x, c0, nch);
+}
+
 // A block handles one group of `grp` IP peers over 4 chunks of 64 words (a wave per chunk, lane =
 // word): the group's tests and their except records are staged into LDS once (one coalesced load
 // per block, instead of a chain of dependent scalar loads per peer and except), and each wave loads

@@ -25,6 +25,7 @@
 #include <dlfcn.h>
 #include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <csignal>
 #include <cstdlib>
@@ -55,6 +56,7 @@
 #include "dev_front.hpp"
 #include "dev_emit.hpp"
 #include "dev_query.hpp"
+#include "dev_gather.hpp"
 
 // Host side: context, planner, enqueueing; the C ABI below
 #include "ctx.hpp"
@@ -63,7 +65,8 @@
 
 extern "C" {
 
-const char* cyc_version(void) { return "cyclonus_hip 0.1 (gfx950)"; }
+const char* cyc_version(void) { return "cyclonus_hip 0.2 (gfx950, ABI 2)"; }
+int cyc_abi_version(void) { return CYC_ABI_VERSION; }
 
 // Diagnostic (env CYC_SEGV_TRACE=1): on SIGSEGV print the native frames as module + offset
 // (resolve offline with addr2line -e <module> <offset>), then die with the default action.
@@ -132,6 +135,7 @@ void cyc_ctx_destroy(cyc_ctx* c) {
     if (c->ports_ev) (void)hipEventDestroy(c->ports_ev);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    comm_release(c);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -582,9 +586,9 @@ int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
   if (!c->ran) return fail(c, CYC_ERR_ARG, "no run yet");
   return guarded(c, [&]() -> int {
     DeviceGuard dg(c->device);
-    // the device, not an event recorded after every run: an event at each step's end held the next
-    // step's first launch ~4.5 us (config #2: 0.0640 -> 0.0598 ms per step without it, r05at)
-    HIPCHK(hipDeviceSynchronize());
+    // the last run's stream, not an event recorded after every run: an event at each step's end held
+    // the next step's first launch ~4.5 us (config #2: 0.0640 -> 0.0598 ms per step without it, r05at)
+    HIPCHK(hipStreamSynchronize(c->last_stream));
     for (int d = 0; d < 2; d++) {
       uint32_t v = 0xFFFFFFFFu;
       if (c->dir[d].n && c->n_act[d]) HIPCHK(hipMemcpy(&v, c->dir[d].rep_cnt(), 4, hipMemcpyDeviceToHost));
@@ -624,6 +628,11 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
       c->ip_range = int(value);
       c->order_lo = c->order_hi = -1;  // the next run re-plans which IP rows are range-built
     }
+    else if (n == "ip_iv") {
+      range(-1, 1);
+      c->ip_iv = int(value);
+      c->order_lo = c->order_hi = -1;  // the next run re-plans which IP rows are interval-built
+    }
     else if (n == "member_wave") range(-1, 1), c->member_wave = int(value);
     else if (n == "class_rpb") range(0, 64), c->class_rpb_opt = value;
     else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
@@ -633,6 +642,11 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "step_events") range(0, 1), c->step_events = int(value);
     else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
     else if (n == "emit_split") range(1, 8), c->emit_split = int(value);
+    else if (n == "emit_footprint") {
+      range(1, 8);
+      c->emit_footprint = int(value);
+      c->order_lo = c->order_hi = -1;  // the row order is re-planned
+    }
     else if (n == "emit_buf") range(0, 2), c->emit_buf = int(value);
     else if (n == "ip_items") {
       range(-1, 1);
@@ -658,6 +672,8 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "front_fused") *value = c->front_fused;
   else if (n == "pod_rows") *value = c->pod_rows;
   else if (n == "ip_range") *value = c->ip_range;
+  else if (n == "ip_iv") *value = c->ip_iv;
+  else if (n == "ip_iv_rows") *value = c->Rv;  // (the last range plan's interval-built rows)
   else if (n == "member_wave") *value = c->member_wave;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "pl_wave") *value = c->pl_wave;
@@ -671,6 +687,7 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "step_events") *value = c->step_events;
   else if (n == "emit_interleave") *value = c->emit_interleave;
   else if (n == "emit_split") *value = c->emit_split;
+  else if (n == "emit_footprint") *value = c->emit_footprint;
   else if (n == "ip_items") *value = c->ip_items_opt;
   else if (n == "emit_buf") *value = c->emit_buf;
   else if (n == "plvt_max_mb") *value = c->plvt_max_mb;
@@ -926,3 +943,6 @@ int cyc_query_targets(cyc_ctx* c, const char* js, size_t len, char* out_json, si
 }
 
 }  // extern "C"
+
+// Multi-GPU table assembly: the RCCL communicator and the all-gather of row shards (C ABI included)
+#include "comm.hpp"

@@ -102,6 +102,11 @@ static void enq_peer_rows(cyc_ctx* c, int d, hipStream_t st, int which = PEERS_P
       k_pod_rows<false><<<g, 256, 0, st>>>(Rp, E, W, plist, ido, c->word_off.as<uint32_t>(), c->run_e.as<uint32_t>(),
                                            c->run_mask.as<uint64_t>(), c->PM.as<uint64_t>(), c->ER.as<uint64_t>(), w0, nw);
   }
+  const uint32_t v0 = c->rv_off[dlo], Rv = (which & PEERS_IP) ? c->rv_off[dhi] - v0 : 0u;
+  if (Rv && nw)
+    k_ip_rows_iv<<<(Rv + 3) / 4, 256, 0, st>>>(Rv, W, c->ipv_tests.as<DIPIv>() + v0, c->ipv_iv.as<uint2>(),
+                                             c->ip_words.as<DWordIP>(), c->PM.as<uint64_t>(), c->ip_rng.as<uint32_t>(), ip_cnz(c),
+                                             c0, nch);
   const uint32_t q0 = c->rr_off[dlo], Rr = (which & PEERS_IP) ? c->rr_off[dhi] - q0 : 0u;
   if (Rr && nw)
     k_ip_rows_range<<<(Rr + 3) / 4, 256, 0, st>>>(Rr, W, c->ipr_tests.as<DIPRange>() + q0, c->ipr_iv.as<uint2>(),
@@ -415,9 +420,15 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
                                             : uint64_t(nr[0]) * rw[0] * 8 >= (8ull << 30) ? 1u : 0u;
     // emit_split > 1: consecutive parts of both planes' row lists (class-clustered, so nearly address
     // order) as separate launches, the first carrying the status copy and the span reset
-    const uint32_t parts = uint32_t(std::max(1, std::min<int>(c->emit_split, int(std::max<uint32_t>(nr[0], 1)))));
+    // emit_footprint F > 1: launch h over the rows the plan put in address part h (rows i of the run
+    // with i F / n == h: the first ceil(h n / F) rows lie in the parts before h)
+    const bool fp = c->emit_footprint > 1;
+    const uint32_t parts = uint32_t(std::max(1, std::min<int>(fp ? c->emit_footprint : c->emit_split,
+                                                              int(std::max<uint32_t>(nr[0], 1)))));
     for (uint32_t h = 0; h < parts; h++) {
-      const uint32_t r0 = uint32_t(uint64_t(nr[0]) * h / parts), r1 = uint32_t(uint64_t(nr[0]) * (h + 1) / parts);
+      const uint32_t r0 = fp ? uint32_t((uint64_t(nr[0]) * h + parts - 1) / parts) : uint32_t(uint64_t(nr[0]) * h / parts);
+      const uint32_t r1 = fp ? uint32_t((uint64_t(nr[0]) * (h + 1) + parts - 1) / parts)
+                             : uint32_t(uint64_t(nr[0]) * (h + 1) / parts);
       EmitArgs e1 = ea;
       e1.n_rows[0] = e1.n_rows[1] = r1 - r0;
       for (int pl = 0; pl < 2; pl++) e1.order[pl] = ea.order[pl] + r0;
@@ -537,6 +548,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   fb.ip_grp = IP_GROUP;
   fb.ipr_iv = c->ipr_iv.as<uint2>();
   fb.ipsort = c->ipsort.as<uint32_t>();
+  fb.ipv_iv = c->ipv_iv.as<uint2>();
   fb.ip_ilist = c->ipi_list.as<uint32_t>();
   for (int x = 0; x < 2; x++) {
     const int dlo = one_win ? 0 : x, dhi = one_win ? 2 : x + 1;
@@ -553,6 +565,9 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fb.Rr[x] = one_win && x ? 0u : c->rr_off[dhi] - c->rr_off[dlo];
     fb.rtests[x] = c->ipr_tests.as<DIPRange>() + c->rr_off[dlo];
     fb.nb[9 + x] = fb.Rr[x] && fb.inch[x] ? blocks((uint64_t(fb.Rr[x]) + 3) / 4) : 0u;
+    fb.Rv[x] = one_win && x ? 0u : c->rv_off[dhi] - c->rv_off[dlo];
+    fb.vtests[x] = c->ipv_tests.as<DIPIv>() + c->rv_off[dlo];
+    fb.nb[11 + x] = fb.Rv[x] && fb.inch[x] ? blocks((uint64_t(fb.Rv[x]) + 3) / 4) : 0u;
   }
   fb.E = E;
   fb.EW = EW;
@@ -951,6 +966,7 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
     c->timed_graph = false;
   }
   c->ran = true;
+  c->last_stream = st;  // cyc_last_classes waits for this stream only
 
   if (!pb.blocks.empty()) return blocks_status(c, st);
 

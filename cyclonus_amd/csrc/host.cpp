@@ -1197,9 +1197,9 @@ std::vector<ProbeConfig> load_probe_configs(const cyc_probe_config* cfgs, int64_
       return std::string(p ? p : "", size_t(n));
     };
     c.port.is_str = cfgs[i].port_is_name != 0;
-    if (c.port.is_str) c.port.s = str(cfgs[i].port_name, cfgs[i].port_name_len, "port_name");
+    if (c.port.is_str) c.port.s = str(cfgs[i].port_name_ptr, cfgs[i].port_name_len, "port_name");
     else c.port.i = cfgs[i].port;
-    c.proto = str(cfgs[i].protocol, cfgs[i].protocol_len, "protocol");
+    c.proto = str(cfgs[i].protocol_ptr, cfgs[i].protocol_len, "protocol");
   }
   return out;
 }

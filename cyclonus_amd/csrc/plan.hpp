@@ -196,6 +196,16 @@ static void prepare_device(cyc_ctx* c) {
     c->ipsort_host = p4;
     c->ipsort_host.insert(c->ipsort_host.end(), p6.begin(), p6.end());
     upload(c->ipsort, c->ipsort_host);
+    // a family whose pods' addresses never decrease in pod order (addresses handed out in pod order:
+    // configs #2-#4) sorts to pod order, so its sorted positions ARE its pods in pod order: a network's
+    // pods of that family are then pod-index intervals (ip_rows_iv_blk)
+    auto mono = [](const std::vector<uint32_t>& pods) {
+      for (size_t x = 1; x < pods.size(); x++)
+        if (pods[x] < pods[x - 1]) return false;
+      return true;
+    };
+    c->ip_mono[0] = mono(p4);
+    c->ip_mono[1] = mono(p6);
   }
   upload(c->cidrs, pb.cidrs);
   upload(c->ipbs, pb.ipbs);
@@ -625,8 +635,13 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
     std::iota(ord.begin(), ord.end(), uint32_t(c->rl[d]));
     const auto& i1 = c->ids[d].of_pod;
     const auto& i2 = c->ids[1 - d].of_pod;
-    std::stable_sort(ord.begin(), ord.end(),
-                     [&](uint32_t x, uint32_t y) { return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y]; });
+    // emit_footprint F > 1 (target rows): the list is F address parts of the rows, each clustered
+    const uint64_t F = src ? 1u : uint64_t(c->emit_footprint), nrow = std::max<uint64_t>(ord.size(), 1);
+    auto part = [&](uint32_t x) { return (uint64_t(x) - uint64_t(c->rl[d])) * F / nrow; };
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+      if (part(x) != part(y)) return part(x) < part(y);
+      return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y];
+    });
     std::vector<uint32_t> pairs(ord.size() * 2);
     for (size_t r = 0; r < ord.size(); r++) {
       pairs[2 * r] = ord[r];
@@ -738,29 +753,31 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   // same-family except), their count and word span: built from ranges when few and close
   // (no-panic runs only: the ordered walk with panic bits keeps its dense rows)
   const uint32_t n4 = uint32_t(c->ip4_key.size());
-  auto range_rows = [&](const DIPTest& t, DIPRange& out) -> bool {
-    if (pb.may_err || !t.cidr.valid || c->ip_range == 0) return false;
-    auto bounds = [&](const DCidr& cd, uint32_t& a, uint32_t& b) {
-      if (cd.fam == 4) {
-        const uint32_t lo = cd.net[3] & cd.mask[3], hi = lo | ~cd.mask[3];
-        a = uint32_t(std::lower_bound(c->ip4_key.begin(), c->ip4_key.end(), lo) - c->ip4_key.begin());
-        b = uint32_t(std::upper_bound(c->ip4_key.begin(), c->ip4_key.end(), hi) - c->ip4_key.begin());
-      } else {
-        std::array<uint32_t, 4> lo, hi;
-        for (int i = 0; i < 4; i++) {
-          lo[i] = cd.net[i] & cd.mask[i];
-          hi[i] = lo[i] | ~cd.mask[i];
-        }
-        a = n4 + uint32_t(std::lower_bound(c->ip6_key.begin(), c->ip6_key.end(), lo) - c->ip6_key.begin());
-        b = n4 + uint32_t(std::upper_bound(c->ip6_key.begin(), c->ip6_key.end(), hi) - c->ip6_key.begin());
+  // a network's pods of its family as positions [a, b) of the address index (ipsort_host)
+  auto bounds = [&](const DCidr& cd, uint32_t& a, uint32_t& b) {
+    if (cd.fam == 4) {
+      const uint32_t lo = cd.net[3] & cd.mask[3], hi = lo | ~cd.mask[3];
+      a = uint32_t(std::lower_bound(c->ip4_key.begin(), c->ip4_key.end(), lo) - c->ip4_key.begin());
+      b = uint32_t(std::upper_bound(c->ip4_key.begin(), c->ip4_key.end(), hi) - c->ip4_key.begin());
+    } else {
+      std::array<uint32_t, 4> lo, hi;
+      for (int i = 0; i < 4; i++) {
+        lo[i] = cd.net[i] & cd.mask[i];
+        hi[i] = lo[i] | ~cd.mask[i];
       }
-    };
-    std::vector<uint2> iv(1);
+      a = n4 + uint32_t(std::lower_bound(c->ip6_key.begin(), c->ip6_key.end(), lo) - c->ip6_key.begin());
+      b = n4 + uint32_t(std::upper_bound(c->ip6_key.begin(), c->ip6_key.end(), hi) - c->ip6_key.begin());
+    }
+  };
+  // ipaddress.go:22-40 on the index: the CIDR's positions less each same-family except's (an except of
+  // the other family never contains a pod of this one); false if an except does not parse
+  auto index_intervals = [&](const DIPTest& t, std::vector<uint2>& iv) -> bool {
+    iv.assign(1, uint2{});
     bounds(t.cidr, iv[0].x, iv[0].y);
     for (uint32_t e = 0; e < t.excnt; e++) {
       const DCidr& x = c->plan.ip_ex[t.exoff + e];
       if (!x.valid) return false;
-      if (x.fam != t.cidr.fam) continue;  // an except of the other family never contains a pod of this one
+      if (x.fam != t.cidr.fam) continue;
       uint32_t ea, eb;
       bounds(x, ea, eb);
       std::vector<uint2> next;
@@ -772,6 +789,26 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
       for (const uint2& v : next)
         if (v.y > v.x) iv.push_back(v);
     }
+    if (!iv.empty() && iv[0].y <= iv[0].x) iv.clear();  // a network holding no pod: no interval
+    return true;
+  };
+  // IP rows as pod intervals: the family is address-monotone in pod order, so positions [a, b) of the
+  // index are its pods ipsort_host[a] < ... < ipsort_host[b - 1] and nothing else of the family lies
+  // between them: the row is the family's pods of pod indices [ipsort_host[a], ipsort_host[b - 1]]
+  std::vector<DIPIv> vtests;
+  std::vector<uint2> viv;
+  auto iv_rows = [&](const DIPTest& t, DIPIv& out) -> bool {
+    if (pb.may_err || !t.cidr.valid || c->ip_iv == 0 || !c->ip_mono[t.cidr.fam == 4 ? 0 : 1]) return false;
+    std::vector<uint2> iv;
+    if (!index_intervals(t, iv) || iv.size() > IPV_MAX) return false;
+    out = DIPIv{t.peer, t.cidr.fam == 4 ? 0u : 1u, uint32_t(viv.size()), uint32_t(iv.size())};
+    for (const uint2& v : iv) viv.push_back(make_uint2(c->ipsort_host[v.x], c->ipsort_host[v.y - 1] + 1));
+    return true;
+  };
+  auto range_rows = [&](const DIPTest& t, DIPRange& out) -> bool {
+    if (pb.may_err || !t.cidr.valid || c->ip_range == 0) return false;
+    std::vector<uint2> iv;
+    if (!index_intervals(t, iv)) return false;
     uint64_t n = 0;
     for (const uint2& v : iv) n += v.y - v.x;
     if (n > IPR_MAX_MATCH) return false;
@@ -797,6 +834,7 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
     c->rp_off[d] = uint32_t(pp.size());
     c->ri_off[d] = uint32_t(ip.size());
     c->rr_off[d] = uint32_t(rtests.size());
+    c->rv_off[d] = uint32_t(vtests.size());
     for (uint32_t j : c->plan.pod_peers)
       if (peer_needed[j] && peer_dir[j] == d) pp.push_back(j);
     std::map<std::vector<uint32_t>, uint32_t> ipb_row;
@@ -812,6 +850,11 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
         prow[j] = it.first->second;
         continue;
       }
+      DIPIv vt{};
+      if (iv_rows(c->plan.ip_tests[r], vt)) {
+        vtests.push_back(vt);
+        continue;
+      }
       DIPRange rt{};
       if (range_rows(c->plan.ip_tests[r], rt)) {
         rtests.push_back(rt);
@@ -825,6 +868,10 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   c->Rr = uint32_t(rtests.size());
   upload(c->ipr_tests, rtests);
   upload(c->ipr_iv, riv);
+  c->rv_off[2] = uint32_t(vtests.size());
+  c->Rv = uint32_t(vtests.size());
+  upload(c->ipv_tests, vtests);
+  upload(c->ipv_iv, viv);
   upload(c->peer_row, prow);
   c->prow_host = prow;
   c->rp_off[2] = uint32_t(pp.size());

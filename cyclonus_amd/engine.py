@@ -166,6 +166,52 @@ class Engine:
                                                    ctypes.byref(t)))
         return DeviceTable(t)
 
+    # ---------------------------------------------------------------- multi-GPU assembly (RCCL, comm.hpp)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """cyc_comm_unique_id: the 128-byte RCCL unique id rank 0 makes and hands to every rank."""
+        buf = (ctypes.c_uint8 * 128)()
+        rc = lib().cyc_comm_unique_id(buf)
+        if rc != _lib.OK:
+            raise _lib.CyclonusError(rc, "cyc_comm_unique_id failed")
+        return bytes(buf)
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        """cyc_comm_init: collective over the ranks; the context owns the communicator."""
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(self._ctx, lib().cyc_comm_init(self._ctx, int(nranks), int(rank), buf))
+        return self
+
+    def comm_destroy(self):
+        check(self._ctx, lib().cyc_comm_destroy(self._ctx))
+
+    def rows_shard(self, nranks: int, rank: int, partition: str = "source"):
+        """cyc_rows_shard: rank's rows [lo, hi) of the library's partition of the prepared pods."""
+        lo, hi = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(self._ctx, lib().cyc_rows_shard(self._ctx, _lib.PARTITIONS[partition], int(nranks), int(rank),
+                                              ctypes.byref(lo), ctypes.byref(hi)))
+        return int(lo.value), int(hi.value)
+
+    def planes_allgather(self, d_ingress: int, d_egress: int, d_ingress_full: int, d_egress_full: int, stream: int = 0,
+                         partition: str = "source"):
+        """cyc_planes_allgather (collective): this rank's shard planes -> the whole [P][K][W] planes."""
+        check(self._ctx, lib().cyc_planes_allgather(self._ctx, ctypes.c_void_p(stream or None), _lib.PARTITIONS[partition],
+                                                    ctypes.c_void_p(d_ingress), ctypes.c_void_p(d_egress),
+                                                    ctypes.c_void_p(d_ingress_full), ctypes.c_void_p(d_egress_full)))
+
+    def table_allgather(self, shard: "DeviceTable") -> "DeviceTable":
+        """cyc_table_allgather (collective): a whole device table from this rank's shard table."""
+        t = ctypes.c_void_p()
+        check(self._ctx, lib().cyc_table_allgather(self._ctx, shard._t, ctypes.byref(t)))
+        return DeviceTable(t)
+
+    def merge_sources(self, d_slices, d_ingress_full: int, stream: int = 0):
+        """cyc_rows_merge_sources: every source shard's ingress slices (device pointers, rank order) ->
+        the whole ingress plane, on one GPU."""
+        arr = (ctypes.c_void_p * len(d_slices))(*[ctypes.c_void_p(p) for p in d_slices])
+        check(self._ctx, lib().cyc_rows_merge_sources(self._ctx, ctypes.c_void_p(stream or None), len(d_slices), arr,
+                                                      ctypes.c_void_p(d_ingress_full)))
+
     # ---------------------------------------------------------------- batched blocks
     def prepare_blocks(self, probes, block_end, block_config) -> dict:
         """Batched independent problems (cyc_probe_prepare_blocks): block b = pods

@@ -39,8 +39,8 @@ class TrafficTablesC(ctypes.Structure):
 
 class ProbeConfigC(ctypes.Structure):
     _fields_ = [("all_available", ctypes.c_int32), ("port_is_name", ctypes.c_int32), ("port", ctypes.c_int32),
-                ("port_name", ctypes.c_char_p), ("port_name_len", ctypes.c_int64),
-                ("protocol", ctypes.c_char_p), ("protocol_len", ctypes.c_int64)]
+                ("port_name_ptr", ctypes.c_char_p), ("port_name_len", ctypes.c_int64),
+                ("protocol_ptr", ctypes.c_char_p), ("protocol_len", ctypes.c_int64)]
 
 
 class PolicyTablesC(ctypes.Structure):
@@ -151,6 +151,25 @@ class ResourceTables:
         self.c, self._keep = t, keep
 
 
+def _field(d, name, default=None, nullable=False):
+    """A struct field of a decoded JSON object as encoding/json fills it: keys match the field name
+    case-insensitively and, among several keys naming the field, the last one wins; a JSON null
+    leaves a scalar field unchanged and sets a pointer / map field (nullable) to nil — the JSON entry
+    points' rule (csrc/cjson.hpp)."""
+    got = default
+    if isinstance(d, dict):
+        low = name.lower()
+        for k, v in d.items():
+            if isinstance(k, str) and k.lower() == low and (v is not None or nullable):
+                got = v
+    return got
+
+
+def _go_int32(x) -> int:
+    """int32(x) of a Go int (two's-complement wrap), as the JSON path stores ResolvedPort."""
+    return ((int(x) + (1 << 31)) & 0xFFFFFFFF) - (1 << 31)
+
+
 class TrafficTables:
     """cyc_traffic_tables of matcher.Traffic values {"Source": peer, "Destination": peer, "ResolvedPort",
     "ResolvedPortName", "Protocol"}, peer = {"Internal": None | {"PodLabels", "NamespaceLabels",
@@ -161,22 +180,23 @@ class TrafficTables:
         internal, ip, ns, lcnt, lk, lv, ncnt, nk, nv = ([] for _ in range(9))
         port, pname, proto = [], [], []
         for t in traffics:
-            for end in (t.get("Source") or {}, t.get("Destination") or {}):
-                inner = end.get("Internal")
+            for end in (_field(t, "Source", {}, True) or {}, _field(t, "Destination", {}, True) or {}):
+                inner = _field(end, "Internal", None, True)
                 internal.append(0 if inner is None else 1)
-                ip.append(S(end.get("IP")))
+                ip.append(S(_field(end, "IP")))
                 inner = inner or {}
-                ns.append(S(inner.get("Namespace")))
-                labels, nsl = inner.get("PodLabels") or {}, inner.get("NamespaceLabels") or {}
+                ns.append(S(_field(inner, "Namespace")))
+                labels = _field(inner, "PodLabels", None, True) or {}
+                nsl = _field(inner, "NamespaceLabels", None, True) or {}
                 lcnt.append(len(labels))
                 lk += [S(k) for k in labels]
                 lv += [S(v) for v in labels.values()]
                 ncnt.append(len(nsl))
                 nk += [S(k) for k in nsl]
                 nv += [S(v) for v in nsl.values()]
-            port.append(int(t.get("ResolvedPort") or 0))
-            pname.append(S(t.get("ResolvedPortName")))
-            proto.append(S(t.get("Protocol")))
+            port.append(_go_int32(_field(t, "ResolvedPort", 0)))
+            pname.append(S(_field(t, "ResolvedPortName")))
+            proto.append(S(_field(t, "Protocol")))
         c = TrafficTablesC()
         c.str = S.table(keep)
         c.n = len(port)
@@ -212,11 +232,11 @@ class ProbeConfigs:
             pp = p.get("PortProtocol") or p
             port, proto = pp.get("Port"), (pp.get("Protocol") or "").encode()
             self._keep.append(proto)
-            self.c[i].protocol, self.c[i].protocol_len = proto, len(proto)
+            self.c[i].protocol_ptr, self.c[i].protocol_len = proto, len(proto)
             if isinstance(port, str):
                 b = port.encode()
                 self._keep.append(b)
-                self.c[i].port_is_name, self.c[i].port_name, self.c[i].port_name_len = 1, b, len(b)
+                self.c[i].port_is_name, self.c[i].port_name_ptr, self.c[i].port_name_len = 1, b, len(b)
             else:
                 self.c[i].port = int(port or 0)
 
@@ -386,11 +406,11 @@ def dump_probe_configs(probes, path):
     with open(path, "w") as f:
         for i in range(pc.n):
             c = pc.c[i]
-            proto = (c.protocol or b"").decode()
+            proto = (c.protocol_ptr or b"").decode()
             if c.all_available:
                 f.write("all\n")
             elif c.port_is_name:
-                f.write(f"name {c.port_name.decode()} {proto}\n")
+                f.write(f"name {c.port_name_ptr.decode()} {proto}\n")
             else:
                 f.write(f"int {c.port} {proto}\n")
 

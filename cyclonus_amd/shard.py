@@ -8,9 +8,12 @@
 * "target": rank r owns target pods [lo, hi) of BOTH planes (ingress rows keyed by destination,
   egress rows keyed by source).
 
-Every verdict depends only on replicated inputs: nothing on the data path is exchanged.  `assemble`
-/ `assemble_sources` are the optional RCCL all-gathers (torch.distributed, backend "nccl" on ROCm)
-that materialise the whole table on every rank.
+Every verdict depends only on replicated inputs: nothing on the data path is exchanged.  The whole
+table on every rank is the library's own collective (cyc_comm_init + cyc_planes_allgather /
+cyc_table_allgather, csrc/comm.hpp: RCCL broadcasts plus a HIP relayout kernel) — what a cgo host
+calls and bench.py times.  `assemble` / `assemble_sources` below are the same assembly in
+torch.distributed, for process groups the library's RCCL communicator cannot join (gloo: the CPU
+tests and one-GPU rehearsals).  The ranges here must equal cyc_rows_shard's (test_gpu_assemble).
 """
 from __future__ import annotations
 
@@ -53,7 +56,8 @@ def _send(local, n, shape, dim):
 def assemble(local_rows, P: int, group=None, partition: str = "target"):
     """All-gather row shards [rows, K, W] (target rows of either plane, or a source partition's egress
     rows) into the full [P, K, W] plane on every rank.  Shards are padded to the largest shard so a
-    single all-gather moves them."""
+    single all-gather moves them.  The result may alias its inputs: at world 1 it is a view of
+    `local_rows`, with equal shards a view of the gather buffer — clone() it if `local_rows` is reused."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
@@ -75,7 +79,8 @@ def assemble(local_rows, P: int, group=None, partition: str = "target"):
 
 def assemble_sources(local_ingress, P: int, group=None):
     """All-gather a source partition's ingress slices [P, K, Wr] (each rank: the words of its
-    sources in every destination's row) into the full [P, K, W] ingress plane on every rank."""
+    sources in every destination's row) into the full [P, K, W] ingress plane on every rank.  At world 1
+    the result is a view of `local_ingress` (clone() it if that buffer is reused)."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)

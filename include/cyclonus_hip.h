@@ -81,7 +81,13 @@ typedef struct {
   int64_t max_word_runs; /* most egress-identity runs in one 64-pod word */
 } cyc_probe_shape;
 
+/* ABI revision of this header: bumped whenever a struct's layout or a field's meaning changes.  A
+ * binding checks cyc_abi_version() == CYC_ABI_VERSION once at start-up so a library and a binding
+ * built against different headers fail loudly instead of misreading each other's structs. */
+#define CYC_ABI_VERSION 2
+
 /* context / errors */
+int cyc_abi_version(void);
 int cyc_ctx_create(int device_id, cyc_ctx** out);
 void cyc_ctx_destroy(cyc_ctx* ctx);
 const char* cyc_last_error(const cyc_ctx* ctx);
@@ -139,10 +145,12 @@ typedef struct {
   int32_t all_available;  /* 1: one job per destination container (resources.go:336-364) */
   int32_t port_is_name;   /* intstr.Type: 0 Int (port), 1 String (port_name) */
   int32_t port;
-  /* Go strings as (pointer, byte length): any bytes, NUL included; NULL with length 0 = "" */
-  const char* port_name;  /* the named port */
+  /* Go strings as (pointer, byte length): any bytes, NUL included; NULL with length 0 = "".
+   * (ABI 2 renamed the pointers from port_name / protocol when the lengths were added, so a caller
+   * written against ABI 1 that set only the pointer no longer compiles.) */
+  const char* port_name_ptr;  /* the named port */
   int64_t port_name_len;
-  const char* protocol;   /* the raw protocol string (compared as is: "tcp" != "TCP") */
+  const char* protocol_ptr;   /* the raw protocol string (compared as is: "tcp" != "TCP") */
   int64_t protocol_len;
 } cyc_probe_config;
 
@@ -289,6 +297,41 @@ int cyc_table_shape(const cyc_table* t, int64_t* out, int n);
 const char* cyc_table_error(const cyc_table* t);
 void cyc_table_destroy(cyc_table* t);
 
+/* ---- Multi-GPU table assembly over RCCL (north_star: "Source-pod rows shard across the 8 GPUs of one
+ * node, with an RCCL all-gather over xGMI only to assemble the final table").  One process per GPU,
+ * each with its own context.  The shards need no exchange (cyc_probe_run_rows); a Go multi-GPU
+ * Runner.RunProbeForConfig (pkg/connectivity/probe/jobrunner.go:29-31) that returns a whole *Table on
+ * every rank assembles it with these.  Rank 0 makes the unique id, the host hands its 128 bytes to
+ * every rank by its own means (e.g. over the same channel that started the ranks), and every rank
+ * calls cyc_comm_init with it; the context owns the communicator until cyc_comm_destroy or
+ * cyc_ctx_destroy.  RCCL failures return CYC_ERR_RCCL with RCCL's message. */
+#define CYC_COMM_ID_BYTES 128 /* ncclUniqueId */
+int cyc_comm_unique_id(uint8_t* id);  /* id: CYC_COMM_ID_BYTES bytes (needs no context) */
+int cyc_comm_init(cyc_ctx* ctx, int nranks, int rank, const uint8_t* id);  /* collective over the ranks */
+int cyc_comm_destroy(cyc_ctx* ctx);
+/* The library's partition of the prepared pods over nranks: rank `rank`'s rows [*row_lo, *row_hi)
+ * under `partition` (target rows balanced to a row; source rows to a 64-pod word).  The all-gathers
+ * below assume every rank ran exactly these rows. */
+int cyc_rows_shard(cyc_ctx* ctx, int partition, int nranks, int rank, int64_t* row_lo, int64_t* row_hi);
+/* Collective: every rank passes its shard planes (cyc_probe_run_rows output for its cyc_rows_shard
+ * rows, complete on `hip_stream` or before) and receives the whole [P][K][W] ingress and egress
+ * planes (cyc_probe_run's layout over rows [0, P)) in d_ingress_full / d_egress_full, enqueued on
+ * `hip_stream` (asynchronous).  Row shares move by grouped RCCL broadcasts straight into place (in
+ * place when a shard already sits at its rows of the full plane); a source partition's ingress slices
+ * are gathered in ~256 MB chunks and scattered into whole rows by a HIP kernel (two scratch buffers
+ * the context keeps).  The status plane is whole on every rank already (cyc_probe_run_rows). */
+int cyc_planes_allgather(cyc_ctx* ctx, void* hip_stream, int partition, const uint64_t* d_ingress,
+                         const uint64_t* d_egress, uint64_t* d_ingress_full, uint64_t* d_egress_full);
+/* Collective, on a device-resident table: `shard` is this rank's cyc_table_run_rows /
+ * cyc_table_wrap_rows table for its cyc_rows_shard rows; *out becomes a whole table (target rows
+ * [0, P), planes it owns) answering Table.Get(from, to) for every pair on every rank.  Synchronous. */
+int cyc_table_allgather(cyc_ctx* ctx, const cyc_table* shard, cyc_table** out);
+/* One GPU, no communicator: the whole ingress plane from all nranks source shards' ingress slices
+ * (d_slices[r] = rank r's [P][K][Wr_r] plane for its cyc_rows_shard source rows) — the relayout step of
+ * cyc_planes_allgather on its own (enqueued on hip_stream). */
+int cyc_rows_merge_sources(cyc_ctx* ctx, void* hip_stream, int nranks, const uint64_t* const* d_slices,
+                           uint64_t* d_ingress_full);
+
 /* ---- Batched independent problems ("blocks", SURVEY §8f row 3: the generate sweep's many small
  * probe problems, interpreter.go:137-148, in one pass).  Resources.Pods is cut into consecutive pod
  * ranges: block b = pods [block_end[b-1], block_end[b]) answering probe config block_config[b] (an
@@ -321,7 +364,7 @@ const char* cyc_block_error(const cyc_ctx* ctx, int64_t block);
 int cyc_last_timings(cyc_ctx* ctx, double* ms, int n);
 
 /* Diagnostic: number of distinct classes (class rows computed) of the last run, [0] ingress,
- * [1] egress (synchronises the device). */
+ * [1] egress (synchronises the stream the last run was enqueued on, which must still exist). */
 int cyc_last_classes(cyc_ctx* ctx, int64_t* out, int n);
 
 /* What the last enqueued run's emit launched: the kernel name(s) ("k_emit_wide_buf<512,13>",

@@ -31,5 +31,5 @@ common = ["-O3", "-std=c++17", "-fPIC", "-I", b.CSRC, "-I", b.INCLUDE, *defs]
 host = os.path.join(b.BUILD, "host.cpp.o")
 eng = os.path.join(out, "engine.hip.o")
 subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", *common, "-munsafe-fp-atomics", "-c", src, "-o", eng], check=True)
-subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "libcyclonus_hip.so"), host, eng], check=True)
+subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", os.path.join(out, "libcyclonus_hip.so"), host, eng, *b.LIBS], check=True)
 print(os.path.join(out, "libcyclonus_hip.so"))

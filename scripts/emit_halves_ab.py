@@ -56,6 +56,13 @@ VARIANTS = {
     "halves": ({}, [(0, H, 0), (H, P, H)]),
     "halves_il1": ({"emit_interleave": 1}, [(0, H, 0), (H, P, H)]),
     "half_same": ({}, [(0, H, 0), (0, H, 0)]),
+    # VERDICT r5 ask 2 (the footprint hypothesis): one front, the emit as two launches over the address
+    # halves of both planes (rows [0, P/2), then [P/2, P)), each class-clustered within its half; and
+    # each half run alone into its own half of the same planes
+    "fp2": ({"emit_footprint": 2}, [(0, P, 0)]),
+    "fp4": ({"emit_footprint": 4}, [(0, P, 0)]),
+    "first": ({}, [(0, H, 0)]),
+    "second": ({}, [(H, P, H)]),
 }
 
 
@@ -70,7 +77,7 @@ def spec(name):
 
 
 def setv(name):
-    for k, v in (("emit_interleave", -1), ("emit_split", 1)):
+    for k, v in (("emit_interleave", -1), ("emit_split", 1), ("emit_footprint", 1)):
         eng.set_option(k, v)
     for k, v in spec(name)[0].items():
         eng.set_option(k, v)

@@ -190,11 +190,11 @@ struct Configs {
         c[i].all_available = 1;
         continue;
       }
-      c[i].protocol = protos[i].data();
+      c[i].protocol_ptr = protos[i].data();
       c[i].protocol_len = int64_t(protos[i].size());
       if (kinds[i] == "name") {
         c[i].port_is_name = 1;
-        c[i].port_name = names[i].data();
+        c[i].port_name_ptr = names[i].data();
         c[i].port_name_len = int64_t(names[i].size());
       } else {
         c[i].port = int32_t(std::stol(ports[i]));

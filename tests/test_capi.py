@@ -170,3 +170,33 @@ def test_cpp_driver_flat_tables(tmp_path):
     r = subprocess.run([drv, "--flat", *paths, "--no-gpu"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 3 and r.stdout.startswith("error cyc_resources_load rc=%d" % _lib.ERR_ARG), r.stdout
     assert "pod_ns[0] = 99 out of range" in r.stdout, r.stdout
+
+
+def test_comm_entry_points_validate_arguments():
+    """The RCCL assembly entry points refuse bad arguments and calls out of order without touching a
+    GPU (the collectives themselves run in tests/test_gpu_assemble.py)."""
+    import ctypes
+
+    from cyclonus_amd.engine import Engine
+
+    L = _lib.lib()
+    e = Engine(0)
+    uid = (ctypes.c_uint8 * 128)()
+    assert L.cyc_comm_unique_id(None) == _lib.ERR_ARG
+    assert L.cyc_comm_init(None, 1, 0, uid) == _lib.ERR_ARG
+    assert L.cyc_comm_init(e._ctx, 1, 0, None) == _lib.ERR_ARG
+    assert L.cyc_comm_init(e._ctx, 0, 0, uid) == _lib.ERR_ARG
+    assert L.cyc_comm_init(e._ctx, 65, 0, uid) == _lib.ERR_ARG
+    assert L.cyc_comm_init(e._ctx, 2, 2, uid) == _lib.ERR_ARG
+    assert L.cyc_comm_init(e._ctx, 2, -1, uid) == _lib.ERR_ARG
+    lo, hi = ctypes.c_int64(), ctypes.c_int64()
+    assert L.cyc_rows_shard(e._ctx, 1, 2, 0, ctypes.byref(lo), ctypes.byref(hi)) == _lib.ERR_ARG
+    assert b"prepare" in L.cyc_last_error(e._ctx)
+    p = ctypes.c_void_p(16)
+    rc = L.cyc_planes_allgather(e._ctx, None, 1, p, p, p, p)
+    assert rc == _lib.ERR_ARG and b"cyc_comm_init first" in L.cyc_last_error(e._ctx)
+    out = ctypes.c_void_p()
+    assert L.cyc_table_allgather(e._ctx, None, ctypes.byref(out)) == _lib.ERR_ARG
+    assert L.cyc_rows_merge_sources(e._ctx, None, 2, None, p) == _lib.ERR_ARG
+    assert L.cyc_comm_destroy(e._ctx) == _lib.OK  # no communicator: nothing to do
+    assert L.cyc_abi_version() == _lib.ABI_VERSION

@@ -82,14 +82,14 @@ def test_probe_configs():
     pc = flat.ProbeConfigs([{"Port": 80, "Protocol": "TCP"}, {"Port": "serve-81-udp", "Protocol": "UDP"},
                             {"AllAvailable": True}, {"PortProtocol": {"Port": 53, "Protocol": "sctp"}}])
     assert pc.n == 4
-    assert (pc.c[0].port, pc.c[0].port_is_name, pc.c[0].protocol, pc.c[0].protocol_len) == (80, 0, b"TCP", 3)
-    assert (pc.c[1].port_is_name, pc.c[1].port_name, pc.c[1].port_name_len) == (1, b"serve-81-udp", 12)
+    assert (pc.c[0].port, pc.c[0].port_is_name, pc.c[0].protocol_ptr, pc.c[0].protocol_len) == (80, 0, b"TCP", 3)
+    assert (pc.c[1].port_is_name, pc.c[1].port_name_ptr, pc.c[1].port_name_len) == (1, b"serve-81-udp", 12)
     assert pc.c[2].all_available == 1
-    assert (pc.c[3].port, pc.c[3].protocol) == (53, b"sctp")
+    assert (pc.c[3].port, pc.c[3].protocol_ptr) == (53, b"sctp")
     # Go strings may hold NUL bytes: they travel as pointer + length, not as C strings
     pc = flat.ProbeConfigs([{"Port": "a\u0000b", "Protocol": "T\u0000CP"}])
     assert pc.c[0].port_name_len == 3 and pc.c[0].protocol_len == 4
-    addr = ctypes.c_void_p.from_buffer(pc.c[0], flat.ProbeConfigC.protocol.offset).value
+    addr = ctypes.c_void_p.from_buffer(pc.c[0], flat.ProbeConfigC.protocol_ptr.offset).value
     assert ctypes.string_at(addr, 4) == b"T\x00CP"
 
 
@@ -159,3 +159,26 @@ def test_malformed_tables_refused():
                        "b": {"Namespace": "x", "PodSelector": {}, "Peers": None, "SourceRules": []}}, "Egress": {}}
     with pytest.raises(_lib.CyclonusError, match="primary key"):
         Engine(0).load_policy_tables(one)
+
+
+def test_traffic_tables_follow_encoding_json():
+    """The flat traffic tables read a matcher.Traffic dict as encoding/json (and the JSON entry point)
+    would: field names case-insensitively with the last key winning, null pointers / maps as nil, and
+    ResolvedPort stored as int32 (two's-complement wrap) like the JSON path."""
+    a = [{"Source": {"Internal": {"PodLabels": {"a": "b"}, "Namespace": "x"}, "IP": "10.0.0.1"},
+          "Destination": {"Internal": None, "IP": "1.2.3.4"}, "ResolvedPort": 80, "Protocol": "TCP"}]
+    b = [{"source": {"internal": {"podlabels": {"a": "b"}, "NAMESPACE": "x"}, "ip": "10.0.0.1"},
+          "DESTINATION": {"internal": {"Namespace": "y"}, "Internal": None, "Ip": "1.2.3.4"},
+          "resolvedport": 80, "Protocol": "UDP", "protocol": "TCP"}]
+    ta, tb = flat.TrafficTables(a), flat.TrafficTables(b)
+
+    def rows(t):
+        strs = np.ctypeslib.as_array(t.c.str.off, (t.c.str.n + 1,))
+        blob = ctypes.string_at(t.c.str.bytes, int(strs[-1]))
+        s = [blob[strs[i]:strs[i + 1]].decode() for i in range(t.c.str.n)]
+        g = lambda p, n: list(np.ctypeslib.as_array(p, (n,)))  # noqa: E731
+        return (g(t.c.internal, 2), [s[i] for i in g(t.c.ip, 2)], [s[i] for i in g(t.c.ns, 2)], g(t.c.label_off, 3),
+                g(t.c.port, 1), [s[i] for i in g(t.c.protocol, 1)])
+
+    assert rows(ta) == rows(tb)
+    assert flat._go_int32(1 << 31) == -(1 << 31) and flat._go_int32(70000) == 70000 and flat._go_int32((1 << 32) + 80) == 80

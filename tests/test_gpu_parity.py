@@ -374,18 +374,105 @@ def test_ip_interval_words(gpu, seed):
     and on addresses stepping by 256, with the fused front's IP rows as per-chunk work items (ip_items
     auto) or as groups of rows per wave (0), against the oracle."""
     for pols, res, probes in (_ip_interval_problem(seed), _ip_stride_problem(seed)):
-        for ipr, items in ((-1, -1), (0, -1), (1, -1), (0, 0), (-1, 0)):  # (ip_items 0: a group of rows per wave)
+        # (ip_items 0: a group of rows per wave; ip_iv 0: no pod-interval rows — the other paths run)
+        for ipr, items, iv in ((-1, -1, -1), (-1, -1, 0), (0, -1, 0), (1, -1, 0), (0, 0, 0), (-1, 0, 0)):
             eng = Engine(0)
             eng.set_option("ip_range", ipr)
             eng.set_option("ip_items", items)
+            eng.set_option("ip_iv", iv)
             assert eng.get_option("ip_range") == ipr
             o, g = run_both(pols, res, probes, engine=eng)
-            assert_same(o, g, f"ip intervals seed {seed} ip_range {ipr} ip_items {items}")
+            assert_same(o, g, f"ip intervals seed {seed} ip_range {ipr} ip_items {items} ip_iv {iv}")
             for opts in ({"front_fused": 0}, {"graphs": 0}):
                 for k, v in opts.items():
                     eng.set_option(k, v)
                 o2, g2 = run_both(pols, res, probes, engine=eng)
                 assert_same(o2, g2, f"ip intervals seed {seed} ip_range {ipr} {opts}")
+
+
+def _ip_mono_problem(seed, n_pods=9000):
+    """Addresses handed out in pod order per family (IPv4, v4-mapped sharing the IPv4 counter, IPv6),
+    families interleaved pod by pod, with gaps and repeated addresses; 141 words over 3 chunks.
+    IPBlocks of every prefix length around random pods, with 0-20 nested excepts (more than IPV_MAX
+    intervals falls back to the other IP-row paths), edge networks (0.0.0.0/0, ::/0, ::ffff:0:0/96)."""
+    import ipaddress
+
+    rng = np.random.default_rng(seed)
+    a4, a6 = 0, 0
+    pods, at4, at6 = [], [], []
+    for n in range(n_pods):
+        u = rng.random()
+        step = int(rng.choice([0, 1, 1, 1, 2, 7]))  # 0: the previous pod's address again
+        if u < 0.45 or u >= 0.9:
+            a4 += step
+            v4 = ipaddress.IPv4Address((10 << 24) + a4)
+            ip = str(v4) if u < 0.45 else "::ffff:" + str(v4)
+            at4.append(a4)
+        else:
+            a6 += step
+            ip = str(ipaddress.IPv6Address((0xFD00 << 112) + a6))
+            at6.append(a6)
+        pods.append({"Namespace": "x", "Name": f"p{n}", "Labels": {"i": str(n % 7)}, "IP": ip,
+                     "Containers": [{"Name": "c", "Port": 80, "Protocol": "TCP", "PortName": "serve-80-tcp"}]})
+    res = {"Namespaces": {"x": {"ns": "x"}}, "Pods": pods}
+
+    def net(v6, center, plen):
+        if v6:
+            base = (0xFD00 << 112) + center
+            return str(ipaddress.IPv6Network((base >> (128 - plen) << (128 - plen), plen)))
+        base = (10 << 24) + center
+        return str(ipaddress.IPv4Network((base >> (32 - plen) << (32 - plen), plen)))
+
+    pols = []
+    for k in range(24):
+        peers = []
+        for _ in range(int(rng.integers(1, 4))):
+            v6 = rng.random() < 0.4
+            addrs = at6 if v6 else at4
+            center = int(addrs[int(rng.integers(0, len(addrs)))])
+            bits = 128 if v6 else 32
+            plen = bits - int(rng.integers(0, 15))
+            cidr = net(v6, center, plen)
+            ex = []
+            for _ in range(int(rng.choice([0, 1, 2, 3, 20]))):
+                ec = center + int(rng.integers(-(1 << max(bits - plen - 1, 0)), 1 << max(bits - plen - 1, 0)))
+                ex.append(net(v6, max(ec, 0), min(bits, plen + int(rng.integers(1, 8)))))
+            if rng.random() < 0.1:
+                cidr, ex = str(rng.choice(["0.0.0.0/0", "::/0", "::ffff:0:0/96"])), ex[:2]
+            peers.append({"ipBlock": {"cidr": cidr, "except": ex} if ex else {"cidr": cidr}})
+        spec = {"podSelector": {"matchLabels": {"i": str(k % 7)}}, "policyTypes": ["Ingress", "Egress"],
+                "ingress": [{"from": peers}], "egress": [{"to": peers[::-1]}]}
+        pols.append({"metadata": {"name": f"m{k}", "namespace": "x"}, "spec": spec})
+    return pols, res, [{"AllAvailable": True}]
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_ip_pod_interval_rows(gpu, seed):
+    """IP rows as pod intervals (ip_iv, address-monotone families): whole planes equal the other IP-row
+    paths' (ip_iv 0, pinned to the oracle by the tests above) through the fused front, the DAG and the
+    eager launches, on the whole table and on source and target shards; sampled rows against the oracle."""
+    pols, res, probes = _ip_mono_problem(seed)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    sh = eng.prepare(probes)
+    P, K = sh["pods"], sh["slots"]
+    ref = Engine(0).build_policies(pols).load_resources(res)
+    ref.prepare(probes)
+    ref.set_option("ip_iv", 0)
+    orc = Oracle(pols, res)
+    for part, lo, hi in (("target", 0, P), ("source", 0, 4096), ("source", 4096, P), ("target", 1000, 5000)):
+        want = ref.run_host(lo, hi, part)
+        for opts in ({}, {"front_fused": 0}, {"graphs": 0}, {"graphs": 1}):
+            for k, v in {"front_fused": 1, "graphs": -1, **opts}.items():
+                eng.set_option(k, v)
+            got = eng.run_host(lo, hi, part)
+            assert eng.get_option("ip_iv_rows") > 0
+            for name, a, b in zip(("status", "ingress", "egress"), want, got):
+                assert np.array_equal(a, b), f"seed {seed} {part} [{lo}, {hi}) {opts}: {name} plane differs"
+        if part == "target" and lo == 0:
+            for pod in (0, 63, 64, 4095, 4096, P // 2, P - 1):
+                for k in range(K):
+                    assert np.array_equal(got[1][pod, k], orc.row(probes, "ingress", pod, k)), (seed, pod, k)
+                    assert np.array_equal(got[2][pod, k], orc.row(probes, "egress", pod, k)), (seed, pod, k)
 
 
 def _shared_ipblock_problem(seed, bad=False):
