@@ -197,17 +197,6 @@ struct cyc_ctx {
                         // (enq_front_fused), 0 = the two-branch DAG
   int emit_interleave = -1;  // "emit_interleave": a target-row emit's row list alternates the planes'
                              // rows (1) or is [plane 0][plane 1] (0); -1 = auto (planes >= 8 GB)
-  int emit_footprint = 1;  // "emit_footprint": a target-row emit as F launches, launch h writing only rows
-                           // [h P / F, (h + 1) P / F) of both planes, class-clustered within them (the TLB
-                           // footprint test, VERDICT r5 ask 2); 1 = one launch over the whole planes
-  int emit_split = 1;   // "emit_split": a target-row emit as this many launches over consecutive parts
-                        // of each plane's row list (1..8)
-  int emit_buf = 2;      // "emit_buf": 56-104 KB plane rows through 1024 x 7 buffer-op blocks (2), 512 x 13
-                         // buffer-op blocks (1) or 1024 x 7 flat-address blocks (0).  The emit's rate depends
-                         // on the planes' physical placement; over 14 placements of config #3's planes 1024 x 7
-                         // averaged 3.389 ms per step against 3.542 for 512 x 13 (1-2 % behind on the best
-                         // placements, up to 8 % ahead on the worst; a target shard at N = 8 -5.7 %),
-                         // profiles/r05_plane_placement.txt, r05_shard_ab.txt
   // what the last enqueued emit launched (cyc_last_emit): kernel name(s) and launch count
   std::string emit_kernel;
   int emit_launches = 0;
@@ -254,6 +243,14 @@ struct cyc_ctx {
   std::vector<uint64_t> blk_off_h;          // per block: plane slab offset (words), status offset (bytes); then totals
   std::vector<int> blk_rc;                  // per block status of the last run
   std::vector<std::string> blk_msg;         // and its message
+  // Row phases ("row_phases"): a whole-table run as F consecutive target-row runs, phase k on child
+  // context phase_ctx[k] — prepared like this one, so each keeps its own range plan — each phase's
+  // front and emit back to back.  A phase's class rows (~200 MB for config #3's half) stay in the
+  // 256 MB MALL until its emit re-reads them; the whole table's (~400 MB) do not, and its emit reads
+  // them from HBM between its writes (round 6, profiles/r06_emit_footprint_ab.txt).
+  int row_phases = -1;  // -1 auto (2 for no-panic whole tables of >= 8 GB planes), 1 = off, 2..4
+  cyc_ctx* phase_ctx[4] = {nullptr, nullptr, nullptr, nullptr};
+  int phase_used = 0;   // the last run's phases (0: a plain run)
   // multi-GPU table assembly (comm.hpp): the context's RCCL communicator, a second stream on which
   // gathered chunks are relaid out under the next chunk's all-gather, and the chunks' double buffer
   struct Comm {

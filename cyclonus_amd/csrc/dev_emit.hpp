@@ -40,7 +40,6 @@ struct EmitArgs {
   // (their readers are all done): no fill launch or memset node before the next front
   uint32_t* reset;
   uint64_t reset_n;
-  uint32_t buf;        // 56-104 KB rows through k_emit_wide_buf<512,13> (else k_emit_wide<1024,7>)
 };
 
 // Block blockIdx.x's row r of the n-row list and its XCD x; false when the block has no row.

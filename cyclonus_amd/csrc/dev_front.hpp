@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
   for (int x = 0; x < 2; x++) {
     if (b < f.nb[2 + x]) {
       if (f.pod_direct)
-        return pod_rows_direct_blk<false>(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.selres, f.L, f.pod_eid, f.id_ns, f.id_nsls,
+        return pod_rows_direct_blk<false>(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.sv, f.pod_eid, f.id_ns, f.id_nsls,
                                           f.id_ls, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
       return peer_bits_blk(f.Ru_[x], f.E, f.EW, f.pod_peers_u_[x], f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob_[x], b,
                            f.nb[2 + x], f.ew0[x], f.new_[x], f.grp_ns_[x], f.word_ns);

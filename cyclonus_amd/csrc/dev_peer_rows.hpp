@@ -61,11 +61,21 @@ constexpr uint32_t PR_DIRECT_G = 4;  // pod peers per wave of the direct pod-pee
 __host__ __device__ inline uint64_t pod_direct_waves(uint32_t Rp, uint32_t nw) {
   return uint64_t((Rp + PR_DIRECT_G - 1) / PR_DIRECT_G) * nw;
 }
+// No panic possible (the fused front): both matchers through a SelView — the dense selector table, or
+// selectors evaluated here (one-requirement records: one label-table gather each) when the front builds
+// no table (sel_lazy), so a PM build with full pod-peer rows needs no launch A.
+__device__ __forceinline__ uint32_t pod_peer_match_sv(const DPeer& pr, const SelView& sv, uint32_t ns, uint32_t nsls, uint32_t ls) {
+  const bool nsel = pr.nskind == 2, psel = pr.podsel != CYC_ALL;
+  const uint32_t rn = nsel ? sel_at(sv, pr.nsval, nsls) : 1u;
+  const uint32_t rp = psel ? sel_at(sv, pr.podsel, ls) : 1u;
+  if (pr.nskind == 0) return ns == pr.nsval && rp == 1 ? 1u : 0u;
+  return rn == 1 && rp == 1 ? 1u : 0u;
+}
 template <bool ERR>
 __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uint32_t W,
                                                          const uint32_t* __restrict__ pod_peers,
-                                                         const DPeer* __restrict__ peers, const uint8_t* __restrict__ selres,
-                                                         uint32_t L, const uint32_t* __restrict__ pod_eid,
+                                                         const DPeer* __restrict__ peers, const SelView& sv,
+                                                         const uint32_t* __restrict__ pod_eid,
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                          const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
                                                          uint64_t* __restrict__ ER, uint32_t bid_, uint32_t nblk_, uint32_t w0,
@@ -85,7 +95,8 @@ __device__ __forceinline__ void pod_rows_direct_blk(uint32_t Rp, uint32_t P, uin
   const uint32_t ns = id_ns[e], nsls = id_nsls[e], ls = id_ls[e];
   uint32_t o[PR_DIRECT_G];
 #pragma unroll
-  for (uint32_t u = 0; u < PR_DIRECT_G; u++) o[u] = pod_peer_outcome(pr[u], selres, L, ns, nsls, ls);
+  for (uint32_t u = 0; u < PR_DIRECT_G; u++)
+    o[u] = ERR || sv.selres ? pod_peer_outcome(pr[u], sv.selres, sv.L, ns, nsls, ls) : pod_peer_match_sv(pr[u], sv, ns, nsls, ls);
 #pragma unroll
   for (uint32_t u = 0; u < PR_DIRECT_G; u++) {
     if (p0 + u >= Rp) break;  // wave-uniform
@@ -106,7 +117,10 @@ __global__ __launch_bounds__(256) void k_pod_rows_direct(uint32_t Rp, uint32_t P
                                                          const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                          const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ PM,
                                                          uint64_t* __restrict__ ER, uint32_t w0, uint32_t nw) {
-  pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, selres, L, pod_eid, id_ns, id_nsls, id_ls, PM, ER, blockIdx.x, gridDim.x, w0, nw);
+  SelView sv{};
+  sv.selres = selres;
+  sv.L = L;
+  pod_rows_direct_blk<ERR>(Rp, P, W, pod_peers, peers, sv, pod_eid, id_ns, id_nsls, id_ls, PM, ER, blockIdx.x, gridDim.x, w0, nw);
 }
 
 // Pod-peer rows of the fused front on PM builds (no panic possible), stored sparse, 64-word chunks

@@ -309,16 +309,13 @@ static const char* enq_emit_launch(const EmitArgs& ea_in, hipStream_t st, uint64
     return "k_emit_words";
   }
   const uint64_t row_bytes = ea.row_words * 8;
-  // A 512 x 13 one-pass block with flat addresses held 84 VGPRs, 5 waves a SIMD, and ran config #3
-  // 3.5 % slower per step (profiles/r03_emit_ab.txt); through buffer ops it holds 54 (8 waves a
-  // SIMD) and beats flat 1024 x 7 on a good plane placement: config #3 emit 3000 vs 3058-3070 us
-  // (profiles/r04_emit_buf_ab.txt) — but over many placements 1024 x 7 through buffer ops wins on
-  // average (cyc_ctx::emit_buf).
+  // 56-112 KB rows (config #3's 98 KB): 1024 x 7 blocks through buffer ops, one pass.  A 512 x 13
+  // one-pass block held 84 VGPRs with flat addresses (config #3 3.5 % slower, profiles/r03_emit_ab.txt)
+  // and 54 through buffer ops, 1-2 % ahead of 1024 x 7 on the best plane placements but up to 20 %
+  // behind on others: over 14 placements 3.542 vs 3.389 ms per step (profiles/r05_plane_placement.txt;
+  // the flat-address 1024 x 7 form trailed both) — only 1024 x 7 through buffer ops is kept.
   // (128 x 13 buffer blocks for config #4's 25 KB rows lost: 442-447 vs 419-424 us.)
-  if (row_bytes > 512 * 7 * 16 && row_bytes <= 512 * 13 * 16 && ea.buf == 1) {  // 56-104 KB: config #3's 98 KB rows, one pass
-    k_emit_wide_buf<512, 13><<<g, 512, 0, st>>>(ea);
-    return "k_emit_wide_buf<512,13>";
-  } else if (row_bytes > 512 * 7 * 16 && row_bytes <= 1024 * 7 * 16 && ea.buf == 2) {
+  if (row_bytes > 512 * 7 * 16 && row_bytes <= 1024 * 7 * 16) {
     k_emit_wide_buf<1024, 7><<<g, 1024, 0, st>>>(ea);
     return "k_emit_wide_buf<1024,7>";
   } else if (row_bytes > 512 * 7 * 16) {  // > 104 KB: 1024 x 7 passes
@@ -394,7 +391,6 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
   ea.reset = c->ip_rng.as<uint32_t>();
   ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
-  ea.buf = uint32_t(c->emit_buf);
   c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
     ea.row_lo[pl] = uint32_t(c->rl[pl]);
@@ -418,23 +414,8 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
     // and 8 shards — profiles/r01_emit_interleave_sweep.txt)
     ea.interleave = c->emit_interleave >= 0 ? uint32_t(c->emit_interleave)
                                             : uint64_t(nr[0]) * rw[0] * 8 >= (8ull << 30) ? 1u : 0u;
-    // emit_split > 1: consecutive parts of both planes' row lists (class-clustered, so nearly address
-    // order) as separate launches, the first carrying the status copy and the span reset
-    // emit_footprint F > 1: launch h over the rows the plan put in address part h (rows i of the run
-    // with i F / n == h: the first ceil(h n / F) rows lie in the parts before h)
-    const bool fp = c->emit_footprint > 1;
-    const uint32_t parts = uint32_t(std::max(1, std::min<int>(fp ? c->emit_footprint : c->emit_split,
-                                                              int(std::max<uint32_t>(nr[0], 1)))));
-    for (uint32_t h = 0; h < parts; h++) {
-      const uint32_t r0 = fp ? uint32_t((uint64_t(nr[0]) * h + parts - 1) / parts) : uint32_t(uint64_t(nr[0]) * h / parts);
-      const uint32_t r1 = fp ? uint32_t((uint64_t(nr[0]) * (h + 1) + parts - 1) / parts)
-                             : uint32_t(uint64_t(nr[0]) * (h + 1) / parts);
-      EmitArgs e1 = ea;
-      e1.n_rows[0] = e1.n_rows[1] = r1 - r0;
-      for (int pl = 0; pl < 2; pl++) e1.order[pl] = ea.order[pl] + r0;
-      if (h) e1.st_bytes = e1.reset_n = 0;
-      note(enq_emit_launch(e1, st, out_in, out_eg));
-    }
+    ea.n_rows[0] = ea.n_rows[1] = nr[0];
+    note(enq_emit_launch(ea, st, out_in, out_eg));
     return true;
   }
   // rows of different lengths (a source shard): ONE launch over units of about one block pass each
@@ -906,6 +887,85 @@ static int blocks_status(cyc_ctx* c, hipStream_t st) {
 // allow_capture = false: never capture a graph for this run (cyc_table_run's planes are new on
 // every call, so a captured graph would be re-instantiated each time): graphs = 1 runs as 2.
 // src: rows [lo, hi) are a source shard (CYC_ROWS_SOURCE), else target rows.
+// ---- row phases (cyc_ctx::row_phases): the children a whole-table run is split over
+static void copy_options(cyc_ctx* k, const cyc_ctx* c) {
+  k->use_graphs = c->use_graphs;
+  k->ip_iv = c->ip_iv;
+  k->ip_range = c->ip_range;
+  k->pod_rows = c->pod_rows;
+  k->member_wave = c->member_wave;
+  k->pod_words = c->pod_words;
+  k->class_rpb_opt = c->class_rpb_opt;
+  k->step_events = c->step_events;
+  k->pl_wave = c->pl_wave;
+  k->class_inplace = c->class_inplace;
+  k->pr_group = c->pr_group;
+  k->sel_lazy = c->sel_lazy;
+  k->front_fused = c->front_fused;
+  k->emit_interleave = c->emit_interleave;
+  k->ip_items_opt = c->ip_items_opt;
+  k->plvt_max_mb = c->plvt_max_mb;
+  k->row_phases = 1;  // (a child never splits again)
+}
+static void drop_phases(cyc_ctx* c) {
+  for (auto& k : c->phase_ctx)
+    if (k) {
+      cyc_ctx_destroy(k);
+      k = nullptr;
+    }
+  c->phase_used = 0;
+}
+// Phases of a run: a whole table (every target row, or a source run over every pod — the same planes)
+// of a no-panic, unbatched build; auto = 2 once each plane is >= 8 GB (config #3).
+static int phases_of(const cyc_ctx* c, int64_t lo, int64_t hi) {
+  const Problem& pb = c->pb;
+  if (c->row_phases == 1 || pb.may_err || !pb.blocks.empty() || lo != 0 || hi != int64_t(pb.P) || pb.P < 128) return 1;
+  if (c->row_phases > 1) return c->row_phases;
+  return uint64_t(pb.P) * pb.K * pb.W * 8 >= (8ull << 30) ? 2 : 1;
+}
+static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
+                        int64_t hi, bool allow_capture, bool src);
+static int run_phases(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int F,
+                      bool allow_capture) {
+  const Problem& pb = c->pb;
+  for (int k = 0; k < F; k++) {
+    if (c->phase_ctx[k]) continue;  // made once per prepare: the inputs, tables and options of this context
+    cyc_ctx* ch = nullptr;
+    HIPCHK(hipGetLastError());
+    if (cyc_ctx_create(c->device, &ch) != CYC_OK || !ch->stream) throw HipErr{"row phases: child context"};
+    c->phase_ctx[k] = ch;
+    ch->policy = c->policy;
+    ch->res = c->res;
+    ch->have_policy = ch->have_res = true;
+    ch->pb = c->pb;
+    copy_options(ch, c);
+    build_identities(ch);
+    prepare_device(ch);
+    ch->prepared = true;
+  }
+  const uint64_t row = uint64_t(pb.K) * pb.W;
+  const bool ev = c->use_graphs == 0 || c->step_events;
+  if (ev) HIPCHK(hipEventRecord(c->ev[0], st));
+  c->emit_kernel.clear();
+  c->emit_launches = 0;
+  for (int k = 0; k < F; k++) {
+    const int64_t a = int64_t(pb.P) * k / F, b = int64_t(pb.P) * (k + 1) / F;
+    cyc_ctx* ch = c->phase_ctx[k];
+    const int rc = run_pipeline(ch, st, d_in + uint64_t(a) * row, d_eg + uint64_t(a) * row, d_status, a, b, allow_capture, false);
+    if (rc != CYC_OK) return fail(c, rc, ch->err);
+    if (c->emit_kernel.find(ch->emit_kernel) == std::string::npos)
+      c->emit_kernel += (c->emit_kernel.empty() ? "" : " + ") + ch->emit_kernel;
+    c->emit_launches += ch->emit_launches;
+  }
+  if (ev) HIPCHK(hipEventRecord(c->ev[3], st));
+  c->timed = ev;
+  c->timed_graph = false;
+  c->ran = true;
+  c->last_stream = st;
+  c->phase_used = F;
+  return (int)CYC_OK;
+}
+
 static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
                         int64_t hi, bool allow_capture = true, bool src = false) {
   Problem& pb = c->pb;
@@ -913,6 +973,9 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
   if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
   if (src && (lo % 64 || (hi % 64 && hi != int64_t(P))))
     return fail(c, CYC_ERR_ARG, "source rows: row_lo must be a multiple of 64, row_hi too unless it is the pod count");
+  // a source run over every pod writes the target-row planes: it splits like a whole table
+  if (const int F = phases_of(c, lo, hi); F > 1 && d_in && d_eg) return run_phases(c, st, d_in, d_eg, d_status, F, allow_capture);
+  c->phase_used = 0;
   if (c->order_lo != lo || c->order_hi != hi || c->order_src != src) drop_graph(c);  // range plan buffers are re-made
   ensure_range(c, lo, hi, src);
   if (!c->plvt_ready && front_fused_ok(c) && pod_sparse(c)) {

@@ -513,8 +513,6 @@ static void ensure_plvt(cyc_ctx* c, hipStream_t st) {
 static bool lazy_sel(const cyc_ctx* c) {
   if (!c->dense_sel || c->pb.may_err || c->sel_lazy == 0 || !front_fused_ok(c)) return false;
   const bool pod_peers = c->rp_off[2] > c->rp_off[0];
-  // the full pod-peer rows read the dense selector table
-  if (!ido_mode(c) && !pod_sparse(c) && pod_peers) return false;
   // no pod-peer rows at all (IPBlock-only policies, config #4): the membership is the only selector
   // user, one record and one label-table load per target — no table, and no launch A
   if (!pod_peers && c->sel_lazy < 0) return true;
@@ -635,13 +633,8 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
     std::iota(ord.begin(), ord.end(), uint32_t(c->rl[d]));
     const auto& i1 = c->ids[d].of_pod;
     const auto& i2 = c->ids[1 - d].of_pod;
-    // emit_footprint F > 1 (target rows): the list is F address parts of the rows, each clustered
-    const uint64_t F = src ? 1u : uint64_t(c->emit_footprint), nrow = std::max<uint64_t>(ord.size(), 1);
-    auto part = [&](uint32_t x) { return (uint64_t(x) - uint64_t(c->rl[d])) * F / nrow; };
-    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
-      if (part(x) != part(y)) return part(x) < part(y);
-      return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y];
-    });
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](uint32_t x, uint32_t y) { return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y]; });
     std::vector<uint32_t> pairs(ord.size() * 2);
     for (size_t r = 0; r < ord.size(); r++) {
       pairs[2 * r] = ord[r];

@@ -400,20 +400,17 @@ int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
  *                 them to the class's other pods (1), or they go to a buffer of their own the emit
  *                 copies from (0); auto = 1 when the rows' identities are >= 1/16 of the rows or
  *                 the run is an identity-set build
- *   "emit_buf"    2 (default) / 1 / 0: plane rows of 56-104 KB emitted by 1024 x 7 blocks through buffer
- *                 loads / stores, 512 x 13 buffer blocks, or 1024 x 7 flat-address blocks
- *                 ("class_inplace_active" reports the choice of the last run's row range)
  *   "sel_lazy"    -1 (default: auto) / 0 / 1: on the fused front, label selectors are evaluated where
  *                 membership and pod-peer rows / identity sets use them (1) instead of as the dense
  *                 selector x label-set table first (0); auto = 1 for identity-set builds and once
  *                 that table has >= 64M pairs
+ *   "ip_iv"       -1 (default: auto) / 0: IP rows as pod-index intervals where the network's family holds
+ *                 non-decreasing addresses in pod order (ip_rows_iv_blk), or through the paths below
  *   "ip_items"    -1 (default: auto = 1 for runs over every row) / 0 / 1: the fused front's IP rows as
  *                 per-chunk work items of the rows that touch each chunk (1) or as groups of 16 rows a
  *                 wave over 4 chunks (0)
  *   "emit_interleave" -1 (default: auto = 1 when a plane of a target-row run is >= 8 GB) / 0 / 1: the
  *                 emit's row list alternates ingress and egress rows (1) or holds all ingress rows first
- *   "emit_split"  1 (default) .. 8: a target-row run's emit as that many launches over consecutive
- *                 parts of the planes' row lists
  * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
  * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
  * uses (0 or 1). */

@@ -6,14 +6,12 @@
 The engine is prepared through bench.py's flat path (flat.prepare_flat).  Variants:
   whole      one cyc_probe_run over all target rows (the bench step; emit_interleave auto = 1)
   whole_il0  the same with the row list [ingress rows][egress rows] (emit_interleave = 0)
-  split2     one front, the emit as two launches over the two halves of the row lists (emit_split = 2)
-  split2_il0 split2 with emit_interleave = 0
-  split4     four emit launches
   halves     two cyc_probe_run calls, target rows [0, P/2) then [P/2, P), into the two halves of the
              same 2 x 10 GB planes (the whole pass's footprint)
   halves_il1 halves with the planes' rows alternating (emit_interleave = 1)
   half_same  the first half twice into the first half of the planes (10 GB footprint: what
              scripts/partition_scaling.py times for N = 2)
+  first / second  one half run alone into its own half of the planes
 Reported per variant: back-to-back ms per step (the bench clock; min over reps) and the emit's
 HIP-event time per step from eager runs (graphs = 0: the emit launches of the step summed).
 """
@@ -50,24 +48,18 @@ B_IN, B_EG = d_in.data_ptr(), d_eg.data_ptr()
 VARIANTS = {
     "whole": ({}, [(0, P, 0)]),
     "whole_il0": ({"emit_interleave": 0}, [(0, P, 0)]),
-    "split2": ({"emit_split": 2}, [(0, P, 0)]),
-    "split2_il0": ({"emit_split": 2, "emit_interleave": 0}, [(0, P, 0)]),
-    "split4": ({"emit_split": 4}, [(0, P, 0)]),
     "halves": ({}, [(0, H, 0), (H, P, H)]),
     "halves_il1": ({"emit_interleave": 1}, [(0, H, 0), (H, P, H)]),
     "half_same": ({}, [(0, H, 0), (0, H, 0)]),
-    # VERDICT r5 ask 2 (the footprint hypothesis): one front, the emit as two launches over the address
-    # halves of both planes (rows [0, P/2), then [P/2, P)), each class-clustered within its half; and
-    # each half run alone into its own half of the same planes
-    "fp2": ({"emit_footprint": 2}, [(0, P, 0)]),
-    "fp4": ({"emit_footprint": 4}, [(0, P, 0)]),
+    # each half run alone into its own half of the same planes (VERDICT r5 ask 2; round 6 also timed the
+    # emit as launches over the address halves — option emit_footprint, removed: profiles/r06_emit_footprint_ab.txt)
     "first": ({}, [(0, H, 0)]),
     "second": ({}, [(H, P, H)]),
 }
 
 
 def spec(name):
-    """A variant, optionally with options: "whole:emit_split=2,emit_interleave=0"."""
+    """A variant, optionally with options: "whole:emit_interleave=0,class_inplace=0"."""
     base, _, extra = name.partition(":")
     opts = dict(VARIANTS[base][0])
     for kv in filter(None, extra.split(",")):
@@ -77,7 +69,7 @@ def spec(name):
 
 
 def setv(name):
-    for k, v in (("emit_interleave", -1), ("emit_split", 1), ("emit_footprint", 1)):
+    for k, v in (("emit_interleave", -1), ("class_inplace", -1)):
         eng.set_option(k, v)
     for k, v in spec(name)[0].items():
         eng.set_option(k, v)

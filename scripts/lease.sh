@@ -17,6 +17,7 @@
 #                              CYC_BENCH_BACKEND=gloo for a one-GPU rehearsal, CYC_BENCH_FORCE_DIST=1)
 #   ab CFG SPEC...             kernel stats per library variant (scripts/ab_kernels.sh; REPS env, CYC_SHARD tokens)
 #   pmcab VARIANT...           emit PMC passes per scripts/emit_halves_ab.py variant (scripts/pmc_emit_ab.sh)
+#   emitks VARIANT:LAUNCHES... per-launch emit durations of emit_halves_ab.py variants (scripts/emit_launches.py)
 #   pmc CFG [NAME=V ...]       per-kernel SQ instruction / wait mix, TCC hits, FETCH / WRITE passes (scripts/pmc_passes.sh)
 # Invocations are recorded in scripts/LEASES.md.
 set -e
@@ -39,7 +40,7 @@ for spec in "$@"; do
   case $step in
     tests)  # (K=a+or+b: pytest -k "a or b" — a step's words cannot hold spaces)
       targs=(); for a in "$@"; do if [[ $a == K=* ]]; then targs+=(-k "$(echo "${a#K=}" | tr '+' ' ')"); else targs+=("$a"); fi; done
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${targs[@]}" > $OUT/gpu_tests.log 2>&1 ;;
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --durations=40 --timeout 300 --timeout-method thread "${targs[@]}" > $OUT/gpu_tests.log 2>&1 ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 ;;
     bench) timeout -k 10 300 python -u bench.py --config "$@" > $OUT/bench_$tag.log 2>&1 ;;
     prof)
@@ -68,6 +69,11 @@ for spec in "$@"; do
     ab) timeout -k 10 900 bash scripts/ab_kernels.sh $NAME "$@" ;;
     pmc) timeout -k 10 700 bash scripts/pmc_passes.sh $NAME "$@" ;;
     pmcab) timeout -k 10 900 bash scripts/pmc_emit_ab.sh $NAME "$@" ;;
+    emitks)  # per-launch emit durations of emit_halves_ab.py variants (VARIANT:LAUNCHES ...), kernel trace
+      prof_env
+      vs=(); for a in "$@"; do vs+=("${a%%:*}"); done
+      timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/emitks -o run -- python3 scripts/emit_halves_ab.py run "${vs[@]}" n=10 > $OUT/emitks.log 2>&1
+      python3 scripts/emit_launches.py $OUT/emitks/run_results.db "$@" n=10 > $OUT/emitks_summary.txt 2>&1 ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
   for e in "${envs[@]}"; do unset "${e%%=*}"; done

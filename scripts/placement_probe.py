@@ -4,7 +4,7 @@ caching allocator: one hipMalloc each), then whole-table steps timed round-robin
 torch fill_ of each pair — same library, same process, same front: only the planes' placement differs.
 
     python scripts/placement_probe.py [pairs=4] [steps=20] [reps=3] [NAME=VALUE ...]   (cyc_set_option)
-    python scripts/placement_probe.py pairs=4 "alt=class_inplace:0,emit_buf:1;emit_buf:0"   (each pair also
+    python scripts/placement_probe.py pairs=4 "alt=class_inplace:0;emit_interleave:0"   (each pair also
                                                                    with each option set)
     python scripts/placement_probe.py pairs=2 hip=2 contig=2     (+ pairs from hipExtMallocWithFlags: flags 0 /
                                                                    hipDeviceMallocContiguous)

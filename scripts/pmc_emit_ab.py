@@ -13,8 +13,7 @@ import sys
 out, variants = sys.argv[1], sys.argv[2:]
 N = 3
 # emit launches per step: the runs a step makes x the launches a run's emit makes
-PER_STEP = {"whole": 1, "whole_il0": 1, "split2": 2, "split2_il0": 2, "split4": 4, "halves": 2, "halves_il1": 2, "half_same": 2,
-            "fp2": 2, "fp4": 4, "first": 1, "second": 1}
+PER_STEP = {"whole": 1, "whole_il0": 1, "halves": 2, "halves_il1": 2, "half_same": 2, "first": 1, "second": 1}
 per = collections.defaultdict(lambda: collections.defaultdict(float))
 for path in sorted(glob.glob(os.path.join(out, "pmcab_*", "**", "*counter_collection.csv"), recursive=True)):
     rows = [r for r in csv.DictReader(open(path)) if "k_emit" in r["Kernel_Name"]]

@@ -475,6 +475,40 @@ def test_ip_pod_interval_rows(gpu, seed):
                     assert np.array_equal(got[2][pod, k], orc.row(probes, "egress", pod, k)), (seed, pod, k)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_row_phases(gpu, seed):
+    """A whole table run as 2-4 row phases (each phase's front and emit on a child context prepared
+    like the caller's) equals the single run, through every launch mode, on target and whole-range
+    source runs; the reported emit launches and classes add up over the phases."""
+    pols, res, probes = random_problem(91_000 + seed, n_pods=300 + 97 * seed, n_pols=10)
+    eng = Engine(0).build_policies(pols).load_resources(res)
+    eng.prepare(probes)
+    if eng.shape["may_panic"]:
+        pytest.skip("a build that may panic never splits")
+    want = eng.run_host()
+    assert eng.get_option("row_phases_active") == 0  # (auto: 2 only from 8 GB planes up)
+    for F in (2, 3, 4):
+        eng.set_option("row_phases", F)
+        for graphs in (-1, 1, 0):
+            eng.set_option("graphs", graphs)
+            for part in ("target", "source"):
+                got = eng.run_host(0, None, part)
+                assert eng.get_option("row_phases_active") == F
+                assert eng.last_emit()[1] == F, eng.last_emit()
+                for name, a, b in zip(("status", "ingress", "egress"), want, got):
+                    assert np.array_equal(a, b), f"seed {seed} row_phases {F} graphs {graphs} {part}: {name} differs"
+        assert sum(eng.classes()) > 0
+        eng.set_option("graphs", 0)
+        eng.run_host()
+        t = eng.timings()
+        assert t[0] > 0 and t[1] > 0 and t[2] >= 0, t
+    eng.set_option("row_phases", 1)
+    eng.run_host(0, 100)  # a row range never splits
+    assert eng.get_option("row_phases_active") == 0
+    with pytest.raises(Exception):
+        eng.set_option("row_phases", 0)
+
+
 def _shared_ipblock_problem(seed, bad=False):
     """Policies whose peers reuse a small pool of IPBlocks (equal cidr / except strings) on different
     ports and in both directions: the run plan builds ONE IP row per IPBlock and direction, and every
@@ -801,14 +835,12 @@ def test_launch_modes_and_knobs(gpu):
     for name, v in (("front_fused", 0), ("front_fused", 1), ("class_rpb", 7), ("class_rpb", 16), ("class_rpb", 0), ("graphs", 1), ("graphs", -1),
                     ("step_events", 1), ("step_events", 0), ("pr_group", 5), ("pr_group", -1), ("sel_lazy", 1),
                     ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1),
-                    ("emit_interleave", 1), ("emit_split", 3), ("emit_interleave", 0), ("emit_split", 2),
-                    ("emit_interleave", -1), ("emit_split", 1),
-                    ("ip_items", 0), ("ip_items", 1), ("ip_items", -1), ("emit_buf", 0), ("emit_buf", 1), ("emit_buf", 2)):
+                    ("emit_interleave", 1), ("emit_interleave", 0), ("emit_interleave", -1),
+                    ("ip_items", 0), ("ip_items", 1), ("ip_items", -1), ("ip_iv", 0), ("ip_iv", -1)):
         eng.set_option(name, v)
         assert eng.get_option(name) == v
         assert_same(want, eng.run_host(), f"{name}={v}")
-        if name == "emit_split":  # cyc_last_emit reports the launches the run made
-            assert eng.last_emit()[1] == v, eng.last_emit()
+        assert eng.last_emit()[1] == 1, eng.last_emit()  # cyc_last_emit: one emit launch a run
     # whole-step timing events: off by default for graph / fused-eager runs, always for eager runs
     with pytest.raises(Exception):
         eng.timings()
@@ -826,7 +858,8 @@ def test_launch_modes_and_knobs(gpu):
     eng.set_option("front_fused", 1)
     assert_same(want, eng.run_host(), "fused again")
     for name, v in (("class_rpb", -1), ("class_rpb", 65), ("ip_range", 2), ("ip_group", 8), ("graphs", 3), ("pr_group", 65), ("sel_lazy", 2), ("emit_variant", 1),
-                    ("emit_split", 0), ("emit_split", 9), ("emit_interleave", 2), ("emit_prefetch", 1), ("emit_sweep", 16), ("ip_items", 2), ("emit_buf", 3),
+                    ("emit_split", 2), ("emit_interleave", 2), ("emit_prefetch", 1), ("emit_sweep", 16), ("ip_items", 2), ("emit_buf", 1),
+                    ("ip_iv", 2), ("emit_footprint", 2), ("emit_rows", 1),
                     ("nope", 0)):
         with pytest.raises(Exception):
             eng.set_option(name, v)
