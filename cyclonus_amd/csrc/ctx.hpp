@@ -243,14 +243,19 @@ struct cyc_ctx {
   std::vector<uint64_t> blk_off_h;          // per block: plane slab offset (words), status offset (bytes); then totals
   std::vector<int> blk_rc;                  // per block status of the last run
   std::vector<std::string> blk_msg;         // and its message
-  // Row phases ("row_phases"): a whole-table run as F consecutive target-row runs, phase k on child
-  // context phase_ctx[k] — prepared like this one, so each keeps its own range plan — each phase's
-  // front and emit back to back.  A phase's class rows (~200 MB for config #3's half) stay in the
-  // 256 MB MALL until its emit re-reads them; the whole table's (~400 MB) do not, and its emit reads
-  // them from HBM between its writes (round 6, profiles/r06_emit_footprint_ab.txt).
-  int row_phases = -1;  // -1 auto (2 for no-panic whole tables of >= 8 GB planes), 1 = off, 2..4
-  cyc_ctx* phase_ctx[4] = {nullptr, nullptr, nullptr, nullptr};
-  int phase_used = 0;   // the last run's phases (0: a plain run)
+  // Row phases ("row_phases"): a whole-table run's class rows and emit in two phases — the class rows
+  // of the classes rows [0, P/2) use, the emit of those rows, then the other classes' rows and the emit
+  // of rows [P/2, P) — so a phase's class rows (~200 MB for config #3) are still in the 256 MB MALL when
+  // its emit re-reads them; the whole table's (~400 MB) are not, and its emit reads them from HBM
+  // between its writes (round 6, profiles/r06_emit_footprint_ab.txt).  The front before the class rows
+  // runs once.
+  int row_phases = -1;     // -1 auto (whole no-panic tables of >= 8 GB planes), 1 = off, 2 = whenever possible
+  uint32_t phase_split = 0;   // the range plan's split row (0: no phases): emit lists are [rows < split][rows >= split]
+  uint32_t phase_n1[2] = {0, 0};  // per plane: rows before the split in its emit list
+  int phase_used = 0;      // the last run's phases (2, or 0 for a plain run)
+  DevBuf need[2];          // per identity: the run epoch whose phase-1 rows use the class it represents
+  uint32_t run_epoch = 0;
+  hipEvent_t ev_p[2] = {nullptr, nullptr};  // eager runs: around phase 2's class rows (cyc_last_timings)
   // multi-GPU table assembly (comm.hpp): the context's RCCL communicator, a second stream on which
   // gathered chunks are relaid out under the next chunk's all-gather, and the chunks' double buffer
   struct Comm {

@@ -65,7 +65,14 @@ struct RowArgs {
   // kernel in block slices once k_classify is done with it: no memset node precedes k_member
   uint32_t* ht_clear;
   uint64_t ht_clear_words;
+  // row phases: phase 1 computes the classes with need == epoch, phase 2 the others; 0 = every class
+  const uint32_t* need;
+  uint32_t epoch, phase;
 };
+// This launch computes representative i's class rows (row phases, RowArgs::phase).
+__device__ __forceinline__ bool in_phase(const RowArgs& a, uint32_t i) {
+  return !a.phase || ((a.need[i] == a.epoch) == (a.phase == 1));
+}
 
 // Row of A holding representative i's class rows: its identity slot, or (in-place class rows) the
 // plane row of the first pod of identity i in the run's rows — that pod's plane row IS the class
@@ -840,6 +847,7 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
   const bool kbits = EGRESS ? a.portbits != nullptr : a.K <= 32;
   for (uint32_t r = bid_; r < n_reps; r += nblk_) {
     const uint32_t i = a.reps[r];
+    if (!in_phase(a, i)) continue;  // (block-uniform)
     const uint32_t nt = a.cnt[i];
     const uint32_t* lst = a.list + a.list_off[i];
     uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
@@ -1047,7 +1055,8 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   const uint32_t kc = (bid_ / cg) % nkc;
   const uint32_t r0 = (bid_ / (cg * nkc)) * a.rpb, n_reps = *a.rep_cnt + 1u;
   if (r0 >= n_reps) return;  // whole block
-  const uint32_t nr = min(a.rpb, n_reps - r0), k0 = kc * KC;
+  uint32_t nr = min(a.rpb, n_reps - r0);
+  const uint32_t k0 = kc * KC;
   const uint32_t nrow = EGRESS && !UNI ? a.NB : min(uint32_t(KC), a.K - k0);
   // staged layout: 32-bit word j of row r of representative q at sB32[(q * EW32 + j) * NS + r]
   const uint32_t NS = EGRESS && !UNI ? a.NB : uint32_t(KC), EW32 = 2 * a.EW;
@@ -1064,7 +1073,19 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   // barrier, its identity sets (B) and its first IDO_IPL IP peers with their port bits.  The row
   // loop then reads them from LDS instead of walking reps -> identity -> list chains.
   __shared__ RepHead<KC> s_rep[IDO_RPB_MAX];
-  if (threadIdx.x < nr) {
+  __shared__ uint32_t s_nr;
+  // row phases: only this launch's phase's representatives, compacted (the block's reps lie in wave 0)
+  uint32_t slot = threadIdx.x;
+  if (a.phase) {
+    const bool keep = threadIdx.x < nr && in_phase(a, a.reps[r0 + min(threadIdx.x, nr - 1)]);
+    const uint64_t kb = __ballot(keep);
+    slot = keep ? uint32_t(__popcll(kb & ((1ull << (threadIdx.x & 63)) - 1))) : IDO_RPB_MAX;
+    if (threadIdx.x == 0) s_nr = uint32_t(__popcll(kb));
+    __syncthreads();
+    nr = s_nr;
+    if (!nr) return;  // (block-uniform: no barrier follows for this block)
+  }
+  if (threadIdx.x < min(a.rpb, n_reps - r0) && slot < IDO_RPB_MAX) {
     RepHead<KC> h;
     h.i = a.reps[r0 + threadIdx.x];
     h.arow = uint32_t(arow_of(a, h.i));
@@ -1081,7 +1102,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     h.m = cn ? ipc : 0u;
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) h.du[kk] = !EGRESS && k0 + kk < a.K && st[kk] == CYC_JOB_VALID ? ds[kk] : -2;
-    s_rep[threadIdx.x] = h;
+    s_rep[slot] = h;
   }
   int32_t ud[KC];  // egress UNI: the block's slots' descriptors (block-uniform)
 #pragma unroll

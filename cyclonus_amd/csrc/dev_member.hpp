@@ -29,6 +29,11 @@ struct MemberArgs {
   uint32_t* reps;             // class representatives, act[] order within each block (k_classify)
   uint32_t* rep_cnt;          // set to ~0 by k_member: ends at count - 1
   const uint32_t* id_blk;     // batched blocks: each identity's block (classes never span blocks), else null
+  // row phases (cyc_ctx::row_phases): a class some identity of which has its first row of the run
+  // before `split` is a phase-1 class: need[its representative] = epoch (null: no phases)
+  uint32_t* need;
+  const uint32_t* first_row;  // per identity: its first pod's row in the run (cyc_ctx::arow)
+  uint32_t split, epoch;
 };
 
 // Entry s: words 2s (key) and 2s + 1 (low half: representative); a probe reads both in one load.
@@ -218,6 +223,9 @@ __device__ __forceinline__ void classify_blk(MemberArgs a, uint32_t* __restrict_
                                               a.id_status, a.id_desc, a.K)
                           : i;
   if (live) class_of[i] = c;
+  // (atomicMax: a stale epoch of an earlier run is only ever smaller — or, replayed by a captured graph,
+  // equal, which merely moves a class into phase 1: its row is then ready early, never late)
+  if (live && a.need && a.first_row[i] < a.split) atomicMax(a.need + c, a.epoch);
   const bool f = live && c == i;
   const uint64_t m = __ballot(f);
   if (lane == 0) wsum[wv] = __popcll(m);

@@ -109,8 +109,11 @@ int cyc_ctx_create(int device_id, cyc_ctx** out) {
     bool ok = hipGetDevice(&cur) == hipSuccess && cur == device_id;
     ok = ok && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
     for (auto& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, EV_TIMING) == hipSuccess;
+    for (auto& e : c->ev_p) ok = ok && hipEventCreateWithFlags(&e, EV_TIMING) == hipSuccess;
     if (!ok) {  // (left to the first prepare, which reports the error)
       for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+      for (auto& e : c->ev_p)
         if (e) (void)hipEventDestroy(e), e = nullptr;
       if (c->stream) (void)hipStreamDestroy(c->stream), c->stream = nullptr;
     }
@@ -135,7 +138,6 @@ void cyc_ctx_destroy(cyc_ctx* c) {
     if (c->ports_ev) (void)hipEventDestroy(c->ports_ev);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
-    drop_phases(c);
     comm_release(c);
     (void)hipStreamDestroy(c->stream);
   }
@@ -234,11 +236,11 @@ static int probe_prepare(cyc_ctx* c, const std::function<std::vector<ProbeConfig
     if (!c->stream) {
       HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       for (auto& e : c->ev) HIPCHK(hipEventCreateWithFlags(&e, EV_TIMING));
+      for (auto& e : c->ev_p) HIPCHK(hipEventCreateWithFlags(&e, EV_TIMING));
     }
     clk.lap("stream");
     const std::vector<ProbeConfig> probes = probes_of();
     c->prepared = false;
-    drop_phases(c);  // (children prepared from the previous inputs)
     clk.lap("probe configs");
     c->pb = build_problem(c->policy, c->res, probes, blocks);
     clk.lap("build_problem");
@@ -568,22 +570,6 @@ void cyc_table_destroy(cyc_table* t) {
 int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
   if (!c || !ms) return CYC_ERR_ARG;
   if (!c->timed) return fail(c, CYC_ERR_ARG, c->ran ? "the last run recorded no timing events (step_events = 0)" : "no run yet");
-  if (c->phase_used) {  // row phases: the whole run's span; emit and class rows summed over the phases
-    return guarded(c, [&]() -> int {
-      DeviceGuard dg(c->device);
-      HIPCHK(hipEventSynchronize(c->ev[3]));
-      float a = 0;
-      HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[3]));
-      double v[3] = {a, 0, 0};
-      for (int k = 0; k < c->phase_used; k++) {
-        double t[3] = {-1, -1, -1};
-        if (cyc_last_timings(c->phase_ctx[k], t, 3) != CYC_OK || t[1] < 0) v[1] = v[2] = -1;
-        else if (v[1] >= 0) v[1] += t[1], v[2] += t[2];
-      }
-      for (int i = 0; i < n && i < 3; i++) ms[i] = v[i];
-      return (int)CYC_OK;
-    });
-  }
   return guarded(c, [&] {
     DeviceGuard dg(c->device);
     HIPCHK(hipEventSynchronize(c->ev[3]));
@@ -592,6 +578,12 @@ int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
     if (!c->timed_graph) {
       HIPCHK(hipEventElapsedTime(&b, c->ev[2], c->ev[3]));
       HIPCHK(hipEventElapsedTime(&r, c->ev[1], c->ev[2]));
+      if (c->phase_used) {  // row phases: phase 2's class rows ran between the emits (ev_p)
+        float p2 = 0;
+        HIPCHK(hipEventElapsedTime(&p2, c->ev_p[0], c->ev_p[1]));
+        b -= p2;
+        r += p2;
+      }
     }
     double v[3] = {a, c->timed_graph ? -1.0 : b, c->timed_graph ? -1.0 : r};
     for (int i = 0; i < n && i < 3; i++) ms[i] = v[i];
@@ -602,17 +594,6 @@ int cyc_last_timings(cyc_ctx* c, double* ms, int n) {
 int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
   if (!c || !out || n < 2) return CYC_ERR_ARG;
   if (!c->ran) return fail(c, CYC_ERR_ARG, "no run yet");
-  if (c->phase_used) {  // row phases: the class rows every phase computed
-    out[0] = out[1] = 0;
-    for (int k = 0; k < c->phase_used; k++) {
-      int64_t v[2];
-      const int rc = cyc_last_classes(c->phase_ctx[k], v, 2);
-      if (rc != CYC_OK) return fail(c, rc, c->phase_ctx[k]->err);
-      out[0] += v[0];
-      out[1] += v[1];
-    }
-    return (int)CYC_OK;
-  }
   return guarded(c, [&]() -> int {
     DeviceGuard dg(c->device);
     // the last run's stream, not an event recorded after every run: an event at each step's end held
@@ -672,8 +653,9 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     else if (n == "emit_interleave") range(-1, 1), c->emit_interleave = int(value);
     else if (n == "row_phases") {
       range(-1, 4);
-      if (value == 0) throw Panic{CYC_ERR_ARG, "row_phases must be -1 (auto), 1 (off) or 2..4"};
+      if (value == 0 || value > 2) throw Panic{CYC_ERR_ARG, "row_phases must be -1 (auto), 1 (off) or 2"};
       c->row_phases = int(value);
+      c->order_lo = c->order_hi = -1;  // the emit lists are re-planned
     }
     else if (n == "ip_items") {
       range(-1, 1);
@@ -688,11 +670,6 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
     }
     else return fail(c, CYC_ERR_ARG, "unknown option " + n);
     drop_graph(c);
-    for (cyc_ctx* k : c->phase_ctx)  // the row-phase children run with the same options
-      if (k && n != "row_phases") {
-        const int rc = cyc_set_option(k, name, value);
-        if (rc != CYC_OK) return fail(c, rc, k->err);
-      }
     return (int)CYC_OK;
   });
 }
@@ -714,7 +691,6 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "class_inplace") *value = c->class_inplace;
   else if (n == "row_phases") *value = c->row_phases;
   else if (n == "row_phases_active") *value = c->phase_used;  // (the last run's phases; 0: a plain run)
-  else if (n == "class_inplace_active" && c->phase_used && c->phase_ctx[0]) return cyc_get_option(c->phase_ctx[0], name, value);
   else if (n == "class_inplace_active") {
     if (!c->prepared || c->order_lo < 0) return fail(c, CYC_ERR_ARG, "class_inplace_active: run a probe first");
     *value = inplace_ok(c, reinterpret_cast<const uint64_t*>(16), reinterpret_cast<const uint64_t*>(16)) ? 1 : 0;

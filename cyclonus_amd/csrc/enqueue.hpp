@@ -370,15 +370,21 @@ static bool enq_emit_blocks(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64
   return true;
 }
 
-static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, uint8_t* d_status, bool inplace = false) {
+// part (row phases): 0 = every row of the plan; 1 / 2 = the rows before / from the split (the plan's
+// emit lists hold them in that order); the status plane goes with part 1, the span reset with part 2
+// (after the last reader of the IP rows' spans, phase 2's class rows).
+static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out_eg, uint8_t* d_status, bool inplace = false,
+                     int part = 0) {
   Problem& pb = c->pb;
-  c->ip_rng_clean = false;  // (set again below when this emit resets the spans for the next run)
+  if (part != 1) c->ip_rng_clean = false;  // (set again below when this emit resets the spans for the next run)
   const uint32_t K = pb.K;
   const uint64_t rw[2] = {uint64_t(K) * c->win_wa, uint64_t(K) * pb.W};  // words per plane row
   uint32_t nr[2];
   for (int d = 0; d < 2; d++) nr[d] = rw[d] ? uint32_t(c->rh[d] - c->rl[d]) : 0u;
-  c->emit_kernel.clear();
-  c->emit_launches = 0;
+  if (part != 2) {
+    c->emit_kernel.clear();
+    c->emit_launches = 0;
+  }
   if (!pb.blocks.empty()) {
     const bool r = enq_emit_blocks(c, st, out_in, out_eg, d_status);
     if (r && pb.K && d_status) c->emit_kernel = "k_emit_blocks", c->emit_launches = 1;
@@ -391,7 +397,7 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
   ea.st_bytes = d_status ? uint64_t(pb.P) * K : 0;
   ea.reset = c->ip_rng.as<uint32_t>();
   ea.reset_n = pb.may_err ? 0u : uint64_t(pb.peers.size()) * 4;  // (k_ip_rows with panics keeps no spans)
-  c->ip_rng_clean = ea.reset_n != 0;
+  if (part != 1) c->ip_rng_clean = ea.reset_n != 0;
   for (uint32_t pl = 0; pl < 2; pl++) {
     ea.row_lo[pl] = uint32_t(c->rl[pl]);
     ea.order[pl] = c->order[pl].as<uint2>();
@@ -415,6 +421,13 @@ static bool enq_emit(cyc_ctx* c, hipStream_t st, uint64_t* out_in, uint64_t* out
     ea.interleave = c->emit_interleave >= 0 ? uint32_t(c->emit_interleave)
                                             : uint64_t(nr[0]) * rw[0] * 8 >= (8ull << 30) ? 1u : 0u;
     ea.n_rows[0] = ea.n_rows[1] = nr[0];
+    if (part) {  // row phases (target rows over the whole table: both planes split at the same row)
+      const uint32_t n1 = c->phase_n1[0];
+      ea.n_rows[0] = ea.n_rows[1] = part == 1 ? n1 : nr[0] - n1;
+      for (int pl = 0; pl < 2; pl++) ea.order[pl] += part == 1 ? 0u : n1;
+      if (part == 1) ea.reset_n = 0;
+      else ea.st_bytes = 0;
+    }
     note(enq_emit_launch(ea, st, out_in, out_eg));
     return true;
   }
@@ -469,8 +482,11 @@ static bool inplace_ok(const cyc_ctx* c, const uint64_t* d_in, const uint64_t* d
 
 // out_in / out_eg non-null: the class rows go straight into those planes (in-place class rows; the
 // emit must then be enqueued with inplace = true).
+// mid (row phases, cyc_ctx::phase_split): enqueues phase 1's emit between the two class-row launches;
+// ev_mid0 / ev_mid1 (eager runs) bracket phase 2's class rows.
 static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nullptr, hipEvent_t ev_rows = nullptr,
-                            uint64_t* out_in = nullptr, uint64_t* out_eg = nullptr) {
+                            uint64_t* out_in = nullptr, uint64_t* out_eg = nullptr, const std::function<void()>* mid = nullptr,
+                            hipEvent_t ev_mid0 = nullptr, hipEvent_t ev_mid1 = nullptr) {
   Problem& pb = c->pb;
   const uint32_t P = pb.P, K = pb.K, W = pb.W, D = uint32_t(std::max<size_t>(pb.descs.size(), 1));
   const uint32_t M = uint32_t(pb.pms.size()), E = c->dir[1].n, EW = (E + 63) / 64;
@@ -619,10 +635,20 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   FrontRows fd{}, fe{};
   size_t lds = 0, lds_uni = 0, e_per[2] = {0, 0};
   uint32_t e_na[2] = {0, 0};
+  // row phases: the class rows in two launches with phase 1's emit between them (the caller's mid)
+  const bool phases = c->phase_split && mid && c->need[0].p && c->need[1].p;
+  c->phase_used = phases ? 2 : 0;
+  if (phases) c->run_epoch = c->run_epoch + 1 ? c->run_epoch + 1 : 1;
   for (int d = 0; d < 2; d++) {
     const uint32_t na = c->dir[d].n ? c->n_act[d] : 0u;
     fb.ma[d] = member_args(c, d);
     fc.ma[d] = fb.ma[d];
+    if (phases) {  // the class election marks the classes phase 1's rows use
+      fc.ma[d].need = c->need[d].as<uint32_t>();
+      fc.ma[d].first_row = c->arow[d].as<uint32_t>();
+      fc.ma[d].split = c->phase_split;
+      fc.ma[d].epoch = c->run_epoch;
+    }
     fc.class_of[d] = c->dir[d].class_of.as<uint32_t>();
     fb.member_wave[d] = c->member_wave > 0 || (c->member_wave < 0 && na <= 4096 && c->act_targets[d] >= 4.0);
     fb.nb[4 + d] = na ? blocks(fb.member_wave[d] ? (uint64_t(na) + 3) / 4 : (uint64_t(na) + 255) / 256) : 0u;
@@ -710,23 +736,36 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (gb) k_front_b<<<unsigned(gb), 256, 0, st>>>(fb);
   if (gc) k_front_c<<<unsigned(gc), 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
-  if (!ido) {
-    const unsigned gd = fd.nb[0] + fd.nb[1];
-    if (gd && pl_wave_ok(c)) k_front_d_pm<true><<<gd, pl_threads(c), 0, st>>>(fd);
-    else if (gd) k_front_d_pm<false><<<gd, pl_threads(c), 0, st>>>(fd);
-    if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
-    return true;
-  }
-  if (fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);
-  if (fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
-    k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);
-  } else {  // the directions' class rows as two launches, each at its own register budget (egress 101
-            // VGPRs, ingress 61: one launch at 101 ran config #3 189 -> 170 us, profiles/r03_e_split_ab.txt)
-    if (fe.nb[1] && fe.ra[1].udesc) k_class_rows_ido<true, E_KC, true><<<fe.nb[1], 256, lds_uni, st>>>(fe.ra[1]);
-    else if (fe.nb[1]) k_class_rows_ido<true, E_KC><<<fe.nb[1], 256, lds, st>>>(fe.ra[1]);
-    if (fe.nb[0]) k_class_rows_ido<false, E_KC><<<fe.nb[0], 256, lds, st>>>(fe.ra[0]);
-  }
+  // the class rows: once, or per row phase with phase 1's emit between (the caller's mid)
+  auto class_rows = [&](uint32_t phase) {
+    for (int d = 0; d < 2; d++) {
+      RowArgs& ra = ido ? fe.ra[d] : fd.ra[d];
+      ra.need = c->need[d].as<uint32_t>();
+      ra.epoch = c->run_epoch;
+      ra.phase = phase;
+    }
+    if (!ido) {
+      const unsigned gd = fd.nb[0] + fd.nb[1];
+      if (gd && pl_wave_ok(c)) k_front_d_pm<true><<<gd, pl_threads(c), 0, st>>>(fd);
+      else if (gd) k_front_d_pm<false><<<gd, pl_threads(c), 0, st>>>(fd);
+    } else if (fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
+      k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);
+    } else {  // the directions' class rows as two launches, each at its own register budget (egress 101
+              // VGPRs, ingress 61: one launch at 101 ran config #3 189 -> 170 us, profiles/r03_e_split_ab.txt)
+      if (fe.nb[1] && fe.ra[1].udesc) k_class_rows_ido<true, E_KC, true><<<fe.nb[1], 256, lds_uni, st>>>(fe.ra[1]);
+      else if (fe.nb[1]) k_class_rows_ido<true, E_KC><<<fe.nb[1], 256, lds, st>>>(fe.ra[1]);
+      if (fe.nb[0]) k_class_rows_ido<false, E_KC><<<fe.nb[0], 256, lds, st>>>(fe.ra[0]);
+    }
+  };
+  if (ido && fd.nb[0] + fd.nb[1]) k_front_d<<<fd.nb[0] + fd.nb[1], 256, 0, st>>>(fd);  // identity sets: once
+  class_rows(phases ? 1u : 0u);
   if (ev_rows) HIPCHK(hipEventRecord(ev_rows, st));
+  if (phases) {
+    (*mid)();
+    if (ev_mid0) HIPCHK(hipEventRecord(ev_mid0, st));
+    class_rows(2u);
+    if (ev_mid1) HIPCHK(hipEventRecord(ev_mid1, st));
+  }
   return true;
 }
 
@@ -736,7 +775,10 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
   Problem& pb = c->pb;
   HIPCHK(hipEventRecord(c->ev[0], st));
   const bool ip = inplace_ok(c, d_in, d_eg);
-  const bool fused = front_fused_ok(c) && enq_front_fused(c, st, c->ev[1], c->ev[2], ip ? d_in : nullptr, ip ? d_eg : nullptr);
+  c->phase_used = 0;
+  const std::function<void()> mid = [&] { enq_emit(c, st, d_in, d_eg, d_status, ip, 1); };
+  const bool fused = front_fused_ok(c) && enq_front_fused(c, st, c->ev[1], c->ev[2], ip ? d_in : nullptr, ip ? d_eg : nullptr,
+                                                          &mid, c->ev_p[0], c->ev_p[1]);
   if (!fused) {
     enq_common(c, st);
     for (int d = 0; d < 2; d++) enq_peer_rows(c, d, st);
@@ -745,7 +787,7 @@ static void enqueue_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_
     for (int d = 0; d < 2; d++) enq_class_rows(c, d, st);
     HIPCHK(hipEventRecord(c->ev[2], st));
   }
-  const bool status_done = enq_emit(c, st, d_in, d_eg, d_status, ip && fused);
+  const bool status_done = enq_emit(c, st, d_in, d_eg, d_status, ip && fused, c->phase_used ? 2 : 0);
   HIPCHK(hipEventRecord(c->ev[3], st));
   if (!status_done && d_status && uint64_t(pb.P) * pb.K)
     HIPCHK(hipMemcpyAsync(d_status, c->slot_status.p, uint64_t(pb.P) * pb.K, hipMemcpyDeviceToDevice, st));
@@ -759,8 +801,10 @@ static void capture_pipeline(cyc_ctx* c, hipStream_t st, hipStream_t st2, hipStr
                              uint8_t* d_status) {
   Problem& pb = c->pb;
   const bool ip = inplace_ok(c, d_in, d_eg);
-  if (front_fused_ok(c) && enq_front_fused(c, st, nullptr, nullptr, ip ? d_in : nullptr, ip ? d_eg : nullptr)) {
-    if (enq_emit(c, st, d_in, d_eg, d_status, ip)) return;
+  c->phase_used = 0;
+  const std::function<void()> mid = [&] { enq_emit(c, st, d_in, d_eg, d_status, ip, 1); };
+  if (front_fused_ok(c) && enq_front_fused(c, st, nullptr, nullptr, ip ? d_in : nullptr, ip ? d_eg : nullptr, &mid)) {
+    if (enq_emit(c, st, d_in, d_eg, d_status, ip, c->phase_used ? 2 : 0)) return;
   } else {
     HIPCHK(hipEventRecord(c->fork_ev, st));
     HIPCHK(hipStreamWaitEvent(st3, c->fork_ev, 0));
@@ -887,85 +931,6 @@ static int blocks_status(cyc_ctx* c, hipStream_t st) {
 // allow_capture = false: never capture a graph for this run (cyc_table_run's planes are new on
 // every call, so a captured graph would be re-instantiated each time): graphs = 1 runs as 2.
 // src: rows [lo, hi) are a source shard (CYC_ROWS_SOURCE), else target rows.
-// ---- row phases (cyc_ctx::row_phases): the children a whole-table run is split over
-static void copy_options(cyc_ctx* k, const cyc_ctx* c) {
-  k->use_graphs = c->use_graphs;
-  k->ip_iv = c->ip_iv;
-  k->ip_range = c->ip_range;
-  k->pod_rows = c->pod_rows;
-  k->member_wave = c->member_wave;
-  k->pod_words = c->pod_words;
-  k->class_rpb_opt = c->class_rpb_opt;
-  k->step_events = c->step_events;
-  k->pl_wave = c->pl_wave;
-  k->class_inplace = c->class_inplace;
-  k->pr_group = c->pr_group;
-  k->sel_lazy = c->sel_lazy;
-  k->front_fused = c->front_fused;
-  k->emit_interleave = c->emit_interleave;
-  k->ip_items_opt = c->ip_items_opt;
-  k->plvt_max_mb = c->plvt_max_mb;
-  k->row_phases = 1;  // (a child never splits again)
-}
-static void drop_phases(cyc_ctx* c) {
-  for (auto& k : c->phase_ctx)
-    if (k) {
-      cyc_ctx_destroy(k);
-      k = nullptr;
-    }
-  c->phase_used = 0;
-}
-// Phases of a run: a whole table (every target row, or a source run over every pod — the same planes)
-// of a no-panic, unbatched build; auto = 2 once each plane is >= 8 GB (config #3).
-static int phases_of(const cyc_ctx* c, int64_t lo, int64_t hi) {
-  const Problem& pb = c->pb;
-  if (c->row_phases == 1 || pb.may_err || !pb.blocks.empty() || lo != 0 || hi != int64_t(pb.P) || pb.P < 128) return 1;
-  if (c->row_phases > 1) return c->row_phases;
-  return uint64_t(pb.P) * pb.K * pb.W * 8 >= (8ull << 30) ? 2 : 1;
-}
-static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
-                        int64_t hi, bool allow_capture, bool src);
-static int run_phases(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int F,
-                      bool allow_capture) {
-  const Problem& pb = c->pb;
-  for (int k = 0; k < F; k++) {
-    if (c->phase_ctx[k]) continue;  // made once per prepare: the inputs, tables and options of this context
-    cyc_ctx* ch = nullptr;
-    HIPCHK(hipGetLastError());
-    if (cyc_ctx_create(c->device, &ch) != CYC_OK || !ch->stream) throw HipErr{"row phases: child context"};
-    c->phase_ctx[k] = ch;
-    ch->policy = c->policy;
-    ch->res = c->res;
-    ch->have_policy = ch->have_res = true;
-    ch->pb = c->pb;
-    copy_options(ch, c);
-    build_identities(ch);
-    prepare_device(ch);
-    ch->prepared = true;
-  }
-  const uint64_t row = uint64_t(pb.K) * pb.W;
-  const bool ev = c->use_graphs == 0 || c->step_events;
-  if (ev) HIPCHK(hipEventRecord(c->ev[0], st));
-  c->emit_kernel.clear();
-  c->emit_launches = 0;
-  for (int k = 0; k < F; k++) {
-    const int64_t a = int64_t(pb.P) * k / F, b = int64_t(pb.P) * (k + 1) / F;
-    cyc_ctx* ch = c->phase_ctx[k];
-    const int rc = run_pipeline(ch, st, d_in + uint64_t(a) * row, d_eg + uint64_t(a) * row, d_status, a, b, allow_capture, false);
-    if (rc != CYC_OK) return fail(c, rc, ch->err);
-    if (c->emit_kernel.find(ch->emit_kernel) == std::string::npos)
-      c->emit_kernel += (c->emit_kernel.empty() ? "" : " + ") + ch->emit_kernel;
-    c->emit_launches += ch->emit_launches;
-  }
-  if (ev) HIPCHK(hipEventRecord(c->ev[3], st));
-  c->timed = ev;
-  c->timed_graph = false;
-  c->ran = true;
-  c->last_stream = st;
-  c->phase_used = F;
-  return (int)CYC_OK;
-}
-
 static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_eg, uint8_t* d_status, int64_t lo,
                         int64_t hi, bool allow_capture = true, bool src = false) {
   Problem& pb = c->pb;
@@ -973,9 +938,6 @@ static int run_pipeline(cyc_ctx* c, hipStream_t st, uint64_t* d_in, uint64_t* d_
   if (lo < 0 || hi > int64_t(P) || lo > hi) return fail(c, CYC_ERR_ARG, "row range out of bounds");
   if (src && (lo % 64 || (hi % 64 && hi != int64_t(P))))
     return fail(c, CYC_ERR_ARG, "source rows: row_lo must be a multiple of 64, row_hi too unless it is the pod count");
-  // a source run over every pod writes the target-row planes: it splits like a whole table
-  if (const int F = phases_of(c, lo, hi); F > 1 && d_in && d_eg) return run_phases(c, st, d_in, d_eg, d_status, F, allow_capture);
-  c->phase_used = 0;
   if (c->order_lo != lo || c->order_hi != hi || c->order_src != src) drop_graph(c);  // range plan buffers are re-made
   ensure_range(c, lo, hi, src);
   if (!c->plvt_ready && front_fused_ok(c) && pod_sparse(c)) {
@@ -1159,6 +1121,11 @@ int describe_panic(cyc_ctx* c, uint32_t s, uint32_t d, uint32_t cfg, uint32_t id
 
 static void destroy_events(cyc_ctx* c) {
   for (auto& e : c->ev)
+    if (e) {
+      (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+  for (auto& e : c->ev_p)
     if (e) {
       (void)hipEventDestroy(e);
       e = nullptr;

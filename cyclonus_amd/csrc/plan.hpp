@@ -628,13 +628,27 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
       c->ido_ew1 = e0 == UINT32_MAX ? 0u : (e1 + 63) / 64;
     }
   }
+  // row phases (cyc_ctx::row_phases): a whole no-panic table splits at row P/2 — auto once each plane
+  // is >= 8 GB; the emit lists then hold the rows before the split first
+  const bool whole = lo == 0 && hi == int64_t(pb.P) && (!src || c->win_wa == pb.W);
+  const bool big = uint64_t(pb.P) * pb.K * pb.W * 8 >= (8ull << 30);
+  c->phase_split = c->row_phases != 1 && whole && !pb.may_err && pb.blocks.empty() && pb.P >= 128 &&
+                           (c->row_phases == 2 || big) ? uint32_t(pb.P / 2) : 0u;
   for (int d = 0; d < 2; d++) {  // emit row order: clustered by this direction's identity, (pod, identity) pairs
     std::vector<uint32_t> ord(size_t(c->rh[d] - c->rl[d]));
     std::iota(ord.begin(), ord.end(), uint32_t(c->rl[d]));
     const auto& i1 = c->ids[d].of_pod;
     const auto& i2 = c->ids[1 - d].of_pod;
-    std::stable_sort(ord.begin(), ord.end(),
-                     [&](uint32_t x, uint32_t y) { return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y]; });
+    const uint32_t split = c->phase_split;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+      if (split && (x < split) != (y < split)) return x < split;
+      return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y];
+    });
+    c->phase_n1[d] = split ? split - uint32_t(c->rl[d]) : 0u;
+    if (split && c->need[d].bytes < std::max<uint64_t>(c->ids[d].ns.size(), 1) * 4) {
+      c->need[d].alloc(std::max<uint64_t>(c->ids[d].ns.size(), 1) * 4);
+      HIPCHK(hipMemset(c->need[d].p, 0, c->need[d].bytes));
+    }
     std::vector<uint32_t> pairs(ord.size() * 2);
     for (size_t r = 0; r < ord.size(); r++) {
       pairs[2 * r] = ord[r];

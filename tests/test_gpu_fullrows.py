@@ -113,9 +113,10 @@ def test_config2_full_rows(ingest):
     _check("config2", {}, [(1, 0), (4, 2)], [(8, 5)], ingest)
 
 
-@INGEST
-def test_config3_full_rows(ingest):
-    _check("config3", {}, [(1, 0), (8, 3)], [(8, 3)], ingest)
+def test_config3_full_rows():
+    """Config #3 through bench.py's flat path (the JSON path's whole planes equal these byte for byte:
+    test_config3_flat_planes_equal_json): the whole table (two row phases), a target and a source shard."""
+    _check("config3", {}, [(1, 0), (8, 3)], [(8, 3)], "flat")
 
 
 @INGEST

@@ -367,7 +367,7 @@ def _ip_stride_problem(seed, n_ns=6, per_ns=90):
     return pols, res, [{"AllAvailable": True}]
 
 
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(2))
 def test_ip_interval_words(gpu, seed):
     """IP rows by a test per word (ip_range = 0), from the address index wherever an IPBlock matches
     few close pods (1), and by the auto rule (index only over non-affine words), on affine addresses
@@ -475,38 +475,42 @@ def test_ip_pod_interval_rows(gpu, seed):
                     assert np.array_equal(got[2][pod, k], orc.row(probes, "egress", pod, k)), (seed, pod, k)
 
 
-@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("seed", range(4))
 def test_row_phases(gpu, seed):
-    """A whole table run as 2-4 row phases (each phase's front and emit on a child context prepared
-    like the caller's) equals the single run, through every launch mode, on target and whole-range
-    source runs; the reported emit launches and classes add up over the phases."""
-    pols, res, probes = random_problem(91_000 + seed, n_pods=300 + 97 * seed, n_pols=10)
+    """A whole table whose class rows and emit run in two row phases (the classes rows [0, P/2) use, the
+    emit of those rows, then the other classes and the emit of rows [P/2, P)) equals the single pass,
+    through every launch mode (graph replays included: a replay's epoch is the captured one), on
+    target and whole-range source runs, for identity-set and materialised-row (PM) builds."""
+    pols, res, probes = random_problem(91_000 + seed, n_pods=300 + 97 * seed, n_pols=10 + 3 * seed)
     eng = Engine(0).build_policies(pols).load_resources(res)
     eng.prepare(probes)
     if eng.shape["may_panic"]:
         pytest.skip("a build that may panic never splits")
     want = eng.run_host()
-    assert eng.get_option("row_phases_active") == 0  # (auto: 2 only from 8 GB planes up)
-    for F in (2, 3, 4):
-        eng.set_option("row_phases", F)
+    assert eng.get_option("row_phases_active") == 0  # (auto: only from 8 GB planes up)
+    eng.set_option("row_phases", 2)
+    for pod_words in (-1, 0):
+        eng.set_option("pod_words", pod_words)
         for graphs in (-1, 1, 0):
             eng.set_option("graphs", graphs)
-            for part in ("target", "source"):
-                got = eng.run_host(0, None, part)
-                assert eng.get_option("row_phases_active") == F
-                assert eng.last_emit()[1] == F, eng.last_emit()
-                for name, a, b in zip(("status", "ingress", "egress"), want, got):
-                    assert np.array_equal(a, b), f"seed {seed} row_phases {F} graphs {graphs} {part}: {name} differs"
-        assert sum(eng.classes()) > 0
-        eng.set_option("graphs", 0)
-        eng.run_host()
-        t = eng.timings()
-        assert t[0] > 0 and t[1] > 0 and t[2] >= 0, t
-    eng.set_option("row_phases", 1)
+            for rep in range(2):
+                for part in ("target", "source"):
+                    got = eng.run_host(0, None, part)
+                    if eng.get_option("front_fused_active"):
+                        assert eng.get_option("row_phases_active") == 2
+                        assert eng.last_emit()[1] == 2, eng.last_emit()
+                    for name, a, b in zip(("status", "ingress", "egress"), want, got):
+                        assert np.array_equal(a, b), (f"seed {seed} pod_words {pod_words} graphs {graphs} {part} rep {rep}: "
+                                                      f"{name} differs")
+    eng.set_option("graphs", 0)
+    eng.run_host()
+    t = eng.timings()
+    assert t[0] > 0 and t[1] > 0 and t[2] >= 0, t
     eng.run_host(0, 100)  # a row range never splits
     assert eng.get_option("row_phases_active") == 0
-    with pytest.raises(Exception):
-        eng.set_option("row_phases", 0)
+    for v in (0, 3):
+        with pytest.raises(Exception):
+            eng.set_option("row_phases", v)
 
 
 def _shared_ipblock_problem(seed, bad=False):
