@@ -411,7 +411,13 @@ int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
  *                 wave over 4 chunks (0)
  *   "emit_interleave" -1 (default: auto = 1 when a plane of a target-row run is >= 8 GB) / 0 / 1: the
  *                 emit's row list alternates ingress and egress rows (1) or holds all ingress rows first
- * cyc_get_option also reports "launch" (the graphs mode in effect), "front_fused_active" and
+ *   "row_phases"  -1 (default: auto = 2 for whole no-panic tables whose planes are >= 8 GB) / 1 / 2: the
+ *                 class rows and the emit in two row phases (the classes rows [0, P/2) use, those rows'
+ *                 emit, then the other classes and rows [P/2, P)) or in one pass (1); the fused front
+ *                 runs once either way (phase 1's emit on a second stream under phase 2's class rows
+ *                 was 4-7 % slower: profiles/r06_row_phases_ab.txt)
+ * cyc_get_option also reports "launch" (the graphs mode in effect), "row_phases_active" (the last
+ * run's phases: 2, or 0), "front_fused_active" and
  * "pl_wave_active" (all need cyc_probe_prepare); "pod_words" reports the mode the prepared probe
  * uses (0 or 1). */
 int cyc_set_option(cyc_ctx* ctx, const char* name, int64_t value);
