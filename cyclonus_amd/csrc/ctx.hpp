@@ -151,8 +151,6 @@ struct cyc_ctx {
   bool ip_mono[2] = {false, false};
   DevBuf ipv_tests, ipv_iv;
   uint32_t rv_off[3] = {0, 0, 0}, Rv = 0;
-  // per peer id: its interval-built row's intervals packed for the class rows (iv_ref), ~0 for the rest
-  DevBuf ipv_ref;
   uint32_t rpu_off[3] = {0, 0, 0};  // sub-lists of pod_peers_u: one pod peer per distinct matcher
   DevBuf ipi_items, ipi_list;   // IP-row work items of the fused front (DIPItem; ip_rows_items_blk) and their rows
   uint32_t ipi_off[3] = {0, 0, 0};  // items of segment x: [ipi_off[x], ipi_off[x + 1])
@@ -174,8 +172,6 @@ struct cyc_ctx {
                         // replay: profiles/r01_front_fused_ab.txt), else 1
   int ip_iv = -1;       // "ip_iv": IP rows as pod intervals where the network's family is address-monotone
                         // in pod order (-1 auto = 1), 0 never
-  int iv_rows = -1;     // "iv_rows": class rows compute interval-built IP rows' words from their intervals
-                        // instead of loading them (-1 auto = 1), 0 load the PM words
   int ip_range = -1;    // "ip_range": IP rows of few, close pods from the address index: -1 auto (where the
                         // words are not affine), 1 wherever they fit, 0 never
   int pod_rows = -1;    // "pod_rows": pod-peer PM rows per pod directly (1), through identity outcomes

@@ -68,12 +68,6 @@ struct RowArgs {
   // row phases: phase 1 computes the classes with need == epoch, phase 2 the others; 0 = every class
   const uint32_t* need;
   uint32_t epoch, phase;
-  // interval-built IP rows (ip_rows_iv_blk), computed where used instead of loaded (option iv_rows):
-  // per peer id its row's intervals (iv_ref; null: load every PM word), the intervals, the words'
-  // family masks (every pod holds a valid address on such runs: its IPv4 pods are the others)
-  const uint32_t* ipv_ref;
-  const uint2* ipv_iv;
-  const DWordIP* words;
 };
 // This launch computes representative i's class rows (row phases, RowArgs::phase).
 __device__ __forceinline__ bool in_phase(const RowArgs& a, uint32_t i) {
@@ -572,17 +566,12 @@ __device__ __forceinline__ uint64_t pl_word(const RowArgs& a, const uint4& e, ui
   const uint64_t v = a.PM[uint64_t(e.x) * a.W + w];
   return (e.z & PL_IP) ? v & cnz_mask(a.ip_cnz, a.W, e.x, w) : v;
 }
-constexpr uint32_t PL_IVPOOL = 256;  // staged intervals per representative (2 KB)
 struct PlShared {  // one per block, shared by both directions' instantiations of a fused launch
   uint4 e[PL_LDS];        // (row, port matcher, first word, last word)
   uint32_t bits[PL_LDS];  // port test bits
   uint32_t pre[PL_TGT + 1], poff[PL_TGT];
   uint32_t all;
   int32_t rdu[32];  // ingress, K <= 32: the representative's job descriptor per slot (-1: slot not VALID)
-  // wave-per-chunk rows: the intervals of the representative's interval-built IP entries (iv_rows), taken
-  // in the flatten with an LDS counter; an entry whose intervals do not fit loads its PM words
-  uint2 iv[PL_IVPOOL];
-  uint32_t ivn;
 };
 
 constexpr int PL_ITEMS = 1;
@@ -723,12 +712,10 @@ constexpr uint32_t PL_WBATCH = 4, PL_NB = 4;
 struct PlLane {
   uint32_t row, bits;
   uint64_t cm;
-  uint32_t iv;  // the entry's staged intervals (fam, LDS offset, count - 1; iv_ref layout) or IV_NONE
 };
-__device__ __forceinline__ PlLane pl_lane(const RowArgs& a, const uint4* src, uint32_t x, uint32_t m, const uint32_t* ivsrc = nullptr) {
-  PlLane l{PL_SKIP, 0u, 0ull, IV_NONE};
+__device__ __forceinline__ PlLane pl_lane(const RowArgs& a, const uint4* src, uint32_t x, uint32_t m) {
+  PlLane l{PL_SKIP, 0u, 0ull};
   if (x < m) {
-    if (ivsrc) l.iv = ivsrc[x];
     const uint4 e = src[x];  // (row, port bits, first word | PL_IP, last word)
     l.row = e.x;
     l.bits = e.y;
@@ -762,14 +749,13 @@ __device__ __forceinline__ void pl_load_batch(const RowArgs& a, const PlLane& g,
 }
 
 template <bool EGRESS, bool UNI = false>
-__device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared& sh, const uint64_t* s_m6, const uint4* spill,
-                                               uint32_t i, uint32_t m, bool allow_all, uint64_t lastmask, uint32_t w0,
-                                               uint32_t wa) {
+__device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared& sh, const uint4* spill, uint32_t i,
+                                               uint32_t m, bool allow_all, uint64_t lastmask, uint32_t w0, uint32_t wa) {
   static_assert(PL_LDS % 64 == 0, "a lane group of entries is all in LDS or all spilled");
   const uint32_t lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
   // the chunks holding the window's words (<= 64 chunks in all: pl_wave_ok)
   const uint32_t cend = (w0 + wa + 63) / 64;
-  const PlLane g0 = pl_lane(a, sh.e, lane, m, a.ipv_ref ? sh.bits : nullptr);  // entries 0..63, one per lane, for every chunk
+  const PlLane g0 = pl_lane(a, sh.e, lane, m);  // entries 0..63, one per lane, for every chunk
   uint64_t* const rows = a.A + arow_of(a, i) * a.K * a.WA;  // the class row's slot 0
   const bool pair = a.WA % 2 == 0 && w0 % 2 == 0 && reinterpret_cast<uintptr_t>(a.A) % 16 == 0;
   uint32_t vslots = 0;  // ingress: the representative's VALID slots (class_rows_pl_blk staged them)
@@ -805,28 +791,9 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
     for (uint32_t x0 = 0; x0 < (allow_all ? 0u : m); x0 += 64) {
       PlLane g = g0;  // (uniform branches: an LDS or a global load, never a flat one)
       if (x0 >= PL_LDS) g = pl_lane(a, spill, x0 + lane, m);
-      else if (x0) g = pl_lane(a, sh.e, x0 + lane, m, a.ipv_ref ? sh.bits : nullptr);
-      // the entries with a nonzero PM word in this chunk; their words are loaded PL_WBATCH at a time,
-      // those of interval-built rows computed from their staged intervals
+      else if (x0) g = pl_lane(a, sh.e, x0 + lane, m);
+      // the entries with a nonzero PM word in this chunk; their words are loaded PL_WBATCH at a time
       uint64_t todo = __ballot((g.cm >> c) & 1ull);
-      uint64_t tiv = a.ipv_ref ? todo & __ballot(g.iv != IV_NONE) : 0ull;
-      todo &= ~tiv;
-      const uint64_t m6 = tiv ? s_m6[wl - w0] : 0ull;  // the word's IPv6 pods (the rest are IPv4)
-      while (tiv) {
-        const uint32_t src = __ffsll((unsigned long long)tiv) - 1;
-        tiv &= tiv - 1;
-        const uint32_t r = __builtin_amdgcn_readlane(g.iv, src), b = __builtin_amdgcn_readlane(g.bits, src);
-        const uint32_t o = iv_ref_off(r), n = iv_ref_cnt(r);
-        uint64_t v = 0;
-        for (uint32_t t = 0; t < n; t++) {
-          const uint2 iv = sh.iv[o + t];
-          v |= pod_span_bits(wl, iv.x, iv.y);
-        }
-        v &= (r >> 31) ? m6 : ~m6;
-#pragma unroll
-        for (uint32_t d = 0; d < PL_NB; d++)
-          if ((b >> d) & 1u) acc[d] |= v;
-      }
       while (todo) {
         uint32_t bits[PL_WBATCH];
         uint64_t v[PL_WBATCH];
@@ -873,7 +840,7 @@ __device__ __forceinline__ void pl_wave_chunks(const RowArgs& a, const PlShared&
 }
 
 template <bool EGRESS, bool WAVE>
-__device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint64_t* s_m6, uint32_t bid_, uint32_t nblk_) {
+__device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
   ht_clear_slice(a, bid_, nblk_);
   const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC;
@@ -884,7 +851,7 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     const uint32_t nt = a.cnt[i];
     const uint32_t* lst = a.list + a.list_off[i];
     uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
-    if (threadIdx.x == 0) sh.all = sh.ivn = 0;
+    if (threadIdx.x == 0) sh.all = 0;
     // ingress (K <= 32): the representative's descriptor per slot, read by the peers' slot bits below
     // and by the chunk walk (the first barrier of the target loop, or the one after it, publishes it)
     if (!EGRESS && threadIdx.x < min(a.K, 32u)) {
@@ -894,11 +861,6 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
       sh.rdu[threadIdx.x] = st == CYC_JOB_VALID ? ds : -1;
     }
     uint32_t m = 0;
-    if (WAVE && a.ipv_ref) {  // interval entries: the window's IPv6 pods per word (published by the barriers below)
-      uint32_t w0, wa;
-      rep_window(a, i, w0, wa);
-      for (uint32_t x = threadIdx.x; x < wa; x += blockDim.x) s_m6[x] = a.words[w0 + x].m6;
-    }
     for (uint32_t t0 = 0; t0 < nt; t0 += PL_TGT) {  // targets in chunks: offsets, counts, prefix sums
       const uint32_t ntc = min(PL_TGT, nt - t0);
       static_assert(PL_TGT == 64, "one wave scans a target chunk");
@@ -931,7 +893,6 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
         // and the port bits), whatever the peer's kind: no load waits inside a divergent branch
         const DPeer pr = a.peers[j];
         const uint32_t prj = a.prow[j];
-        const uint32_t ivr = WAVE && a.ipv_ref ? a.ipv_ref[j] : IV_NONE;
         const uint32_t row = pr.kind == 3 ? prj : j;
         const uint32_t rlo = a.ip_rng[4 * row], rhi = a.ip_rng[4 * row + 1];
         const uint32_t pbits = a.portbits ? a.portbits[pr.kind == 0 ? 0u : pr.port] : 0u;
@@ -963,26 +924,9 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
           if (kbits && !bits) en.x = PL_SKIP;  // the port matcher passes no slot / descriptor here
         }
         const uint32_t x = m + e;
-        // wave-per-chunk rows: an interval-built IP row's intervals go to the LDS pool (its slot of
-        // sh.bits, unused by those rows, names them); the rest load their PM words
-        uint32_t ivs = IV_NONE;
-        if (WAVE && pr.kind == 3 && ivr != IV_NONE && en.x < PL_SKIP && x < PL_LDS) {
-          const uint32_t n = iv_ref_cnt(ivr), o = atomicAdd(&sh.ivn, n);
-          if (o + n <= PL_IVPOOL) {
-            const uint2* src = a.ipv_iv + iv_ref_off(ivr);
-            uint2 v[4];
-#pragma unroll
-            for (uint32_t t = 0; t < 4; t++) v[t] = src[min(t, n - 1)];  // (all in flight)
-#pragma unroll
-            for (uint32_t t = 0; t < 4; t++)
-              if (t < n) sh.iv[o + t] = v[t];
-            for (uint32_t t = 4; t < n; t++) sh.iv[o + t] = src[t];
-            ivs = iv_ref(ivr >> 31, o, n);
-          }
-        }
         if (x < PL_LDS) {
           sh.e[x] = en;
-          sh.bits[x] = WAVE && a.ipv_ref ? ivs : bits;
+          sh.bits[x] = bits;
         } else {
           spill[x] = en;
         }
@@ -1010,9 +954,9 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
     uint32_t w0, wa;
     rep_window(a, i, w0, wa);
     if (WAVE && EGRESS && a.udesc) {
-      pl_wave_chunks<EGRESS, true>(a, sh, s_m6, spill, i, m, allow_all, lastmask, w0, wa);
+      pl_wave_chunks<EGRESS, true>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
     } else if (WAVE) {
-      pl_wave_chunks<EGRESS>(a, sh, s_m6, spill, i, m, allow_all, lastmask, w0, wa);
+      pl_wave_chunks<EGRESS>(a, sh, spill, i, m, allow_all, lastmask, w0, wa);
     } else {
       const uint32_t items = nkc * wa;
       for (uint32_t it0 = threadIdx.x; it0 < items; it0 += PL_ITEMS * blockDim.x)
@@ -1024,8 +968,7 @@ __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh
 template <bool EGRESS, bool WAVE>
 __global__ __launch_bounds__(256) void k_class_rows_pl(RowArgs a) {
   __shared__ PlShared sh;
-  extern __shared__ uint64_t s_m6[];  // (iv_rows: the class window's words, pl_lds_bytes)
-  class_rows_pl_blk<EGRESS, WAVE>(a, sh, s_m6, blockIdx.x, gridDim.x);
+  class_rows_pl_blk<EGRESS, WAVE>(a, sh, blockIdx.x, gridDim.x);
 }
 
 // Class rows from identity sets (IDO builds).  Block = (class representative, KC job slots,

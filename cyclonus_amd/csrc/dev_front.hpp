@@ -265,10 +265,9 @@ __global__ __launch_bounds__(256) void k_front_d(FrontRows f) {
 template <bool WAVE>
 __global__ __launch_bounds__(256) void k_front_d_pm(FrontRows f) {
   __shared__ PlShared sh;
-  extern __shared__ uint64_t s_m6[];  // (iv_rows: the class window's words, pl_lds_bytes)
   const uint32_t b = blockIdx.x;
-  if (b < f.nb[1]) class_rows_pl_blk<true, WAVE>(f.ra[1], sh, s_m6, b, f.nb[1]);
-  else class_rows_pl_blk<false, WAVE>(f.ra[0], sh, s_m6, b - f.nb[1], f.nb[0]);
+  if (b < f.nb[1]) class_rows_pl_blk<true, WAVE>(f.ra[1], sh, b, f.nb[1]);
+  else class_rows_pl_blk<false, WAVE>(f.ra[0], sh, b - f.nb[1], f.nb[0]);
 }
 
 // egress blocks first: they are the slower ones (per-destination port masks), so the launch's

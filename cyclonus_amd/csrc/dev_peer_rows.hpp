@@ -641,12 +641,6 @@ struct DIPIv {
   uint32_t peer, fam, ivoff, ivcnt;  // fam 0 = IPv4, 1 = IPv6; intervals ipv_iv[ivoff .. ivoff + ivcnt), ascending
 };
 constexpr uint32_t IPV_MAX = 16;  // intervals an interval-built row may have (1 + its same-family excepts)
-// A row's intervals as the class rows read them (RowArgs::ipv_ref, per peer id): family in bit 31, first
-// interval in bits 5-30, count - 1 in bits 0-4; IV_NONE for rows that are not interval-built
-constexpr uint32_t IV_NONE = 0xFFFFFFFFu, IV_OFF_MAX = (1u << 26) - 1;
-__host__ __device__ inline uint32_t iv_ref(uint32_t fam, uint32_t off, uint32_t cnt) { return (fam << 31) | (off << 5) | (cnt - 1); }
-__host__ __device__ inline uint32_t iv_ref_cnt(uint32_t r) { return (r & 31u) + 1u; }
-__host__ __device__ inline uint32_t iv_ref_off(uint32_t r) { return (r >> 5) & IV_OFF_MAX; }
 __device__ __forceinline__ uint64_t pod_span_bits(uint32_t w, uint32_t x, uint32_t y) {  // pods [x, y) in word w
   const uint32_t b0 = w * 64, a = max(x, b0), b = min(y, b0 + 64);
   if (b <= a) return 0ull;

@@ -643,7 +643,6 @@ int cyc_set_option(cyc_ctx* c, const char* name, int64_t value) {
       c->ip_iv = int(value);
       c->order_lo = c->order_hi = -1;  // the next run re-plans which IP rows are interval-built
     }
-    else if (n == "iv_rows") range(-1, 1), c->iv_rows = int(value);
     else if (n == "member_wave") range(-1, 1), c->member_wave = int(value);
     else if (n == "class_rpb") range(0, 64), c->class_rpb_opt = value;
     else if (n == "pl_wave") range(0, 1), c->pl_wave = int(value);
@@ -684,7 +683,6 @@ int cyc_get_option(cyc_ctx* c, const char* name, int64_t* value) {
   else if (n == "ip_range") *value = c->ip_range;
   else if (n == "ip_iv") *value = c->ip_iv;
   else if (n == "ip_iv_rows") *value = c->Rv;  // (the last range plan's interval-built rows)
-  else if (n == "iv_rows") *value = c->iv_rows;
   else if (n == "member_wave") *value = c->member_wave;
   else if (n == "class_rpb") *value = c->class_rpb_opt;
   else if (n == "pl_wave") *value = c->pl_wave;

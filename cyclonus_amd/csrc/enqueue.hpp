@@ -224,11 +224,6 @@ static RowArgs row_args(cyc_ctx* c, int d) {
   ra.ht_clear = reinterpret_cast<uint32_t*>(dd.ht_key.p);
   ra.ht_clear_words = uint64_t(dd.ht_cap) * 4;
   ra.rpb = 1;
-  if (c->iv_rows != 0 && c->Rv && c->ipv_ref.p) {  // interval-built IP rows computed where used
-    ra.ipv_ref = c->ipv_ref.as<uint32_t>();
-    ra.ipv_iv = c->ipv_iv.as<uint2>();
-    ra.words = c->ip_words.as<DWordIP>();
-  }
   return ra;
 }
 
@@ -239,10 +234,6 @@ static bool pl_wave_ok(const cyc_ctx* c) {
   return c->pl_wave && pb.K <= PL_NB && pb.descs.size() <= PL_NB && pb.descs.size() && pb.pms.size() &&
          port_bits_on(c) && pb.W <= 64 * 64;
 }
-
-// Dynamic LDS of the wave-per-chunk PM class rows: the class window's IPv6 pod masks when interval-built
-// IP rows are computed where used (RowArgs::ipv_ref)
-static size_t pl_lds_bytes(const RowArgs& ra) { return ra.ipv_ref ? size_t(ra.WA) * 8 : 0; }
 
 static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
   Problem& pb = c->pb;
@@ -269,9 +260,9 @@ static void enq_class_rows(cyc_ctx* c, int d, hipStream_t st) {
     else k_class_rows_ido<true, 4><<<gi, 256, per * ra.rpb, st>>>(ra);
   } else {  // per-class flattened peer lists (the IP word spans are final here)
     const bool wave = pl_wave_ok(c);
-    if (d == 0 && wave) k_class_rows_pl<false, true><<<pl_blocks(c, d), pl_threads(c), pl_lds_bytes(ra), st>>>(ra);
+    if (d == 0 && wave) k_class_rows_pl<false, true><<<pl_blocks(c, d), pl_threads(c), 0, st>>>(ra);
     else if (d == 0) k_class_rows_pl<false, false><<<pl_blocks(c, d), pl_threads(c), 0, st>>>(ra);
-    else if (wave) k_class_rows_pl<true, true><<<pl_blocks(c, d), pl_threads(c), pl_lds_bytes(ra), st>>>(ra);
+    else if (wave) k_class_rows_pl<true, true><<<pl_blocks(c, d), pl_threads(c), 0, st>>>(ra);
     else k_class_rows_pl<true, false><<<pl_blocks(c, d), pl_threads(c), 0, st>>>(ra);
   }
 }
@@ -691,7 +682,8 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   // 16 representatives), else 4 (config #3: E 106 -> 96 us at N = 1 with 16; at N = 8 a source
   // shard's ~1,900 blocks of 4 ran 22.8 us, of 8 24.0 — profiles/r04_class_rpb_ab.txt).  With row
   // phases each of the two launches computes about half of the classes, so half of its blocks count
-  // (config #3 phased E per step: 16 per block 141.8 us, 8: 121.4, 4: 133.2 — profiles/r06_class_rpb_ab.txt)
+  // (config #3 phased E per step, 8 per block against 16: 121.4 vs 141.8 us on one box, 122.8 vs 123.8
+  // on another — profiles/r06_class_rpb_ab.txt)
   auto e_blocks = [&](int d, uint32_t rpb) {
     return uint64_t(ido_chunk_groups(fe.ra[d].WA)) * ((K + E_KC - 1) / E_KC) * ((e_na[d] + rpb - 1) / rpb);
   };
@@ -757,8 +749,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     }
     if (!ido) {
       const unsigned gd = fd.nb[0] + fd.nb[1];
-      if (gd && pl_wave_ok(c))
-        k_front_d_pm<true><<<gd, pl_threads(c), std::max(pl_lds_bytes(fd.ra[0]), pl_lds_bytes(fd.ra[1])), st>>>(fd);
+      if (gd && pl_wave_ok(c)) k_front_d_pm<true><<<gd, pl_threads(c), 0, st>>>(fd);
       else if (gd) k_front_d_pm<false><<<gd, pl_threads(c), 0, st>>>(fd);
     } else if (fe.nb[0] && fe.nb[1] && fe.ra[1].udesc) {
       k_front_e_uni<<<fe.nb[0] + fe.nb[1], 256, std::max(lds, lds_uni), st>>>(fe);

@@ -879,13 +879,6 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
   c->Rv = uint32_t(vtests.size());
   upload(c->ipv_tests, vtests);
   upload(c->ipv_iv, viv);
-  {  // the class rows' view of the interval-built rows (iv_ref): per peer id, its row's intervals
-    std::vector<uint32_t> ref(std::max<size_t>(pb.peers.size(), 1), IV_NONE);
-    for (const DIPIv& t : vtests)
-      if (t.ivcnt && t.ivoff + t.ivcnt <= IV_OFF_MAX) ref[t.peer] = iv_ref(t.fam, t.ivoff, t.ivcnt);
-    for (uint32_t j = 0; j < prow.size(); j++) ref[j] = ref[prow[j]];
-    upload(c->ipv_ref, ref);
-  }
   upload(c->peer_row, prow);
   c->prow_host = prow;
   c->rp_off[2] = uint32_t(pp.size());

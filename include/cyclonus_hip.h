@@ -406,8 +406,6 @@ int cyc_last_emit(cyc_ctx* ctx, char* name, size_t cap, int64_t* launches);
  *                 that table has >= 64M pairs
  *   "ip_iv"       -1 (default: auto) / 0: IP rows as pod-index intervals where the network's family holds
  *                 non-decreasing addresses in pod order (ip_rows_iv_blk), or through the paths below
- *   "iv_rows"     -1 (default: auto = 1) / 0 / 1: the class rows compute the words of interval-built IP
- *                 rows from their intervals (1) or load them from the built rows (0)
  *   "ip_items"    -1 (default: auto = 1 for runs over every row) / 0 / 1: the fused front's IP rows as
  *                 per-chunk work items of the rows that touch each chunk (1) or as groups of 16 rows a
  *                 wave over 4 chunks (0)

@@ -443,8 +443,7 @@ def _ip_mono_problem(seed, n_pods=9000, wide=False):
         spec = {"podSelector": {"matchLabels": {"i": str(k % 7)}}, "policyTypes": ["Ingress", "Egress"],
                 "ingress": [{"from": peers}], "egress": [{"to": peers[::-1]}]}
         pols.append({"metadata": {"name": f"m{k}", "namespace": "x"}, "spec": spec})
-    if wide:  # one policy of every pod with 48 IPBlocks of 10-15 excepts: its classes' intervals overflow
-        # the class-row kernel's LDS pool (PL_IVPOOL), so some entries compute and the rest load
+    if wide:  # one policy of every pod with 48 IPBlocks of 10-15 excepts (rows of many intervals)
         peers = []
         for _ in range(48):
             v6 = rng.random() < 0.4
@@ -464,9 +463,8 @@ def _ip_mono_problem(seed, n_pods=9000, wide=False):
 def test_ip_pod_interval_rows(gpu, seed, wide):
     """IP rows as pod intervals (ip_iv, address-monotone families): whole planes equal the other IP-row
     paths' (ip_iv 0, pinned to the oracle by the tests above) through the fused front, the DAG and the
-    eager launches, with the class rows computing those rows' words from their intervals (iv_rows auto)
-    or loading them (0), on the whole table and on source and target shards; sampled rows against the
-    oracle.  wide: classes with more intervals than the class-row kernel stages."""
+    eager launches, on the whole table and on source and target shards; sampled rows against the
+    oracle.  wide: rows of 10-16 intervals in every class (an all-pods policy with 48 IPBlocks)."""
     pols, res, probes = _ip_mono_problem(seed, wide=wide)
     eng = Engine(0).build_policies(pols).load_resources(res)
     sh = eng.prepare(probes)
@@ -477,8 +475,8 @@ def test_ip_pod_interval_rows(gpu, seed, wide):
     orc = Oracle(pols, res)
     for part, lo, hi in (("target", 0, P), ("source", 0, 4096), ("source", 4096, P), ("target", 1000, 5000)):
         want = ref.run_host(lo, hi, part)
-        for opts in ({}, {"iv_rows": 0}, {"front_fused": 0}, {"graphs": 0}, {"graphs": 1}):
-            for k, v in {"front_fused": 1, "graphs": -1, "iv_rows": -1, **opts}.items():
+        for opts in ({}, {"front_fused": 0}, {"graphs": 0}, {"graphs": 1}):
+            for k, v in {"front_fused": 1, "graphs": -1, **opts}.items():
                 eng.set_option(k, v)
             got = eng.run_host(lo, hi, part)
             assert eng.get_option("ip_iv_rows") > 0
@@ -856,8 +854,7 @@ def test_launch_modes_and_knobs(gpu):
                     ("step_events", 1), ("step_events", 0), ("pr_group", 5), ("pr_group", -1), ("sel_lazy", 1),
                     ("sel_lazy", -1), ("class_inplace", 0), ("class_inplace", 1), ("class_inplace", -1),
                     ("emit_interleave", 1), ("emit_interleave", 0), ("emit_interleave", -1),
-                    ("ip_items", 0), ("ip_items", 1), ("ip_items", -1), ("ip_iv", 0), ("ip_iv", -1), ("iv_rows", 0),
-                    ("iv_rows", 1), ("iv_rows", -1)):
+                    ("ip_items", 0), ("ip_items", 1), ("ip_items", -1), ("ip_iv", 0), ("ip_iv", -1)):
         eng.set_option(name, v)
         assert eng.get_option(name) == v
         assert_same(want, eng.run_host(), f"{name}={v}")
