@@ -19,8 +19,10 @@ if sys.argv[1] == "show":
                       "on d.kernel_id = s.id order by d.start").fetchall()
     # replays end with the emit (and the graph's trailing copy, if any): the last replay = the kernels
     # after the second-to-last emit ended
-    # a step's last emit launch (source shards emit each plane with its own launch)
-    ends = [i for i, r in enumerate(rows) if "k_emit" in r[0] and (i + 1 == len(rows) or "k_emit" not in rows[i + 1][0])]
+    # a step's last emit launch (source shards emit each plane with its own launch; a row-phased step
+    # runs phase 2's class rows between its two emits)
+    mid = ("k_emit", "k_front_e", "k_class_rows", "k_front_d")
+    ends = [i for i, r in enumerate(rows) if "k_emit" in r[0] and (i + 1 == len(rows) or not any(m in rows[i + 1][0] for m in mid))]
     spans = []
     for a, b in zip(ends, ends[1:]):
         seg = rows[a + 1:b + 1]
