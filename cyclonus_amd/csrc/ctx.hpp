@@ -129,6 +129,12 @@ struct cyc_ctx {
   bool plvt_ready = false;
   int64_t plvt_max_mb = 1024;  // "plvt_max_mb": largest PLVT built (0: never, the LVT gathers instead)
   DevBuf sel_one;   // SelView::one
+  std::vector<uint4> sel_one_h;  // its host copy (the identity-set peer records, pb_rec)
+  // per identity-set row (pod_peers_u): its matcher as three 16-byte records — (namespace matcher kind,
+  // namespace / selector, pod selector, 0), then the namespace selector's and the pod selector's
+  // one-requirement records (SelView::one; SEL_ALL when there is none): peer_bits_blk loads a row
+  // group's records in one vector load instead of pod_peers -> peers -> one chains
+  DevBuf pb_rec;
   DevBuf req_post, post_pods;  // label postings: per requirement (offset, count) x 2 values; pod lists
   std::vector<uint8_t> req_post_ok;  // the requirement's pods are its postings (EQ, IN of <= 2 values)
   DevBuf pp_scan, pp_post;     // sparse pod rows: pod peers scanned per word / built from postings

@@ -114,6 +114,9 @@ constexpr uint32_t IDO_LDS_BYTES = 48 * 1024;  // staged identity sets per class
 constexpr uint32_t PB_GROUP = 16;  // pod peers per identity-set wave (8: +4 % launch B, profiles/r02_pb_group_ab.txt)
 // pod peers whose selector loads are in flight together (8: k_front_b 61 -> 81 VGPRs)
 constexpr uint32_t PB_HALF_MAX = 4;
+#ifndef CYC_PB_WIDE
+#define CYC_PB_WIDE 8  // peers whose label-table gathers are in flight together (pb_rec path)
+#endif
 // Identity words [ew0, ew0 + new) of the rows only (a source shard's ingress peers: the words of the
 // egress identities its sources have).
 __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t EW, const uint32_t* __restrict__ pod_peers,
@@ -121,25 +124,65 @@ __device__ __forceinline__ void peer_bits_blk(uint32_t Rp, uint32_t E, uint32_t 
                                                    const uint32_t* __restrict__ id_ns, const uint32_t* __restrict__ id_nsls,
                                                    const uint32_t* __restrict__ id_ls, uint64_t* __restrict__ idob, uint32_t bid_, uint32_t nblk_,
                                                    uint32_t ew0, uint32_t new_, const uint2* __restrict__ grp_ns,
-                                                   const uint2* __restrict__ word_ns) {
+                                                   const uint2* __restrict__ word_ns, const uint4* __restrict__ prec = nullptr) {
   // the wave index is wave-uniform: a scalar, so the peers' records below are scalar loads
   const uint32_t wv = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const uint32_t groups = (Rp + PB_GROUP - 1) / PB_GROUP;
   if (wv >= groups * new_) return;
-  const uint32_t g = wv / new_, ew = ew0 + wv % new_;
+  const uint32_t g = wv / new_, ew = ew0 + wv % new_, g0 = g * PB_GROUP;
+  // the identities' own records and (pb_rec) the group's matcher records — 3 x 16 B a row, lane 3x +
+  // part, ONE vector load — are issued before the skip test's loads, so their latencies overlap
+  const uint32_t e = ew * 64 + lane;
+  const bool live = e < E;
+  const uint32_t ns = live ? id_ns[e] : 0u, nsls = live ? id_nsls[e] : 0u, ls = live ? id_ls[e] : 0u;
+  const bool use_rec = prec && !sv.selres;
+  const uint4 R = use_rec ? prec[min(3 * g0 + (lane < 3 * PB_GROUP ? lane : 0u), 3 * Rp - 1)] : uint4{0, 0, 0, 0};
   {  // a group of exact-namespace peers (podpeermatcher.go:115-125: ns == the policy's namespace) whose
      // namespaces the word's identities do not have matches none of them: zeros, no selector loads
     const uint2 gr = grp_ns[g], wr = word_ns[ew];
     if (gr.y < wr.x || gr.x > wr.y) {
-      const uint32_t p = g * PB_GROUP + lane;
+      const uint32_t p = g0 + lane;
       if (lane < PB_GROUP && p < Rp) idob[uint64_t(p) * EW + ew] = 0;
       return;
     }
   }
-  const uint32_t e = ew * 64 + lane;
-  const bool live = e < E;
-  const uint32_t ns = live ? id_ns[e] : 0u, nsls = live ? id_nsls[e] : 0u, ls = live ? id_ls[e] : 0u;
   uint64_t mine = 0;
+  if (use_rec) {
+    // per PB_WIDE peers every label-table gather at once: two memory round trips a batch fewer than the
+    // pod_peers -> peers -> one chain (podpeermatcher.go:21-28)
+    constexpr uint32_t PB_WIDE = CYC_PB_WIDE;
+#pragma unroll
+    for (uint32_t h = 0; h < PB_GROUP; h += PB_WIDE) {
+      uint32_t xn[PB_WIDE], xp[PB_WIDE];
+#pragma unroll
+      for (uint32_t x = 0; x < PB_WIDE; x++) {  // (record fields: scalar reads of lanes 3x + 1 / 2)
+        const uint32_t on_x = __builtin_amdgcn_readlane(R.x, 3 * (h + x) + 1), on_y = __builtin_amdgcn_readlane(R.y, 3 * (h + x) + 1);
+        const uint32_t op_x = __builtin_amdgcn_readlane(R.x, 3 * (h + x) + 2), op_y = __builtin_amdgcn_readlane(R.y, 3 * (h + x) + 2);
+        xn[x] = sv.LVT[uint64_t(on_x < SEL_ALL ? on_y : 0u) * sv.L + nsls];
+        xp[x] = sv.LVT[uint64_t(op_x < SEL_ALL ? op_y : 0u) * sv.L + ls];
+      }
+#pragma unroll
+      for (uint32_t x = 0; x < PB_WIDE; x++) {
+        const uint32_t q = 3 * (h + x);
+        const uint32_t nk = __builtin_amdgcn_readlane(R.x, q), nv = __builtin_amdgcn_readlane(R.y, q),
+                       ps = __builtin_amdgcn_readlane(R.z, q);
+        const uint32_t on_x = __builtin_amdgcn_readlane(R.x, q + 1), op_x = __builtin_amdgcn_readlane(R.x, q + 2);
+        uint32_t rn = 1u, rp = 1u;
+        if (nk == 2 && on_x == SEL_WALK) rn = sel_eval(sv, sv.LVT, sv.L, nv, nsls);
+        else if (nk == 2 && on_x != SEL_ALL)
+          rn = req_holds(on_x & 0xFFu, xn[x], __builtin_amdgcn_readlane(R.z, q + 1), __builtin_amdgcn_readlane(R.w, q + 1), on_x >> 8);
+        if (ps != CYC_ALL && op_x == SEL_WALK) rp = sel_eval(sv, sv.LVT, sv.L, ps, ls);
+        else if (ps != CYC_ALL && op_x != SEL_ALL)
+          rp = req_holds(op_x & 0xFFu, xp[x], __builtin_amdgcn_readlane(R.z, q + 2), __builtin_amdgcn_readlane(R.w, q + 2), op_x >> 8);
+        const bool m = live && g0 + h + x < Rp && (nk != 0 || ns == nv) && rn == 1 && rp == 1;
+        const uint64_t b = __ballot(m);
+        if (lane == h + x) mine = b;
+      }
+    }
+    const uint32_t p = g0 + lane;
+    if (lane < PB_GROUP && p < Rp) idob[uint64_t(p) * EW + ew] = mine;
+    return;
+  }
   // PB_HALF peers at a time, in phases — their records, then every selector outcome, then the ballots —
   // so the loads of all of them are in flight together instead of one dependent chain per peer
   // (podpeermatcher.go:21-28 namespace then pod matcher; no panic on this path, so both matchers

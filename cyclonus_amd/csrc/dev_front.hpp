@@ -90,6 +90,7 @@ struct FrontB {
   const uint32_t* pod_peers_u_[2];
   uint64_t* idob_[2];
   const uint2* grp_ns_[2];   // per group of PB_GROUP rows: the namespace range of its exact-namespace peers
+  const uint4* pbrec_[2];    // per row its matcher records (pb_rec; null: the peers' chains)
   const uint2* word_ns;      // per egress identity word: its identities' namespace range
   const DPeer* peers;
   const uint8_t* selres;
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(256) void k_front_b(FrontB f) {
         return pod_rows_direct_blk<false>(f.Rp[x], f.P, f.W, f.plist[x], f.peers, f.sv, f.pod_eid, f.id_ns, f.id_nsls,
                                           f.id_ls, f.PM, nullptr, b, f.nb[2 + x], f.pw0[x], f.pnw[x]);
       return peer_bits_blk(f.Ru_[x], f.E, f.EW, f.pod_peers_u_[x], f.peers, f.sv, f.id_ns, f.id_nsls, f.id_ls, f.idob_[x], b,
-                           f.nb[2 + x], f.ew0[x], f.new_[x], f.grp_ns_[x], f.word_ns);
+                           f.nb[2 + x], f.ew0[x], f.new_[x], f.grp_ns_[x], f.word_ns, f.pbrec_[x]);
     }
     b -= f.nb[2 + x];
   }

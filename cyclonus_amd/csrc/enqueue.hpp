@@ -157,6 +157,10 @@ static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
   k_classify<<<grid1(c->n_act[d], 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
 }
 
+#ifndef CYC_PB_REC
+#define CYC_PB_REC 1  // identity-set waves read their rows' matcher records (pb_rec); 0: the peers' chains
+#endif
+
 // 6. class rows of direction d
 // IDO class rows: representatives per block (cyc_set_option "class_rpb"; 0 = auto: 4, or more in
 // the fused front, enq_front_fused), as many as fit the staged identity-set budget
@@ -582,6 +586,7 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
     fb.pod_peers_u_[x] = c->pod_peers_u.as<uint32_t>() + ux;
     fb.idob_[x] = c->idob.as<uint64_t>() + uint64_t(ux) * EW;
     fb.grp_ns_[x] = c->ido_grp_ns.as<uint2>() + c->ido_goff[x];
+    fb.pbrec_[x] = c->pb_rec.p && CYC_PB_REC ? c->pb_rec.as<uint4>() + 3 * uint64_t(ux) : nullptr;
     fb.ew0[x] = x == 0 ? c->ido_ew0 : 0u;
     fb.new_[x] = x == 0 ? c->ido_ew1 - c->ido_ew0 : EW;
     fb.nb[2 + x] = (fb.Ru_[x] && E && fb.new_[x]) ? blocks((uint64_t((fb.Ru_[x] + PB_GROUP - 1) / PB_GROUP) * fb.new_[x] + 3) / 4) : 0u;

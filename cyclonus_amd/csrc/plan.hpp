@@ -227,6 +227,7 @@ static void prepare_device(cyc_ctx* c) {
     for (uint32_t k : pb.ls_key)
       if (kx[k] < 0) kx[k] = int32_t(nk++);
     c->dense_sel = uint64_t(nk + 1) * pb.L * 4 <= (256ull << 20);
+    c->sel_one_h.clear();
     if (c->dense_sel) {
       std::vector<uint32_t> lvt(uint64_t(nk + 1) * pb.L, 0xFFFFFFFFu);
       for (uint32_t l = 0; l < pb.L; l++)
@@ -250,6 +251,7 @@ static void prepare_device(cyc_ctx* c) {
           one[sid] = uint4{q.op | (vc << 8), q.key, vc > 0 ? pb.req_vals[q.voff] : 0u, vc > 1 ? pb.req_vals[q.voff + 1] : 0u};
         }
         upload(c->sel_one, one);
+        c->sel_one_h = one;
       }
       // the same table per pod (PLVT, sparse pod-peer rows) is gathered on the device when a run
       // first needs it (ensure_plvt): IDO builds never read it, and it is (keys + 1) x P words
@@ -927,6 +929,18 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
     }
     c->rpu_off[2] = uint32_t(ppu.size());
     upload(c->pod_peers_u, ppu);
+    {  // the rows' matcher records (pb_rec), read by the identity-set waves when selectors are evaluated there
+      std::vector<uint4> rec(std::max<size_t>(ppu.size(), 1) * 3, uint4{0, 0, 0, 0});
+      const bool one = c->sel_one_h.size() >= std::max<size_t>(pb.S, 1);
+      for (size_t x = 0; one && x < ppu.size(); x++) {
+        const DPeer& pr = pb.peers[ppu[x]];
+        rec[3 * x] = uint4{pr.nskind, pr.nsval, pr.podsel, 0u};
+        rec[3 * x + 1] = pr.nskind == 2 ? c->sel_one_h[pr.nsval] : uint4{SEL_ALL, 0u, 0u, 0u};
+        rec[3 * x + 2] = pr.podsel != CYC_ALL ? c->sel_one_h[pr.podsel] : uint4{SEL_ALL, 0u, 0u, 0u};
+      }
+      if (one) upload(c->pb_rec, rec);
+      else c->pb_rec.alloc(0);
+    }
     upload(c->peer_ido, pi);
     gns.push_back(uint2{0u, 0xFFFFFFFFu});
     upload(c->ido_grp_ns, gns);
