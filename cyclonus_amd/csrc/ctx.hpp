@@ -259,8 +259,6 @@ struct cyc_ctx {
   uint32_t phase_split = 0;   // the range plan's split row (0: no phases): emit lists are [rows < split][rows >= split]
   uint32_t phase_n1[2] = {0, 0};  // per plane: rows before the split in its emit list
   int phase_used = 0;      // the last run's phases (2, or 0 for a plain run)
-  DevBuf need[2];          // per identity: the run epoch whose phase-1 rows use the class it represents
-  uint32_t run_epoch = 0;
   hipEvent_t ev_p[2] = {nullptr, nullptr};  // eager runs: around phase 2's class rows (cyc_last_timings)
   // multi-GPU table assembly (comm.hpp): the context's RCCL communicator, a second stream on which
   // gathered chunks are relaid out under the next chunk's all-gather, and the chunks' double buffer

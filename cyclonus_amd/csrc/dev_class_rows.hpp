@@ -65,13 +65,23 @@ struct RowArgs {
   // kernel in block slices once k_classify is done with it: no memset node precedes k_member
   uint32_t* ht_clear;
   uint64_t ht_clear_words;
-  // row phases: phase 1 computes the classes with need == epoch, phase 2 the others; 0 = every class
-  const uint32_t* need;
-  uint32_t epoch, phase;
+  // row phases: 1 = the classes rows [0, split) use, 2 = the others, 0 = every class (phase_reps)
+  uint32_t phase;
 };
-// This launch computes representative i's class rows (row phases, RowArgs::phase).
-__device__ __forceinline__ bool in_phase(const RowArgs& a, uint32_t i) {
-  return !a.phase || ((a.need[i] == a.epoch) == (a.phase == 1));
+// The representatives: k_classify lists the phase-1 classes' at the head of reps[] (rep_cnt[0] + 1 of
+// them) and, on row-phased runs, the phase-2 classes' from its tail backwards (rep_cnt[1]): logical
+// index k is reps[k] for k < n1, else reps[n_ident - 1 - (k - n1)].  (A class's representative is its
+// smallest identity — the election keeps the minimum — and identities are numbered in pod order, so
+// its first row is the class's first row: the representative alone decides the class's phase.)
+__device__ __forceinline__ uint32_t rep_at(const RowArgs& a, uint32_t k) {
+  const uint32_t n1 = *a.rep_cnt + 1u;
+  return k < n1 ? a.reps[k] : a.reps[a.n_ident - 1u - (k - n1)];
+}
+// This launch's representatives (RowArgs::phase): logical indices [lo, lo + n)
+__device__ __forceinline__ void phase_reps(const RowArgs& a, uint32_t& lo, uint32_t& n) {
+  const uint32_t n1 = *a.rep_cnt + 1u, n2 = a.rep_cnt[1];
+  lo = a.phase == 2 ? n1 : 0u;
+  n = a.phase == 1 ? n1 : a.phase == 2 ? n2 : n1 + n2;
 }
 
 // Row of A holding representative i's class rows: its identity slot, or (in-place class rows) the
@@ -277,8 +287,10 @@ __device__ __forceinline__ void class_ident_blk(RowArgs a, uint32_t bid_, uint32
   const uint32_t wi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wv = bid_ * 4 + wi, lane = threadIdx.x & 63;
   const uint32_t nbc = (a.NB + G - 1) / G;
   const uint32_t r = wv / nbc, nb0 = (wv % nbc) * G;
-  if (r >= *a.rep_cnt + 1u) return;
-  const uint32_t i = a.reps[r];
+  uint32_t rlo, rn;
+  phase_reps(a, rlo, rn);
+  if (r >= rn) return;
+  const uint32_t i = rep_at(a, rlo + r);
   int32_t du[G];
   {  // ingress: the slots' status and descriptor, all G pairs loaded at once
     uint8_t st[G];
@@ -559,8 +571,10 @@ __global__ __launch_bounds__(256) void k_class_rows(RowArgs a) {
   const uint32_t kc = (blockIdx.x / chunks) % nkc;
   const uint32_t lw = (blockIdx.x % chunks) * 256 + threadIdx.x;
   const uint32_t r = blockIdx.x / (chunks * nkc);
-  if (r >= *a.rep_cnt + 1u) return;
-  const uint32_t i = a.reps[r];
+  uint32_t rlo, rn;
+  phase_reps(a, rlo, rn);
+  if (r >= rn) return;
+  const uint32_t i = rep_at(a, rlo + r);
   uint32_t w0, wa;
   rep_window(a, i, w0, wa);
   if (lw < wa) class_row_word<EGRESS, true, KC>(a, i, kc, w0 + lw, w0);
@@ -886,11 +900,12 @@ template <bool EGRESS, bool WAVE>
 __device__ __forceinline__ void class_rows_pl_blk(const RowArgs& a, PlShared& sh, uint32_t bid_, uint32_t nblk_) {
   constexpr int KC = 4;
   ht_clear_slice(a, bid_, nblk_);
-  const uint32_t n_reps = *a.rep_cnt + 1u, nkc = (a.K + KC - 1) / KC;
+  const uint32_t nkc = (a.K + KC - 1) / KC;
+  uint32_t rlo, n_reps;
+  phase_reps(a, rlo, n_reps);
   const bool kbits = EGRESS ? a.portbits != nullptr : a.K <= 32;
   for (uint32_t r = bid_; r < n_reps; r += nblk_) {
-    const uint32_t i = a.reps[r];
-    if (!in_phase(a, i)) continue;  // (block-uniform)
+    const uint32_t i = rep_at(a, rlo + r);
     const uint32_t nt = a.cnt[i];
     const uint32_t* lst = a.list + a.list_off[i];
     uint4* spill = a.ip_list + a.ip_off[i] - PL_LDS;  // entries x >= PL_LDS live at spill[x]
@@ -1096,9 +1111,11 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   // and slot words are loaded once for all its representatives
   const uint32_t cg = ido_chunk_groups(a.WA), nkc = (a.K + KC - 1) / KC;
   const uint32_t kc = (bid_ / cg) % nkc;
-  const uint32_t r0 = (bid_ / (cg * nkc)) * a.rpb, n_reps = *a.rep_cnt + 1u;
+  uint32_t rlo, n_reps;
+  phase_reps(a, rlo, n_reps);
+  const uint32_t r0 = (bid_ / (cg * nkc)) * a.rpb;
   if (r0 >= n_reps) return;  // whole block
-  uint32_t nr = min(a.rpb, n_reps - r0);
+  const uint32_t nr = min(a.rpb, n_reps - r0);
   const uint32_t k0 = kc * KC;
   const uint32_t nrow = EGRESS && !UNI ? a.NB : min(uint32_t(KC), a.K - k0);
   // staged layout: 32-bit word j of row r of representative q at sB32[(q * EW32 + j) * NS + r]
@@ -1116,21 +1133,9 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
   // barrier, its identity sets (B) and its first IDO_IPL IP peers with their port bits.  The row
   // loop then reads them from LDS instead of walking reps -> identity -> list chains.
   __shared__ RepHead<KC> s_rep[IDO_RPB_MAX];
-  __shared__ uint32_t s_nr;
-  // row phases: only this launch's phase's representatives, compacted (the block's reps lie in wave 0)
-  uint32_t slot = threadIdx.x;
-  if (a.phase) {
-    const bool keep = threadIdx.x < nr && in_phase(a, a.reps[r0 + min(threadIdx.x, nr - 1)]);
-    const uint64_t kb = __ballot(keep);
-    slot = keep ? uint32_t(__popcll(kb & ((1ull << (threadIdx.x & 63)) - 1))) : IDO_RPB_MAX;
-    if (threadIdx.x == 0) s_nr = uint32_t(__popcll(kb));
-    __syncthreads();
-    nr = s_nr;
-    if (!nr) return;  // (block-uniform: no barrier follows for this block)
-  }
-  if (threadIdx.x < min(a.rpb, n_reps - r0) && slot < IDO_RPB_MAX) {
+  if (threadIdx.x < nr) {
     RepHead<KC> h;
-    h.i = a.reps[r0 + threadIdx.x];
+    h.i = rep_at(a, rlo + r0 + threadIdx.x);
     h.arow = uint32_t(arow_of(a, h.i));
     const uint32_t cn = a.cnt[h.i], ipc = a.ip_cnt[h.i];
     h.ipoff = a.ip_off[h.i];
@@ -1145,7 +1150,7 @@ __device__ __forceinline__ void class_rows_ido_blk(RowArgs a, uint32_t bid_, uin
     h.m = cn ? ipc : 0u;
 #pragma unroll
     for (int kk = 0; kk < KC; kk++) h.du[kk] = !EGRESS && k0 + kk < a.K && st[kk] == CYC_JOB_VALID ? ds[kk] : -2;
-    s_rep[slot] = h;
+    s_rep[threadIdx.x] = h;
   }
   int32_t ud[KC];  // egress UNI: the block's slots' descriptors (block-uniform)
 #pragma unroll

@@ -27,13 +27,13 @@ struct MemberArgs {
   const uint4* actrec;        // per act[] entry: (label set, namespace targets lo, hi, list offset)
   uint32_t n_act;
   uint32_t* reps;             // class representatives, act[] order within each block (k_classify)
-  uint32_t* rep_cnt;          // set to ~0 by k_member: ends at count - 1
+  uint32_t* rep_cnt;          // [0] set to ~0 by k_member: ends at count - 1 of reps[]'s head; [1] set to 0:
+                              // the count of its tail (row phases' phase-2 classes, RowArgs::phase_reps)
   const uint32_t* id_blk;     // batched blocks: each identity's block (classes never span blocks), else null
-  // row phases (cyc_ctx::row_phases): a class some identity of which has its first row of the run
-  // before `split` is a phase-1 class: need[its representative] = epoch (null: no phases)
-  uint32_t* need;
+  // row phases (cyc_ctx::row_phases): a class whose representative's first row of the run is at or
+  // after `split` is a phase-2 class, listed from the tail of reps[] (null: no phases)
   const uint32_t* first_row;  // per identity: its first pod's row in the run (cyc_ctx::arow)
-  uint32_t split, epoch;
+  uint32_t split;
 };
 
 // Entry s: words 2s (key) and 2s + 1 (low half: representative); a probe reads both in one load.
@@ -79,7 +79,7 @@ __device__ __forceinline__ void ht_elect(const MemberArgs& a, uint64_t h, uint32
 }
 
 __device__ __forceinline__ void member_blk(MemberArgs a, uint32_t bid_, uint32_t nblk_) {
-  if (bid_ == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
+  if (bid_ == 0 && threadIdx.x == 0) a.rep_cnt[0] = ~0u, a.rep_cnt[1] = 0u;  // k_classify counts up from here
   uint32_t ii = bid_ * blockDim.x + threadIdx.x;
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
@@ -133,7 +133,7 @@ __global__ void k_member(MemberArgs a) { member_blk(a, blockIdx.x, gridDim.x); }
 // per identity leaves the chip nearly idle behind a chain of dependent loads.  Same list order
 // (ascending target id = primary-key order), same hash, same representative election.
 __device__ __forceinline__ void member_wave_blk(MemberArgs a, uint32_t bid_, uint32_t nblk_) {
-  if (bid_ == 0 && threadIdx.x == 0) *a.rep_cnt = ~0u;  // k_classify counts up from here
+  if (bid_ == 0 && threadIdx.x == 0) a.rep_cnt[0] = ~0u, a.rep_cnt[1] = 0u;  // k_classify counts up from here
   const uint32_t lane = threadIdx.x & 63, ii = __builtin_amdgcn_readfirstlane(bid_ * 4 + (threadIdx.x >> 6));  // wave-uniform
   if (ii >= a.n_act) return;
   const uint32_t i = a.act[ii];
@@ -214,7 +214,7 @@ __device__ __forceinline__ uint32_t class_of_identity(uint32_t i, const uint8_t*
 }
 
 __device__ __forceinline__ void classify_blk(MemberArgs a, uint32_t* __restrict__ class_of, uint32_t bid_, uint32_t nblk_) {
-  __shared__ uint32_t wsum[4], base;
+  __shared__ uint32_t wsum[4], wsum2[4], base, base2;
   const uint32_t ii = bid_ * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool live = ii < a.n_act;
@@ -223,18 +223,22 @@ __device__ __forceinline__ void classify_blk(MemberArgs a, uint32_t* __restrict_
                                               a.id_status, a.id_desc, a.K)
                           : i;
   if (live) class_of[i] = c;
-  // (atomicMax: a stale epoch of an earlier run is only ever smaller — or, replayed by a captured graph,
-  // equal, which merely moves a class into phase 1: its row is then ready early, never late)
-  if (live && a.need && a.first_row[i] < a.split) atomicMax(a.need + c, a.epoch);
-  const bool f = live && c == i;
-  const uint64_t m = __ballot(f);
-  if (lane == 0) wsum[wv] = __popcll(m);
+  // row phases: the representative (the class's smallest identity: identities are numbered in pod
+  // order, so its first row is the class's) of a class first used at or after the split is listed from
+  // the tail, so each phase's class-row launch covers exactly its own classes
+  const bool f = live && c == i, late = f && a.first_row && a.first_row[i] >= a.split;
+  const uint64_t m = __ballot(f && !late), m2 = __ballot(late);
+  if (lane == 0) wsum[wv] = __popcll(m), wsum2[wv] = __popcll(m2);
   __syncthreads();
-  if (threadIdx.x == 0) base = atomicAdd(a.rep_cnt, wsum[0] + wsum[1] + wsum[2] + wsum[3]) + 1u;
+  if (threadIdx.x == 0) {
+    base = atomicAdd(a.rep_cnt, wsum[0] + wsum[1] + wsum[2] + wsum[3]) + 1u;
+    if (a.first_row) base2 = atomicAdd(a.rep_cnt + 1, wsum2[0] + wsum2[1] + wsum2[2] + wsum2[3]);
+  }
   __syncthreads();
-  uint32_t off = base;
-  for (uint32_t x = 0; x < wv; x++) off += wsum[x];
-  if (f) a.reps[off + __popcll(m & ((1ull << lane) - 1))] = i;
+  uint32_t off = base, off2 = base2;
+  for (uint32_t x = 0; x < wv; x++) off += wsum[x], off2 += wsum2[x];
+  if (f && !late) a.reps[off + __popcll(m & ((1ull << lane) - 1))] = i;
+  if (late) a.reps[a.n_ident - 1u - (off2 + __popcll(m2 & ((1ull << lane) - 1)))] = i;
 }
 __global__ __launch_bounds__(256) void k_classify(MemberArgs a, uint32_t* __restrict__ class_of) { classify_blk(a, class_of, blockIdx.x, gridDim.x); }
 

@@ -600,9 +600,9 @@ int cyc_last_classes(cyc_ctx* c, int64_t* out, int n) {
     // the next step's first launch ~4.5 us (config #2: 0.0640 -> 0.0598 ms per step without it, r05at)
     HIPCHK(hipStreamSynchronize(c->last_stream));
     for (int d = 0; d < 2; d++) {
-      uint32_t v = 0xFFFFFFFFu;
-      if (c->dir[d].n && c->n_act[d]) HIPCHK(hipMemcpy(&v, c->dir[d].rep_cnt(), 4, hipMemcpyDeviceToHost));
-      out[d] = int64_t(uint32_t(v + 1u));
+      uint32_t v[2] = {0xFFFFFFFFu, 0u};  // reps[]'s head (count - 1) and tail (row phases' phase-2 classes)
+      if (c->dir[d].n && c->n_act[d]) HIPCHK(hipMemcpy(v, c->dir[d].rep_cnt(), 8, hipMemcpyDeviceToHost));
+      out[d] = int64_t(uint32_t(v[0] + 1u)) + int64_t(v[1]);
     }
     return (int)CYC_OK;
   });

@@ -641,18 +641,15 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   size_t lds = 0, lds_uni = 0, e_per[2] = {0, 0};
   uint32_t e_na[2] = {0, 0};
   // row phases: the class rows in two launches with phase 1's emit between them (the caller's mid)
-  const bool phases = c->phase_split && mid && c->need[0].p && c->need[1].p;
+  const bool phases = c->phase_split && mid;
   c->phase_used = phases ? 2 : 0;
-  if (phases) c->run_epoch = c->run_epoch + 1 ? c->run_epoch + 1 : 1;
   for (int d = 0; d < 2; d++) {
     const uint32_t na = c->dir[d].n ? c->n_act[d] : 0u;
     fb.ma[d] = member_args(c, d);
     fc.ma[d] = fb.ma[d];
-    if (phases) {  // the class election marks the classes phase 1's rows use
-      fc.ma[d].need = c->need[d].as<uint32_t>();
+    if (phases) {  // the class election lists phase 2's classes apart (from the tail of reps[])
       fc.ma[d].first_row = c->arow[d].as<uint32_t>();
       fc.ma[d].split = c->phase_split;
-      fc.ma[d].epoch = c->run_epoch;
     }
     fc.class_of[d] = c->dir[d].class_of.as<uint32_t>();
     fb.member_wave[d] = c->member_wave > 0 || (c->member_wave < 0 && na <= 4096 && c->act_targets[d] >= 4.0);
@@ -748,8 +745,6 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   auto class_rows = [&](uint32_t phase) {
     for (int d = 0; d < 2; d++) {
       RowArgs& ra = ido ? fe.ra[d] : fd.ra[d];
-      ra.need = c->need[d].as<uint32_t>();
-      ra.epoch = c->run_epoch;
       ra.phase = phase;
     }
     if (!ido) {

@@ -647,10 +647,6 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
       return i1[x] != i1[y] ? i1[x] < i1[y] : i2[x] < i2[y];
     });
     c->phase_n1[d] = split ? split - uint32_t(c->rl[d]) : 0u;
-    if (split && c->need[d].bytes < std::max<uint64_t>(c->ids[d].ns.size(), 1) * 4) {
-      c->need[d].alloc(std::max<uint64_t>(c->ids[d].ns.size(), 1) * 4);
-      HIPCHK(hipMemset(c->need[d].p, 0, c->need[d].bytes));
-    }
     std::vector<uint32_t> pairs(ord.size() * 2);
     for (size_t r = 0; r < ord.size(); r++) {
       pairs[2 * r] = ord[r];
