@@ -493,7 +493,7 @@ def test_ip_pod_interval_rows(gpu, seed, wide):
 def test_row_phases(gpu, seed):
     """A whole table whose class rows and emit run in two row phases (the classes rows [0, P/2) use, the
     emit of those rows, then the other classes and the emit of rows [P/2, P)) equals the single pass,
-    through every launch mode (graph replays included: a replay's epoch is the captured one), on
+    through every launch mode (graph replays included: the election re-lists each replay's phases), on
     target and whole-range source runs, for identity-set and materialised-row (PM) builds."""
     pols, res, probes = random_problem(91_000 + seed, n_pods=300 + 97 * seed, n_pols=10 + 3 * seed)
     eng = Engine(0).build_policies(pols).load_resources(res)
