@@ -501,6 +501,7 @@ def test_row_phases(gpu, seed):
     if eng.shape["may_panic"]:
         pytest.skip("a build that may panic never splits")
     want = eng.run_host()
+    want_classes = eng.classes()
     assert eng.get_option("row_phases_active") == 0  # (auto: only from 8 GB planes up)
     eng.set_option("row_phases", 2)
     for pod_words in (-1, 0):
@@ -513,6 +514,8 @@ def test_row_phases(gpu, seed):
                     if eng.get_option("front_fused_active"):
                         assert eng.get_option("row_phases_active") == 2
                         assert eng.last_emit()[1] == 2, eng.last_emit()
+                        # both phases' representative lists (head and tail) hold every class once
+                        assert eng.classes() == want_classes, (eng.classes(), want_classes)
                     for name, a, b in zip(("status", "ingress", "egress"), want, got):
                         assert np.array_equal(a, b), (f"seed {seed} pod_words {pod_words} graphs {graphs} {part} rep {rep}: "
                                                       f"{name} differs")
