@@ -169,6 +169,8 @@ struct cyc_ctx {
   DevBuf act[2], actrec[2], sel_list;
   DevBuf arow[2];  // per identity: its first pod's row in the run's row range (in-place class rows)
   uint32_t n_act[2] = {0, 0}, n_sel = 0;
+  uint32_t n_act_ph1[2] = {0, 0};  // row phases: active identities whose first row is before the split (every
+                                   // phase-1 class's representative is one of them)
   double act_targets[2] = {0, 0};  // mean namespace targets per active identity (range plan)
   // Diagnostic path selectors (cyc_set_option; results never change, the GPU tests force each path):
   int use_graphs = -1;  // "graphs": 1 = graph replay, 2 = the same DAG enqueued eagerly on three

@@ -157,6 +157,9 @@ static void enq_member(cyc_ctx* c, int d, hipStream_t st, bool clear = true) {
   k_classify<<<grid1(c->n_act[d], 256), 256, 0, st>>>(ma, dd.class_of.as<uint32_t>());
 }
 
+#ifndef CYC_PHASE_GRID
+#define CYC_PHASE_GRID 1  // row phases: each class-row launch's grid sized by its phase's identities (0: all)
+#endif
 #ifndef CYC_PB_REC
 #define CYC_PB_REC 1  // identity-set waves read their rows' matcher records (pb_rec); 0: the peers' chains
 #endif
@@ -742,10 +745,22 @@ static bool enq_front_fused(cyc_ctx* c, hipStream_t st, hipEvent_t ev_front = nu
   if (gc) k_front_c<<<unsigned(gc), 256, 0, st>>>(fc);
   if (ev_front) HIPCHK(hipEventRecord(ev_front, st));  // eager runs: phase timings
   // the class rows: once, or per row phase with phase 1's emit between (the caller's mid)
+  // a phased launch's grid covers only the identities that can represent its phase's classes (the
+  // representatives' first rows decide the phase), not every active identity
+  const uint32_t fd_all[2] = {fd.nb[0], fd.nb[1]}, fe_all[2] = {fe.nb[0], fe.nb[1]};
   auto class_rows = [&](uint32_t phase) {
     for (int d = 0; d < 2; d++) {
       RowArgs& ra = ido ? fe.ra[d] : fd.ra[d];
       ra.phase = phase;
+      if (!CYC_PHASE_GRID || !phase) continue;
+      const uint32_t na = c->dir[d].n ? c->n_act[d] : 0u;
+      const uint32_t nph = phase == 1 ? c->n_act_ph1[d] : na - c->n_act_ph1[d];
+      if (ido) {
+        if (fe_all[d]) fe.nb[d] = blocks(uint64_t(ido_chunk_groups(fe.ra[d].WA)) * ((K + E_KC - 1) / E_KC) *
+                                         ((nph + fe.ra[d].rpb - 1) / fe.ra[d].rpb));
+      } else if (fd_all[d]) {
+        fd.nb[d] = std::min(fd_all[d], nph);
+      }
     }
     if (!ido) {
       const unsigned gd = fd.nb[0] + fd.nb[1];

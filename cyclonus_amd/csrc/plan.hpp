@@ -674,6 +674,9 @@ static void ensure_range(cyc_ctx* c, int64_t lo, int64_t hi, bool src = false) {
       std::vector<uint32_t> ar(I.ns.size(), 0xFFFFFFFFu);
       for (int64_t p = c->rh[d] - 1; p >= c->rl[d]; p--) ar[I.of_pod[size_t(p)]] = uint32_t(p - c->rl[d]);
       upload(c->arow[d], ar);
+      c->n_act_ph1[d] = 0;  // (row phases: the phase-1 launch's representatives are among these)
+      for (uint32_t i : act)
+        if (c->phase_split && ar[i] < c->phase_split) c->n_act_ph1[d]++;
     }
     std::vector<uint8_t> ns_needed(pb.strings.size(), 0);
     for (uint32_t i : act) ns_needed[I.ns[i]] = 1;
