@@ -177,12 +177,31 @@ __device__ __forceinline__ uint32_t class_of_identity(uint32_t i, const uint8_t*
                                                       const uint32_t* __restrict__ list, const uint32_t* __restrict__ id_blk,
                                                       const uint8_t* __restrict__ id_status, const int32_t* __restrict__ id_desc,
                                                       uint32_t K) {
-  if (err[i]) return i;
-  const uint32_t r0 = ht_find_rep(ht_key, ht_cap, hash[i]);
+  // identity i's own fields in one round trip with its hash (none depends on the representative); then,
+  // once the representative is known, its fields and the first 8 job slots of both in one more, and its
+  // list entries (they need its list offset) in the last: three round trips after the probe for the
+  // usual short lists and K <= 8, where the batches below took five
+  const uint8_t ei = err[i];
+  const uint64_t hi = hash[i];
+  const uint32_t n = cnt[i], oi = list_off[i], bi = id_blk ? id_blk[i] : 0u;
+  if (ei) return i;
+  const uint32_t r0 = ht_find_rep(ht_key, ht_cap, hi);
   const uint32_t r = r0 == 0xFFFFFFFFu ? i : r0;
   if (r == i) return i;
-  const uint32_t n = cnt[i], oi = list_off[i], orr = list_off[r];
-  bool eq = cnt[r] == n && (!id_blk || id_blk[r] == id_blk[i]);
+  const uint32_t nr = cnt[r], orr = list_off[r], br = id_blk ? id_blk[r] : 0u;
+  uint8_t si[8], sr[8];
+  int32_t di[8], dr[8];
+  if (id_desc && K) {
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) {
+      const uint64_t k = min(u, K - 1);
+      si[u] = id_status[uint64_t(i) * K + k];
+      sr[u] = id_status[uint64_t(r) * K + k];
+      di[u] = id_desc[uint64_t(i) * K + k];
+      dr[u] = id_desc[uint64_t(r) * K + k];
+    }
+  }
+  bool eq = nr == n && br == bi;
   for (uint32_t j0 = 0; eq && j0 < n; j0 += 8) {
     uint32_t x[8], y[8];
 #pragma unroll
@@ -196,15 +215,15 @@ __device__ __forceinline__ uint32_t class_of_identity(uint32_t i, const uint8_t*
   }
   if (eq && id_desc) {
     for (uint32_t k0 = 0; eq && k0 < K; k0 += 8) {
-      uint8_t si[8], sr[8];
-      int32_t di[8], dr[8];
+      if (k0) {
 #pragma unroll
-      for (uint32_t u = 0; u < 8; u++) {
-        const uint64_t k = min(k0 + u, K - 1);
-        si[u] = id_status[uint64_t(i) * K + k];
-        sr[u] = id_status[uint64_t(r) * K + k];
-        di[u] = id_desc[uint64_t(i) * K + k];
-        dr[u] = id_desc[uint64_t(r) * K + k];
+        for (uint32_t u = 0; u < 8; u++) {
+          const uint64_t k = min(k0 + u, K - 1);
+          si[u] = id_status[uint64_t(i) * K + k];
+          sr[u] = id_status[uint64_t(r) * K + k];
+          di[u] = id_desc[uint64_t(i) * K + k];
+          dr[u] = id_desc[uint64_t(r) * K + k];
+        }
       }
 #pragma unroll
       for (uint32_t u = 0; u < 8; u++) eq = eq && si[u] == sr[u] && (si[u] != CYC_JOB_VALID || di[u] == dr[u]);
